@@ -1,0 +1,139 @@
+/*
+ * neptune_lp.h — C ABI of the MI355X (gfx950) batched LP-relaxation engine for NEPTUNE's
+ * node x function placement/routing MIP.
+ *
+ * What this replaces.  The reference hands the whole MIP to OR-Tools/SCIP through pywraplp:
+ *   core/solvers/solver.py:7      pywraplp.Solver.CreateSolver('SCIP')        -> nep_model_create
+ *   core/solvers/solver.py:15-20  load_data -> init_vars / init_constraints   -> nep_model_desc
+ *   core/solvers/solver.py:35-40  init_objective(); Solver.Solve(); status == OPTIMAL
+ *                                 (SCIP solves one LP relaxation per B&B node) -> nep_lp_solve_batch
+ *   core/solvers/solver.py:45-46  score() = Objective().Value()               -> obj / primal_obj
+ *   neptune/utils/output.py:5-21  x[i,f,j].solution_value(), c[f,j], n[j]     -> nep_lp_get_solution
+ * The model rows/columns are exactly those of neptune/utils/variables.py, constraints_step1.py,
+ * constraints_step2.py and objectives.py (see DESIGN.md §2 for the row-by-row map).
+ *
+ * Conventions.  Plain pointers and sizes only.  Every call returns NEP_OK (0) on success or a
+ * negative NEP_ERR_*; nep_last_error() gives a thread-local message.  Host arrays are read during
+ * the call only.  The library owns all device workspaces; one model serves `max_batch` LP slots
+ * (B&B nodes) that can be warm-started from each other.  All device work of a model is ordered on
+ * one HIP stream; the HIP context is created on first use (safe after fork()).
+ *
+ * Integer-variable vector ("z_int"), in the reference's variable-creation order minus x:
+ *   step 1: c[F*N] (f-major), then n[N] (MinUtilization / MinDelayAndUtilization only)
+ *   step 2: c[F*N], moved_from[F*N], moved_to[F*N], allocated, deallocated, then n[N] (MU / MDU)
+ */
+#ifndef NEPTUNE_LP_H
+#define NEPTUNE_LP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NEP_API_VERSION 1
+
+/* variants: neptune.py:41-66 (NeptuneMinDelay / MinUtilization / MinDelayAndUtilization) */
+enum { NEP_MIN_DELAY = 0, NEP_MIN_UTILIZATION = 1, NEP_MIN_DELAY_AND_UTILIZATION = 2 };
+/* steps: neptune_step1.py (step 1), neptune_step2.py mode="delete" / "create" */
+enum { NEP_STEP1 = 1, NEP_STEP2_DELETE = 2, NEP_STEP2_CREATE = 3 };
+
+enum { NEP_OK = 0, NEP_ERR_ARG = -1, NEP_ERR_HIP = -2, NEP_ERR_NOMEM = -3, NEP_ERR_STATE = -4 };
+
+/* per-LP status */
+enum {
+  NEP_LP_OPTIMAL = 0,          /* certified: gap(primal obj, Lagrangian bound) and residuals <= tol */
+  NEP_LP_ITERATION_LIMIT = 1,  /* obj still holds a VALID lower bound (Lagrangian) */
+  NEP_LP_INFEASIBLE = 2,       /* proven by presolve (empty routing row, crossed bounds) */
+  NEP_LP_CUTOFF = 3,           /* Lagrangian bound exceeded opts.cutoff: node can be pruned */
+  NEP_LP_NUMERICAL = 4
+};
+
+typedef struct {
+  int32_t n_nodes;             /* N */
+  int32_t n_functions;         /* F */
+  int32_t variant;             /* NEP_MIN_* */
+  int32_t step;                /* NEP_STEP1 / NEP_STEP2_DELETE / NEP_STEP2_CREATE */
+  double alpha;                /* neptune_step1.py:68 (default 0.5) */
+  double soften_step1_sol;     /* neptune_step2.py:6 (default 1.3) */
+  double max_score;            /* step 2: step-1 objective (neptune.py:22) */
+  double prev_network_delay;   /* step 2 MinDelay: sum D[i,j] W[f,i] prev_x[i,f,j] (constraints_step2.py:66-68) */
+  double big_m;                /* constraints_step1.py:1 (1e6) */
+  double epsilon;              /* constraints_step1.py:2 (1e-6) */
+  const double *delay;         /* [N*N] node_delay_matrix D[i][j] */
+  const double *workload;      /* [F*N] workload_matrix W[f][i] (already * workload_coeff) */
+  const double *core_per_req;  /* [F*N] core_per_req_matrix cpr[f][j] */
+  const double *function_memory; /* [F] */
+  const double *node_memory;   /* [N] */
+  const double *node_cores;    /* [N] */
+  const double *node_cost;     /* [N] (input_to_data.py:186: 5) */
+  double node_budget;          /* (input_to_data.py:187: 300) */
+  const double *max_delay;     /* [F] max_delay_matrix (input_to_data.py:136: 1000) */
+  const double *old_allocations; /* [F*N] step 2 only (0/1) */
+} nep_model_desc;
+
+typedef struct {
+  double tol;                  /* certified relative tolerance (default 1e-7) */
+  double cutoff;               /* stop when the Lagrangian bound exceeds this (default +inf) */
+  int64_t max_iters;           /* default 200000 */
+  int32_t check_every;         /* PDHG iterations between certificate checks (default 64) */
+  int32_t warm_start;          /* 1: continue from the slot's current state (after nep_lp_copy_state) */
+} nep_lp_opts;
+
+typedef struct {
+  int32_t n_int;               /* length of z_int */
+  int32_t n_rows;              /* R: routing rows after exact zero-workload source aggregation */
+  int32_t n_tiles;             /* x-pass workgroups per LP */
+  int32_t max_batch;
+  int64_t x_entries;           /* R*N per LP */
+  int64_t bytes_per_iter;      /* algorithmic HBM bytes of one PDHG iteration of one LP */
+  double step_size;            /* eta = 0.95 / ||K||_2 (scaled) */
+} nep_model_info;
+
+typedef struct {
+  int64_t x_pass_launches;     /* launches of the fused routing-row kernel */
+  double x_pass_ms;            /* summed HIP-event duration of the sampled x-pass launches */
+  int64_t x_pass_sampled;      /* number of sampled launches in x_pass_ms */
+  int64_t x_pass_lp_iters;     /* LP-iterations carried by the sampled launches */
+  double solve_ms;             /* wall time inside nep_lp_solve_batch (device-synchronised) */
+  int64_t lp_iterations;       /* PDHG iterations summed over LPs */
+} nep_stats;
+
+int nep_model_create(const nep_model_desc *desc, int32_t max_batch, void *hip_stream, void **out_model);
+void nep_model_destroy(void *model);
+int nep_model_get_info(void *model, nep_model_info *info);
+
+/* Solve B node LPs in slots[0..B-1].  lb_int/ub_int: host [B][n_int] bounds on z_int (branching
+ * fixings; pass NULL for the root bounds).  Outputs (host, length B): obj = certified LP value
+ * (Lagrangian lower bound), primal_obj = objective of the primal iterate, status, iters. */
+int nep_lp_solve_batch(void *model, int32_t B, const int32_t *slots, const double *lb_int, const double *ub_int,
+                       const nep_lp_opts *opts, double *obj, double *primal_obj, int32_t *status, int64_t *iters);
+
+/* z_int (host, n_int) and optionally the dense routing x[i][f][j] (host float, N*F*N) of a slot. */
+int nep_lp_get_solution(void *model, int32_t slot, double *z_int, float *x_dense);
+/* aggregated routing rows (host float, R*N) and the row map (row_f, row_src; src = -1: pooled
+ * zero-workload sources of function f, each routed identically). */
+int nep_lp_get_rows(void *model, int32_t slot, float *xbar, int32_t *row_f, int32_t *row_src);
+int nep_lp_copy_state(void *model, int32_t src_slot, int32_t dst_slot);
+
+int nep_get_stats(void *model, nep_stats *stats);
+
+/* diagnostics: out16 = {primal obj, Lagrangian, best Lagrangian, primal residual, gap, omega, tau,
+ * sigma, eta, iterations, iterations since restart, status, active, fpr at restart, last fpr, ||K||} */
+int nep_lp_get_diag(void *model, int32_t slot, double *out16);
+/* device state of a slot (any pointer may be NULL): duals [n_dual], row activities [n_dual],
+ * packed f32 duals of the x pass [F*NP+NP+4], node bounds [n_int] */
+int nep_debug_state(void *model, int32_t slot, double *y, double *kz, float *kty, double *lb, double *ub);
+/* host-only model build (no device work): step size, scalings, row norms, dims = {R, tiles, n_int,
+ * n_dual}.  Lets the CPU test-suite check the model build without a GPU. */
+int nep_debug_build(const nep_model_desc *desc, double *eta, double *rho, double *gam, double *rownorm,
+                    int32_t *dims);
+void nep_reset_stats(void *model);
+
+const char *nep_last_error(void);
+int nep_api_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,244 @@
+"""ctypes binding of the MI355X LP engine (`include/neptune_lp.h`, lib/libneptune_lp.so).
+
+This is the product path: there is no CPU fallback.  If the shared library is missing (not built)
+or no GPU is visible, every call raises `EngineUnavailable` loudly.
+"""
+import ctypes
+import math
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("NEPTUNE_LP_LIB",
+                          os.path.normpath(os.path.join(_HERE, "..", "..", "lib", "libneptune_lp.so")))
+
+MIN_DELAY, MIN_UTILIZATION, MIN_DELAY_AND_UTILIZATION = 0, 1, 2
+STEP1, STEP2_DELETE, STEP2_CREATE = 1, 2, 3
+LP_OPTIMAL, LP_ITERATION_LIMIT, LP_INFEASIBLE, LP_CUTOFF, LP_NUMERICAL = 0, 1, 2, 3, 4
+VARIANTS = {"MinDelay": MIN_DELAY, "MinUtilization": MIN_UTILIZATION,
+            "MinDelayAndUtilization": MIN_DELAY_AND_UTILIZATION}
+
+_dp = ctypes.POINTER(ctypes.c_double)
+
+
+class EngineUnavailable(RuntimeError):
+    pass
+
+
+class ModelDesc(ctypes.Structure):
+    _fields_ = [("n_nodes", ctypes.c_int32), ("n_functions", ctypes.c_int32), ("variant", ctypes.c_int32),
+                ("step", ctypes.c_int32), ("alpha", ctypes.c_double), ("soften_step1_sol", ctypes.c_double),
+                ("max_score", ctypes.c_double), ("prev_network_delay", ctypes.c_double),
+                ("big_m", ctypes.c_double), ("epsilon", ctypes.c_double),
+                ("delay", _dp), ("workload", _dp), ("core_per_req", _dp), ("function_memory", _dp),
+                ("node_memory", _dp), ("node_cores", _dp), ("node_cost", _dp), ("node_budget", ctypes.c_double),
+                ("max_delay", _dp), ("old_allocations", _dp)]
+
+
+class LpOpts(ctypes.Structure):
+    _fields_ = [("tol", ctypes.c_double), ("cutoff", ctypes.c_double), ("max_iters", ctypes.c_int64),
+                ("check_every", ctypes.c_int32), ("warm_start", ctypes.c_int32)]
+
+
+class ModelInfo(ctypes.Structure):
+    _fields_ = [("n_int", ctypes.c_int32), ("n_rows", ctypes.c_int32), ("n_tiles", ctypes.c_int32),
+                ("max_batch", ctypes.c_int32), ("x_entries", ctypes.c_int64), ("bytes_per_iter", ctypes.c_int64),
+                ("step_size", ctypes.c_double)]
+
+
+class Stats(ctypes.Structure):
+    _fields_ = [("x_pass_launches", ctypes.c_int64), ("x_pass_ms", ctypes.c_double),
+                ("x_pass_sampled", ctypes.c_int64), ("x_pass_lp_iters", ctypes.c_int64),
+                ("solve_ms", ctypes.c_double), ("lp_iterations", ctypes.c_int64)]
+
+
+# every entry point declared in include/neptune_lp.h
+EXPORTS = ("nep_model_create", "nep_model_destroy", "nep_model_get_info", "nep_lp_solve_batch",
+           "nep_lp_get_solution", "nep_lp_get_rows", "nep_lp_copy_state", "nep_get_stats", "nep_reset_stats",
+           "nep_last_error", "nep_api_version", "nep_lp_get_diag", "nep_debug_build", "nep_debug_state")
+
+_lib = None
+
+
+def load_library(path=None):
+    """Load (once) and type the shared library.  Raises EngineUnavailable when absent."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise EngineUnavailable(f"MI355X LP engine not built: {p} missing (run __graft_entry__.build())")
+    lib = ctypes.CDLL(p)
+    vp, i32, i64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64
+    lib.nep_model_create.argtypes = [ctypes.POINTER(ModelDesc), i32, vp, ctypes.POINTER(vp)]
+    lib.nep_model_destroy.argtypes = [vp]
+    lib.nep_model_destroy.restype = None
+    lib.nep_model_get_info.argtypes = [vp, ctypes.POINTER(ModelInfo)]
+    lib.nep_lp_solve_batch.argtypes = [vp, i32, ctypes.POINTER(i32), _dp, _dp, ctypes.POINTER(LpOpts), _dp, _dp,
+                                       ctypes.POINTER(i32), ctypes.POINTER(i64)]
+    lib.nep_lp_get_solution.argtypes = [vp, i32, _dp, ctypes.POINTER(ctypes.c_float)]
+    lib.nep_lp_get_rows.argtypes = [vp, i32, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(i32),
+                                    ctypes.POINTER(i32)]
+    lib.nep_lp_copy_state.argtypes = [vp, i32, i32]
+    lib.nep_get_stats.argtypes = [vp, ctypes.POINTER(Stats)]
+    lib.nep_reset_stats.argtypes = [vp]
+    lib.nep_reset_stats.restype = None
+    lib.nep_lp_get_diag.argtypes = [vp, i32, _dp]
+    lib.nep_debug_build.argtypes = [ctypes.POINTER(ModelDesc), _dp, _dp, _dp, _dp, ctypes.POINTER(i32)]
+    lib.nep_debug_state.argtypes = [vp, i32, _dp, _dp, ctypes.POINTER(ctypes.c_float), _dp, _dp]
+    lib.nep_last_error.restype = ctypes.c_char_p
+    lib.nep_api_version.restype = ctypes.c_int
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def _ptr(a, ctype=ctypes.c_double):
+    return None if a is None else a.ctypes.data_as(ctypes.POINTER(ctype))
+
+
+def _check(lib, rc, what):
+    if rc != 0:
+        raise EngineUnavailable(f"{what} failed ({rc}): {lib.nep_last_error().decode()}")
+
+
+def _arrays(data, N, F):
+    f64 = lambda a: np.ascontiguousarray(np.asarray(a, dtype=np.float64))
+    return dict(
+        delay=f64(data.node_delay_matrix).reshape(N, N),
+        workload=f64(data.workload_matrix).reshape(F, N),
+        cpr=f64(data.core_per_req_matrix).reshape(F, N),
+        fmem=f64(data.function_memory_matrix).reshape(F),
+        nmem=f64(data.node_memory_matrix).reshape(N),
+        ncores=f64(data.node_cores_matrix).reshape(N),
+        ncost=f64(data.node_costs).reshape(N),
+        maxd=f64(data.max_delay_matrix).reshape(F),
+        old=f64(data.old_allocations_matrix).reshape(F, N),
+    )
+
+
+def _desc(k, N, F, variant, step, alpha, soften, max_score, prev_delay, budget):
+    return ModelDesc(N, F, variant, step, float(alpha), float(soften), float(max_score), float(prev_delay), 1e6,
+                     1e-6, _ptr(k["delay"]), _ptr(k["workload"]), _ptr(k["cpr"]), _ptr(k["fmem"]), _ptr(k["nmem"]),
+                     _ptr(k["ncores"]), _ptr(k["ncost"]), float(budget), _ptr(k["maxd"]), _ptr(k["old"]))
+
+
+def debug_build(data, variant, step=STEP1, alpha=0.5, soften_step1_sol=1.3, max_score=0.0, prev_network_delay=0.0):
+    """Host-only model build (no GPU needed): returns eta, rho, gam, rownorm, dims."""
+    lib = load_library()
+    N, F = len(data.nodes), len(data.functions)
+    v = VARIANTS[variant] if isinstance(variant, str) else int(variant)
+    k = _arrays(data, N, F)
+    d = _desc(k, N, F, v, int(step), alpha, soften_step1_sol, max_score, prev_network_delay, data.node_budget)
+    dims = np.zeros(4, np.int32)
+    eta = np.zeros(1)
+    _check(lib, lib.nep_debug_build(ctypes.byref(d), _ptr(eta), None, None, None, _ptr(dims, ctypes.c_int32)),
+           "nep_debug_build")
+    R, T, n_int, n_dual = dims.tolist()
+    rho, gam, rn = np.zeros(n_dual), np.zeros(n_int), np.zeros(n_dual)
+    _check(lib, lib.nep_debug_build(ctypes.byref(d), _ptr(eta), _ptr(rho), _ptr(gam), _ptr(rn), None),
+           "nep_debug_build")
+    return {"eta": float(eta[0]), "rho": rho, "gam": gam, "rownorm": rn, "R": R, "T": T, "n_int": n_int,
+            "n_dual": n_dual}
+
+
+class LPModel:
+    """One structured LP family (a reference step model) with `max_batch` device slots."""
+
+    def __init__(self, data, variant, step=STEP1, alpha=0.5, soften_step1_sol=1.3, max_score=0.0,
+                 prev_network_delay=0.0, max_batch=1):
+        self._lib = load_library()
+        self.N = len(data.nodes)
+        self.F = len(data.functions)
+        self.variant = VARIANTS[variant] if isinstance(variant, str) else int(variant)
+        self.step = int(step)
+        self._keep = _arrays(data, self.N, self.F)
+        d = _desc(self._keep, self.N, self.F, self.variant, self.step, alpha, soften_step1_sol, max_score,
+                  prev_network_delay, data.node_budget)
+        h = ctypes.c_void_p()
+        _check(self._lib, self._lib.nep_model_create(ctypes.byref(d), int(max_batch), None, ctypes.byref(h)),
+               "nep_model_create")
+        self._h = h
+        info = ModelInfo()
+        _check(self._lib, self._lib.nep_model_get_info(self._h, ctypes.byref(info)), "nep_model_get_info")
+        self.info = info
+        self.n_int = info.n_int
+        self.max_batch = info.max_batch
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.nep_model_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def solve(self, slots, lb=None, ub=None, tol=1e-7, cutoff=math.inf, max_iters=200000, check_every=64,
+              warm_start=False):
+        """Solve len(slots) node LPs.  lb/ub: [B, n_int] bounds on the integer vector (None = root).
+        Returns dict of numpy arrays: obj (certified LP value = Lagrangian bound), primal_obj, status, iters."""
+        slots = np.ascontiguousarray(np.asarray(slots, dtype=np.int32).reshape(-1))
+        B = len(slots)
+        lbp = None if lb is None else np.ascontiguousarray(np.asarray(lb, np.float64).reshape(B, self.n_int))
+        ubp = None if ub is None else np.ascontiguousarray(np.asarray(ub, np.float64).reshape(B, self.n_int))
+        obj = np.zeros(B)
+        pobj = np.zeros(B)
+        status = np.zeros(B, np.int32)
+        iters = np.zeros(B, np.int64)
+        opts = LpOpts(float(tol), float(cutoff), int(max_iters), int(check_every), 1 if warm_start else 0)
+        _check(self._lib, self._lib.nep_lp_solve_batch(
+            self._h, B, _ptr(slots, ctypes.c_int32), _ptr(lbp), _ptr(ubp), ctypes.byref(opts), _ptr(obj), _ptr(pobj),
+            _ptr(status, ctypes.c_int32), _ptr(iters, ctypes.c_int64)), "nep_lp_solve_batch")
+        return {"obj": obj, "primal_obj": pobj, "status": status, "iters": iters}
+
+    def solution(self, slot, dense_x=True):
+        z = np.zeros(self.n_int)
+        x = np.zeros((self.N, self.F, self.N), np.float32) if dense_x else None
+        _check(self._lib, self._lib.nep_lp_get_solution(self._h, int(slot), _ptr(z),
+                                                        _ptr(x, ctypes.c_float) if dense_x else None),
+               "nep_lp_get_solution")
+        return z, x
+
+    def rows(self, slot):
+        R = self.info.n_rows
+        xb = np.zeros((R, self.N), np.float32)
+        rf = np.zeros(R, np.int32)
+        rs = np.zeros(R, np.int32)
+        _check(self._lib, self._lib.nep_lp_get_rows(self._h, int(slot), _ptr(xb, ctypes.c_float),
+                                                    _ptr(rf, ctypes.c_int32), _ptr(rs, ctypes.c_int32)),
+               "nep_lp_get_rows")
+        return xb, rf, rs
+
+    DIAG = ("pobj", "lagr", "best_lagr", "pres", "gap", "omega", "tau", "sigma", "eta", "k", "k_since_restart",
+            "status", "active", "restart_fpr", "last_fpr", "sigma_max")
+
+    def diag(self, slot):
+        out = np.zeros(16)
+        _check(self._lib, self._lib.nep_lp_get_diag(self._h, int(slot), _ptr(out)), "nep_lp_get_diag")
+        return dict(zip(self.DIAG, out.tolist()))
+
+    def copy_state(self, src, dst):
+        _check(self._lib, self._lib.nep_lp_copy_state(self._h, int(src), int(dst)), "nep_lp_copy_state")
+
+    def stats(self):
+        s = Stats()
+        _check(self._lib, self._lib.nep_get_stats(self._h, ctypes.byref(s)), "nep_get_stats")
+        return {k: getattr(s, k) for k, _ in Stats._fields_}
+
+    def reset_stats(self):
+        self._lib.nep_reset_stats(self._h)
+
+    # integer-vector layout helpers (include/neptune_lp.h)
+    def layout(self):
+        FN, N = self.F * self.N, self.N
+        has_n = self.variant != MIN_DELAY
+        if self.step == STEP1:
+            return {"c": (0, FN), "n": (FN, FN + N) if has_n else None}
+        out = {"c": (0, FN), "moved_from": (FN, 2 * FN), "moved_to": (2 * FN, 3 * FN),
+               "allocated": (3 * FN, 3 * FN + 1), "deallocated": (3 * FN + 1, 3 * FN + 2)}
+        out["n"] = (3 * FN + 2, 3 * FN + 2 + N) if has_n else None
+        return out

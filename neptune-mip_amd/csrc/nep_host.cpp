@@ -1,0 +1,836 @@
+// nep_host.cpp — host runtime of the NEPTUNE LP engine: model build (exact zero-workload
+// aggregation, coefficients, diagonal scaling, step size), per-node presolve, the batched PDHG
+// solve loop on one HIP stream, solution export, and the extern "C" ABI of include/neptune_lp.h.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <limits>
+#include <memory>
+#include <random>
+#include <string>
+#include <vector>
+
+#include "../../include/neptune_lp.h"
+#include "nep_internal.h"
+
+namespace nep {
+hipError_t launch_x_pass(const DeviceView &v, const int32_t *slots, int nslots, bool check, bool init, bool first,
+                         hipStream_t s);
+hipError_t launch_small_passes(const DeviceView &v, const int32_t *slots, int nslots, bool check, bool init,
+                               bool first, hipStream_t s);
+hipError_t launch_scalar_pass(const DeviceView &v, const int32_t *slots, int nslots, bool check, bool init,
+                              bool first, int iters_done, hipStream_t s);
+hipError_t launch_init_slot(const DeviceView &v, const int32_t *slots, int nslots, bool warm, double eta,
+                            hipStream_t s);
+}  // namespace nep
+
+using namespace nep;
+
+static thread_local std::string g_err;
+static int fail(int code, const std::string &msg) {
+  g_err = msg;
+  return code;
+}
+#define HIPCHK(expr)                                                                         \
+  do {                                                                                       \
+    hipError_t _e = (expr);                                                                  \
+    if (_e != hipSuccess) return fail(NEP_ERR_HIP, std::string(#expr ": ") + hipGetErrorString(_e)); \
+  } while (0)
+
+static const double INF = std::numeric_limits<double>::infinity();
+
+namespace {
+
+struct Coo {
+  std::vector<int> r, c;
+  std::vector<double> v;
+  void add(int row, int col, double val) {
+    r.push_back(row);
+    c.push_back(col);
+    v.push_back(val);
+  }
+};
+
+struct Model {
+  // problem
+  int N = 0, F = 0, NP = 0, variant = 0, step = 1, has_n = 0, step2 = 0;
+  double alpha = 0.5, M = 1e6, eps = 1e-6, sigma4 = -1, cost_n = 0, score_n_coef = 0, w_dis = 0;
+  int R = 0, T = 0, JB = 0, FB = 0, FPB = 8, CPL = 1, max_batch = 1;
+  DualLayout dl{};
+  IntLayout il{};
+  std::vector<int> row_f, row_src, tile_row0, tile_nrows, tile_f, ftile_ptr;
+  std::vector<float> row_m, row_w, row_wobj, row_wsc;
+  std::vector<double> W;            // [F*N]
+  std::vector<double> nat_lb, nat_ub, cost_int;
+  std::vector<double> lo, hi, rownorm, rho, gam;
+  std::vector<double> mem_f;
+  double eta = 0, sigma_max = 0;
+  // device
+  hipStream_t stream = nullptr;
+  bool own_stream = false;
+  DeviceView v{};
+  std::vector<void *> allocs;
+  int32_t *d_slots = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  nep_stats stats{};
+  ~Model() {
+    if (stream) (void)hipStreamSynchronize(stream);
+    for (void *p : allocs) (void)hipFree(p);
+    if (ev0) (void)hipEventDestroy(ev0);
+    if (ev1) (void)hipEventDestroy(ev1);
+    if (own_stream && stream) (void)hipStreamDestroy(stream);
+  }
+};
+
+template <typename T>
+int dalloc(Model &m, T **p, size_t n) {
+  void *q = nullptr;
+  if (n == 0) n = 1;
+  hipError_t e = hipMalloc(&q, n * sizeof(T));
+  if (e != hipSuccess) return fail(NEP_ERR_NOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
+  m.allocs.push_back(q);
+  *p = static_cast<T *>(q);
+  return NEP_OK;
+}
+template <typename T>
+int upload(Model &m, const T **dst, const std::vector<T> &src) {
+  T *p = nullptr;
+  int rc = dalloc(m, &p, src.size());
+  if (rc) return rc;
+  if (!src.empty()) {
+    hipError_t e = hipMemcpy(p, src.data(), src.size() * sizeof(T), hipMemcpyHostToDevice);
+    if (e != hipSuccess) return fail(NEP_ERR_HIP, std::string("hipMemcpy: ") + hipGetErrorString(e));
+  }
+  *dst = p;
+  return NEP_OK;
+}
+
+// ---------------------------------------------------------------------------------------------
+// model build
+// ---------------------------------------------------------------------------------------------
+int build(Model &m, const nep_model_desc &d) {
+  const int N = d.n_nodes, F = d.n_functions;
+  if (N <= 0 || F <= 0) return fail(NEP_ERR_ARG, "n_nodes and n_functions must be positive");
+  if (N > 2048) return fail(NEP_ERR_ARG, "n_nodes > 2048 not supported by this build");
+  if (d.variant < 0 || d.variant > 2) return fail(NEP_ERR_ARG, "bad variant");
+  if (d.step < 1 || d.step > 3) return fail(NEP_ERR_ARG, "bad step");
+  if (!d.delay || !d.workload || !d.core_per_req || !d.function_memory || !d.node_memory || !d.node_cores ||
+      !d.node_cost || !d.max_delay)
+    return fail(NEP_ERR_ARG, "missing input array");
+  if (d.step != NEP_STEP1 && !d.old_allocations) return fail(NEP_ERR_ARG, "step 2 needs old_allocations");
+  m.N = N;
+  m.F = F;
+  m.variant = d.variant;
+  m.step = d.step;
+  m.step2 = d.step != NEP_STEP1;
+  m.has_n = d.variant != NEP_MIN_DELAY;
+  m.alpha = d.alpha;
+  m.M = d.big_m > 0 ? d.big_m : 1e6;
+  m.eps = d.epsilon > 0 ? d.epsilon : 1e-6;
+  m.sigma4 = d.step == NEP_STEP2_CREATE ? 1.0 : -1.0;
+  m.NP = (N + 3) / 4 * 4;
+  const int chunks = m.NP / 4;
+  m.CPL = chunks <= 64 ? 1 : chunks <= 128 ? 2 : chunks <= 256 ? 4 : 8;
+  m.W.assign(d.workload, d.workload + (size_t)F * N);
+  const double *D = d.delay;
+
+  // exact aggregation of zero-workload sources: they enter only the column sums (C1/C2) and their
+  // own C4 row, with zero objective / CPU / score coefficients, so one pooled row of weight
+  // m_f = #zero sources carries them all (x[i,f,:] = pooled row for every such i).
+  for (int f = 0; f < F; ++f) {
+    int zeros = 0;
+    for (int i = 0; i < N; ++i) {
+      const double w = m.W[(size_t)f * N + i];
+      if (w != 0.0) {
+        m.row_f.push_back(f);
+        m.row_src.push_back(i);
+        m.row_m.push_back(1.f);
+        m.row_w.push_back((float)w);
+      } else {
+        ++zeros;
+      }
+    }
+    if (zeros > 0) {
+      m.row_f.push_back(f);
+      m.row_src.push_back(-1);
+      m.row_m.push_back((float)zeros);
+      m.row_w.push_back(0.f);
+    }
+  }
+  m.R = (int)m.row_f.size();
+
+  // objective / score coefficients (objectives.py:4-52, constraints_step2.py:57-88)
+  double sumW = 0.0;
+  for (double w : m.W) sumW += w;
+  double kobj = 0.0;
+  if (!m.step2) {
+    if (d.variant == NEP_MIN_DELAY) {
+      kobj = 1.0;
+    } else if (d.variant == NEP_MIN_DELAY_AND_UTILIZATION && sumW != 0.0) {
+      double mwd = 0.0;   // objectives.py:36-43
+      for (int f = 0; f < F; ++f)
+        for (int i = 0; i < N; ++i) {
+          double best = -INF;
+          for (int j = 0; j < N; ++j) {
+            const double dl = D[(size_t)i * N + j];
+            if (dl <= d.max_delay[f]) best = std::max(best, dl);
+          }
+          if (best == -INF) return fail(NEP_ERR_ARG, "max() of an empty delay set (objectives.py:41)");
+          mwd += m.W[(size_t)f * N + i] * best;
+        }
+      if (mwd == 0.0) return fail(NEP_ERR_ARG, "max_workload_delay == 0: division by zero (objectives.py:50)");
+      kobj = (1.0 - d.alpha) / mwd;
+    }
+    m.cost_n = d.variant == NEP_MIN_UTILIZATION ? 1.0 : d.variant == NEP_MIN_DELAY_AND_UTILIZATION ? d.alpha / N : 0.0;
+  }
+  double score_rhs = INF;
+  std::vector<double> colmaxD(N, -INF);
+  for (int k = 0; k < N; ++k)
+    for (int i = 0; i < N; ++i) colmaxD[i] = std::max(colmaxD[i], D[(size_t)k * N + i]);
+  m.row_wobj.resize(m.R);
+  m.row_wsc.resize(m.R);
+  for (int r = 0; r < m.R; ++r) {
+    m.row_wobj[r] = (float)(kobj * m.row_w[r]);
+    double wsc = 0.0;
+    if (m.step2 && m.row_src[r] >= 0) {
+      const int f = m.row_f[r], i = m.row_src[r];
+      if (d.variant == NEP_MIN_DELAY) wsc = m.row_w[r];
+      else if (d.variant == NEP_MIN_DELAY_AND_UTILIZATION)
+        wsc = (1.0 - d.alpha) * m.row_w[r] / std::max(d.max_delay[f], colmaxD[i]);
+    }
+    m.row_wsc[r] = (float)wsc;
+  }
+  if (m.step2) {
+    if (d.variant == NEP_MIN_DELAY) {
+      score_rhs = d.soften_step1_sol * d.prev_network_delay;
+      m.score_n_coef = 0.0;
+    } else {
+      score_rhs = d.max_score * d.soften_step1_sol;
+      m.score_n_coef = d.variant == NEP_MIN_UTILIZATION ? 1.0 : d.alpha / N;
+    }
+  }
+
+  // tiles: consecutive rows of one function, at most 16 rows (4 per wave)
+  const int TR = 16;
+  m.ftile_ptr.assign(F + 1, 0);
+  {
+    int r = 0;
+    for (int f = 0; f < F; ++f) {
+      int r0 = r;
+      while (r < m.R && m.row_f[r] == f) ++r;
+      for (int t0 = r0; t0 < r; t0 += TR) {
+        m.tile_row0.push_back(t0);
+        m.tile_nrows.push_back(std::min(TR, r - t0));
+        m.tile_f.push_back(f);
+      }
+      m.ftile_ptr[f + 1] = (int)m.tile_f.size();
+    }
+  }
+  m.T = (int)m.tile_f.size();
+  m.JB = (N + kWave - 1) / kWave;
+  m.FPB = 8;
+  m.FB = (F + m.FPB - 1) / m.FPB;
+
+  // integer-variable layout (variables.py order minus x)
+  const int FN = F * N;
+  IntLayout &il = m.il;
+  il.oc = 0;
+  if (!m.step2) {
+    il.omf = il.omt = il.oa = il.od = -1;
+    il.on = m.has_n ? FN : -1;
+    il.n_int = FN + (m.has_n ? N : 0);
+  } else {
+    il.omf = FN;
+    il.omt = 2 * FN;
+    il.oa = 3 * FN;
+    il.od = 3 * FN + 1;
+    il.on = m.has_n ? 3 * FN + 2 : -1;
+    il.n_int = 3 * FN + 2 + (m.has_n ? N : 0);
+  }
+  m.nat_lb.assign(il.n_int, 0.0);
+  m.nat_ub.assign(il.n_int, 1.0);
+  m.cost_int.assign(il.n_int, 0.0);
+  if (m.has_n)
+    for (int j = 0; j < N; ++j) {
+      // C8 (constraints_step1.py:101-103): cost[j] * n[j] <= budget  ->  bound on n
+      if (d.node_cost[j] > 0) m.nat_ub[il.on + j] = std::min(1.0, d.node_budget / d.node_cost[j]);
+      else if (d.node_budget < 0) m.nat_ub[il.on + j] = -1.0;   // infeasible budget row
+      m.cost_int[il.on + j] = m.cost_n;
+    }
+  double sum_old = 0.0;
+  if (m.step2) {
+    m.w_dis = (double)FN;   // objectives.py:56  w = np.ma.size(old)
+    for (int k = 0; k < FN; ++k) {
+      m.cost_int[il.omf + k] = m.w_dis;
+      m.cost_int[il.omt + k] = m.w_dis;
+      sum_old += d.old_allocations[k];
+    }
+    m.cost_int[il.oa] = m.w_dis - 1;
+    m.cost_int[il.od] = m.w_dis + 1;
+    m.nat_lb[il.oa] = m.nat_lb[il.od] = -(double)FN;
+    m.nat_ub[il.oa] = m.nat_ub[il.od] = 0.0;
+  }
+
+  // dual layout + row bounds
+  DualLayout &dl = m.dl;
+  int o = 0;
+  dl.o1 = o; o += FN;
+  dl.o2 = o; o += FN;
+  dl.o3 = o; o += N;
+  dl.o5 = o; o += N;
+  dl.o6 = dl.o7 = dl.oD1 = dl.oD2 = dl.oD3a = dl.oD3b = dl.oD4 = dl.oS = -1;
+  if (m.has_n) { dl.o6 = o; o += N; dl.o7 = o; o += N; }
+  if (m.step2) {
+    dl.oD1 = o; o += FN;
+    dl.oD2 = o; o += FN;
+    dl.oD3a = o++; dl.oD3b = o++; dl.oD4 = o++; dl.oS = o++;
+  }
+  dl.n_dual = o;
+  m.lo.assign(o, -INF);
+  m.hi.assign(o, INF);
+  for (int k = 0; k < FN; ++k) {
+    m.hi[dl.o1 + k] = 0.0;
+    m.lo[dl.o2 + k] = -m.eps;
+  }
+  for (int j = 0; j < N; ++j) {
+    m.hi[dl.o3 + j] = d.node_memory[j];
+    m.hi[dl.o5 + j] = d.node_cores[j];
+    if (m.has_n) { m.hi[dl.o6 + j] = 0.0; m.lo[dl.o7 + j] = -m.eps; }
+  }
+  if (m.step2) {
+    for (int k = 0; k < FN; ++k) {
+      m.lo[dl.oD1 + k] = -d.old_allocations[k];
+      m.lo[dl.oD2 + k] = d.old_allocations[k];
+    }
+    m.lo[dl.oD3a] = -sum_old;
+    m.lo[dl.oD3b] = sum_old;
+    m.lo[dl.oD4] = m.sigma4 * sum_old;
+    m.hi[dl.oS] = score_rhs;
+  }
+  m.mem_f.assign(d.function_memory, d.function_memory + F);
+
+  // non-x entries of K (COO) and x-row norms (x columns are never rescaled)
+  Coo K;
+  std::vector<double> xmax(o, 0.0), xsum(o, 0.0);
+  std::vector<double> mmax(F, 0.0), msum(F, 0.0);
+  for (int r = 0; r < m.R; ++r) {
+    mmax[m.row_f[r]] = std::max(mmax[m.row_f[r]], (double)m.row_m[r]);
+    msum[m.row_f[r]] += m.row_m[r];
+  }
+  const double *cpr = d.core_per_req;
+  for (int f = 0; f < F; ++f)
+    for (int j = 0; j < N; ++j) {
+      const int k = f * N + j;
+      K.add(dl.o1 + k, il.oc + k, -m.M);
+      K.add(dl.o2 + k, il.oc + k, -1.0);
+      K.add(dl.o3 + j, il.oc + k, m.mem_f[f]);
+      xmax[dl.o1 + k] = xmax[dl.o2 + k] = mmax[f];
+      xsum[dl.o1 + k] = xsum[dl.o2 + k] = msum[f];
+      if (m.has_n) {
+        K.add(dl.o6 + j, il.oc + k, 1.0);
+        K.add(dl.o7 + j, il.oc + k, 1.0);
+      }
+      if (m.step2) {
+        K.add(dl.oD1 + k, il.omf + k, 1.0);
+        K.add(dl.oD1 + k, il.oc + k, -1.0);
+        K.add(dl.oD2 + k, il.omt + k, 1.0);
+        K.add(dl.oD2 + k, il.oc + k, 1.0);
+        K.add(dl.oD3a, il.oc + k, -1.0);
+        K.add(dl.oD3b, il.oc + k, 1.0);
+        K.add(dl.oD4, il.oc + k, m.sigma4);
+      }
+    }
+  if (m.has_n)
+    for (int j = 0; j < N; ++j) {
+      K.add(dl.o6 + j, il.on + j, -m.M);
+      K.add(dl.o7 + j, il.on + j, -1.0);
+      if (m.step2 && m.score_n_coef != 0.0) K.add(dl.oS, il.on + j, m.score_n_coef);
+    }
+  if (m.step2) {
+    K.add(dl.oD3a, il.oa, -1.0);
+    K.add(dl.oD3b, il.od, -1.0);
+    K.add(dl.oD4, il.od, 1.0);
+    K.add(dl.oD4, il.oa, 1.0);
+  }
+  for (int r = 0; r < m.R; ++r) {
+    const int f = m.row_f[r], src = m.row_src[r];
+    for (int j = 0; j < N; ++j) {
+      const double w = (double)m.row_w[r] * cpr[(size_t)f * N + j];
+      xmax[dl.o5 + j] = std::max(xmax[dl.o5 + j], std::fabs(w));
+      xsum[dl.o5 + j] += std::fabs(w);
+      if (m.step2 && src >= 0 && m.row_wsc[r] != 0.f) {
+        const double s = std::fabs((double)m.row_wsc[r] * D[(size_t)src * N + j]);
+        xmax[dl.oS] = std::max(xmax[dl.oS], s);
+        xsum[dl.oS] += s;
+      }
+    }
+  }
+  // row norms for the relative residual: max(1, |bounds|, max |coef|)
+  m.rownorm.assign(o, 1.0);
+  for (int k = 0; k < o; ++k) {
+    double rn = std::max(1.0, xmax[k]);
+    if (std::isfinite(m.lo[k])) rn = std::max(rn, std::fabs(m.lo[k]));
+    if (std::isfinite(m.hi[k])) rn = std::max(rn, std::fabs(m.hi[k]));
+    m.rownorm[k] = rn;
+  }
+  for (size_t e = 0; e < K.v.size(); ++e) m.rownorm[K.r[e]] = std::max(m.rownorm[K.r[e]], std::fabs(K.v[e]));
+
+  // Ruiz equilibration (10 sweeps, inf-norm) + Pock-Chambolle (alpha = 1) on rows and the
+  // non-x columns; x columns keep scale 1 so every routing row stays a plain simplex.
+  m.rho.assign(o, 1.0);
+  m.gam.assign(il.n_int, 1.0);
+  std::vector<double> rn(o), cn(il.n_int);
+  for (int sweep = 0; sweep < 11; ++sweep) {
+    const bool pc = sweep == 10;
+    for (int k = 0; k < o; ++k) rn[k] = pc ? m.rho[k] * xsum[k] : m.rho[k] * xmax[k];
+    std::fill(cn.begin(), cn.end(), 0.0);
+    for (size_t e = 0; e < K.v.size(); ++e) {
+      const double a = std::fabs(m.rho[K.r[e]] * K.v[e] * m.gam[K.c[e]]);
+      if (pc) { rn[K.r[e]] += a; cn[K.c[e]] += a; }
+      else { rn[K.r[e]] = std::max(rn[K.r[e]], a); cn[K.c[e]] = std::max(cn[K.c[e]], a); }
+    }
+    for (int k = 0; k < o; ++k)
+      if (rn[k] > 0) m.rho[k] /= std::sqrt(rn[k]);
+    for (int k = 0; k < il.n_int; ++k)
+      if (cn[k] > 0) m.gam[k] /= std::sqrt(cn[k]);
+  }
+
+  // ||K̃||_2 by power iteration on K̃ᵀK̃ (structured x part + COO part)
+  {
+    std::vector<double> zx((size_t)m.R * N), zs(il.n_int), yv(o), gx((size_t)m.R * N), gs(il.n_int);
+    std::mt19937_64 rng(12345);
+    std::normal_distribution<double> nd;
+    for (auto &t : zx) t = nd(rng);
+    for (auto &t : zs) t = nd(rng);
+    double lam = 0.0;
+    for (int it = 0; it < 60; ++it) {
+      double nrm = 0.0;
+      for (double t : zx) nrm += t * t;
+      for (double t : zs) nrm += t * t;
+      nrm = std::sqrt(nrm);
+      for (auto &t : zx) t /= nrm;
+      for (auto &t : zs) t /= nrm;
+      // y = K̃ z
+      std::fill(yv.begin(), yv.end(), 0.0);
+      for (int r = 0; r < m.R; ++r) {
+        const int f = m.row_f[r], src = m.row_src[r];
+        const double mr = m.row_m[r], wr = m.row_w[r], sc = m.row_wsc[r];
+        const double *xr = &zx[(size_t)r * N];
+        double srow = 0.0;
+        for (int j = 0; j < N; ++j) {
+          yv[dl.o1 + f * N + j] += mr * xr[j];
+          yv[dl.o2 + f * N + j] += mr * xr[j];
+          yv[dl.o5 + j] += wr * cpr[(size_t)f * N + j] * xr[j];
+          if (m.step2 && src >= 0 && sc != 0.0) srow += sc * D[(size_t)src * N + j] * xr[j];
+        }
+        if (m.step2) yv[dl.oS] += srow;
+      }
+      for (size_t e = 0; e < K.v.size(); ++e) yv[K.r[e]] += K.v[e] * m.gam[K.c[e]] * zs[K.c[e]];
+      for (int k = 0; k < o; ++k) yv[k] *= m.rho[k];
+      // g = K̃ᵀ y
+      for (int k = 0; k < o; ++k) yv[k] *= m.rho[k];   // now ρ y
+      for (int r = 0; r < m.R; ++r) {
+        const int f = m.row_f[r], src = m.row_src[r];
+        const double mr = m.row_m[r], wr = m.row_w[r], sc = m.row_wsc[r];
+        double *gr = &gx[(size_t)r * N];
+        for (int j = 0; j < N; ++j) {
+          double g = mr * (yv[dl.o1 + f * N + j] + yv[dl.o2 + f * N + j]) + wr * cpr[(size_t)f * N + j] * yv[dl.o5 + j];
+          if (m.step2 && src >= 0 && sc != 0.0) g += sc * D[(size_t)src * N + j] * yv[dl.oS];
+          gr[j] = g;
+        }
+      }
+      std::fill(gs.begin(), gs.end(), 0.0);
+      for (size_t e = 0; e < K.v.size(); ++e) gs[K.c[e]] += K.v[e] * yv[K.r[e]];
+      for (int k = 0; k < il.n_int; ++k) gs[k] *= m.gam[k];
+      double dot = 0.0;
+      for (size_t k = 0; k < zx.size(); ++k) dot += zx[k] * gx[k];
+      for (int k = 0; k < il.n_int; ++k) dot += zs[k] * gs[k];
+      lam = dot;
+      zx.swap(gx);
+      zs.swap(gs);
+    }
+    m.sigma_max = std::sqrt(std::max(lam, 1e-30));
+    m.eta = 0.95 / m.sigma_max;
+  }
+  return NEP_OK;
+}
+
+int setup_device(Model &m, int max_batch, void *stream) {
+  m.max_batch = max_batch;
+  if (stream) {
+    m.stream = (hipStream_t)stream;
+  } else {
+    HIPCHK(hipStreamCreateWithFlags(&m.stream, hipStreamNonBlocking));
+    m.own_stream = true;
+  }
+  HIPCHK(hipEventCreate(&m.ev0));
+  HIPCHK(hipEventCreate(&m.ev1));
+  DeviceView &v = m.v;
+  v.N = m.N; v.NP = m.NP; v.F = m.F; v.R = m.R; v.T = m.T; v.JB = m.JB; v.FB = m.FB; v.FPB = m.FPB; v.CPL = m.CPL;
+  v.has_n = m.has_n; v.step2 = m.step2; v.variant = m.variant;
+  v.M = m.M; v.eps = m.eps; v.sigma4 = m.sigma4; v.cost_n = m.cost_n; v.score_n_coef = m.score_n_coef;
+  v.w_dis = m.w_dis;
+  v.dl = m.dl; v.il = m.il;
+  int rc;
+  if ((rc = upload(m, &v.row_f, m.row_f))) return rc;
+  if ((rc = upload(m, &v.row_src, m.row_src))) return rc;
+  if ((rc = upload(m, &v.row_m, m.row_m))) return rc;
+  if ((rc = upload(m, &v.row_w, m.row_w))) return rc;
+  if ((rc = upload(m, &v.row_wobj, m.row_wobj))) return rc;
+  if ((rc = upload(m, &v.row_wsc, m.row_wsc))) return rc;
+  if ((rc = upload(m, &v.tile_row0, m.tile_row0))) return rc;
+  if ((rc = upload(m, &v.tile_nrows, m.tile_nrows))) return rc;
+  if ((rc = upload(m, &v.tile_f, m.tile_f))) return rc;
+  if ((rc = upload(m, &v.ftile_ptr, m.ftile_ptr))) return rc;
+  if ((rc = upload(m, &v.gam, m.gam))) return rc;
+  if ((rc = upload(m, &v.rho, m.rho))) return rc;
+  if ((rc = upload(m, &v.lo, m.lo))) return rc;
+  if ((rc = upload(m, &v.hi, m.hi))) return rc;
+  if ((rc = upload(m, &v.rownorm, m.rownorm))) return rc;
+  if ((rc = upload(m, &v.cost_int, m.cost_int))) return rc;
+  if ((rc = upload(m, &v.mem_f, m.mem_f))) return rc;
+  return NEP_OK;
+}
+
+int setup_dense(Model &m, const nep_model_desc &d) {
+  DeviceView &v = m.v;
+  const int N = m.N, NP = m.NP, F = m.F;
+  std::vector<float> Dp((size_t)N * NP, 0.f), cp((size_t)F * NP, 0.f);
+  for (int i = 0; i < N; ++i)
+    for (int j = 0; j < N; ++j) Dp[(size_t)i * NP + j] = (float)d.delay[(size_t)i * N + j];
+  for (int f = 0; f < F; ++f)
+    for (int j = 0; j < N; ++j) {
+      double c = d.core_per_req[(size_t)f * N + j];
+      if (!std::isfinite(c)) c = std::numeric_limits<float>::max();
+      cp[(size_t)f * NP + j] = (float)std::min(c, (double)std::numeric_limits<float>::max());
+    }
+  int rc;
+  if ((rc = upload(m, &v.D, Dp))) return rc;
+  if ((rc = upload(m, &v.cpr, cp))) return rc;
+  // per-slot arrays
+  const int B = m.max_batch;
+  v.sx = (int64_t)m.R * NP;
+  v.smask = (int64_t)F * NP;
+  v.sint = m.il.n_int;
+  v.sdual = m.dl.n_dual;
+  v.skty = (int64_t)F * NP + NP + 4;
+  v.spart = (int64_t)m.T * 2 * NP;
+  v.stpart = (int64_t)m.T * NTS;
+  v.sbpart = (int64_t)(m.FB * m.JB + m.JB) * NBS;
+  v.snpart = (int64_t)m.FB * 3 * NP;
+  if ((rc = dalloc(m, &v.x, (size_t)B * v.sx))) return rc;
+  if ((rc = dalloc(m, &v.xa, (size_t)B * v.sx))) return rc;
+  if ((rc = dalloc(m, &v.mask, (size_t)B * v.smask))) return rc;
+  if ((rc = dalloc(m, &v.zi, (size_t)B * v.sint))) return rc;
+  if ((rc = dalloc(m, &v.zia, (size_t)B * v.sint))) return rc;
+  if ((rc = dalloc(m, &v.lb, (size_t)B * v.sint))) return rc;
+  if ((rc = dalloc(m, &v.ub, (size_t)B * v.sint))) return rc;
+  if ((rc = dalloc(m, &v.y, (size_t)B * v.sdual))) return rc;
+  if ((rc = dalloc(m, &v.ya, (size_t)B * v.sdual))) return rc;
+  if ((rc = dalloc(m, &v.kz, (size_t)B * v.sdual))) return rc;
+  if ((rc = dalloc(m, &v.kty, (size_t)B * v.skty))) return rc;
+  if ((rc = dalloc(m, &v.part, (size_t)B * v.spart))) return rc;
+  if ((rc = dalloc(m, &v.tpart, (size_t)B * v.stpart))) return rc;
+  if ((rc = dalloc(m, &v.bpart, (size_t)B * v.sbpart))) return rc;
+  if ((rc = dalloc(m, &v.npart, (size_t)B * v.snpart))) return rc;
+  if ((rc = dalloc(m, &v.ctrl, (size_t)B))) return rc;
+  if ((rc = dalloc(m, &m.d_slots, (size_t)B))) return rc;
+  HIPCHK(hipMemsetAsync(v.ctrl, 0, sizeof(Ctrl) * B, m.stream));
+  HIPCHK(hipMemsetAsync(v.x, 0, sizeof(float) * B * v.sx, m.stream));
+  HIPCHK(hipMemsetAsync(v.xa, 0, sizeof(float) * B * v.sx, m.stream));
+  HIPCHK(hipMemsetAsync(v.zi, 0, sizeof(double) * B * v.sint, m.stream));
+  HIPCHK(hipMemsetAsync(v.y, 0, sizeof(double) * B * v.sdual, m.stream));
+  HIPCHK(hipStreamSynchronize(m.stream));
+  return NEP_OK;
+}
+
+// per-node presolve: bounds, the C8 cap, n_ub = 0 => c_ub[:, j] = 0, destination masks.
+// Returns false if the node is infeasible.
+bool presolve(const Model &m, const double *lbi, const double *ubi, std::vector<double> &lb, std::vector<double> &ub,
+              std::vector<uint8_t> &mask) {
+  const int n = m.il.n_int, N = m.N, F = m.F, NP = m.NP;
+  lb = m.nat_lb;
+  ub = m.nat_ub;
+  if (lbi)
+    for (int k = 0; k < n; ++k) lb[k] = std::max(lb[k], lbi[k]);
+  if (ubi)
+    for (int k = 0; k < n; ++k) ub[k] = std::min(ub[k], ubi[k]);
+  bool ok = true;
+  if (m.has_n)
+    for (int j = 0; j < N; ++j)
+      if (ub[m.il.on + j] <= 0.0)
+        for (int f = 0; f < F; ++f) ub[m.il.oc + f * N + j] = std::min(ub[m.il.oc + f * N + j], 0.0);
+  for (int k = 0; k < n; ++k)
+    if (lb[k] > ub[k] + 1e-12) ok = false;
+  mask.assign((size_t)F * NP, 0);
+  for (int f = 0; f < F; ++f) {
+    int cnt = 0;
+    for (int j = 0; j < N; ++j) {
+      const bool a = ub[m.il.oc + f * N + j] > 0.0;
+      mask[(size_t)f * NP + j] = a;
+      cnt += a;
+    }
+    if (cnt == 0) ok = false;   // every routing row of f would be empty (C4 infeasible)
+  }
+  return ok;
+}
+
+int solve_batch(Model &m, int B, const int32_t *slots, const double *lbi, const double *ubi, const nep_lp_opts *opts,
+                double *obj, double *pobj, int32_t *status, int64_t *iters) {
+  auto t0 = std::chrono::steady_clock::now();
+  if (B <= 0) return NEP_OK;
+  if (B > m.max_batch) return fail(NEP_ERR_ARG, "B > max_batch");
+  nep_lp_opts o{};
+  o.tol = 1e-7;
+  o.cutoff = INF;
+  o.max_iters = 200000;
+  o.check_every = 64;
+  o.warm_start = 0;
+  if (opts) {
+    if (opts->tol > 0) o.tol = opts->tol;
+    o.cutoff = opts->cutoff;
+    if (opts->max_iters > 0) o.max_iters = opts->max_iters;
+    if (opts->check_every > 0) o.check_every = opts->check_every;
+    o.warm_start = opts->warm_start;
+  }
+  DeviceView &v = m.v;
+  v.tol = o.tol;
+  v.cutoff = o.cutoff;
+  v.max_iters = o.max_iters;
+  const int n = m.il.n_int;
+  std::vector<int32_t> act;
+  std::vector<double> lb, ub;
+  std::vector<uint8_t> mask;
+  for (int b = 0; b < B; ++b) {
+    const int s = slots[b];
+    if (s < 0 || s >= m.max_batch) return fail(NEP_ERR_ARG, "slot out of range");
+    const bool ok = presolve(m, lbi ? lbi + (size_t)b * n : nullptr, ubi ? ubi + (size_t)b * n : nullptr, lb, ub, mask);
+    status[b] = ok ? NEP_LP_ITERATION_LIMIT : NEP_LP_INFEASIBLE;
+    obj[b] = ok ? -INF : INF;
+    pobj[b] = NAN;
+    iters[b] = 0;
+    if (!ok) continue;
+    HIPCHK(hipMemcpyAsync(v.lb + (size_t)s * v.sint, lb.data(), n * sizeof(double), hipMemcpyHostToDevice, m.stream));
+    HIPCHK(hipMemcpyAsync(v.ub + (size_t)s * v.sint, ub.data(), n * sizeof(double), hipMemcpyHostToDevice, m.stream));
+    HIPCHK(hipMemcpyAsync(v.mask + (size_t)s * v.smask, mask.data(), mask.size(), hipMemcpyHostToDevice, m.stream));
+    // synchronous copies above read host vectors that are reused: wait before the next slot
+    HIPCHK(hipStreamSynchronize(m.stream));
+    act.push_back(s);
+  }
+  if (!act.empty()) {
+    HIPCHK(hipMemcpyAsync(m.d_slots, act.data(), act.size() * sizeof(int32_t), hipMemcpyHostToDevice, m.stream));
+    const int na = (int)act.size();
+    HIPCHK(launch_init_slot(v, m.d_slots, na, o.warm_start != 0, m.eta, m.stream));
+    HIPCHK(launch_x_pass(v, m.d_slots, na, false, true, true, m.stream));
+    HIPCHK(launch_small_passes(v, m.d_slots, na, false, true, true, m.stream));
+    HIPCHK(launch_scalar_pass(v, m.d_slots, na, false, true, true, 0, m.stream));
+  }
+  std::vector<Ctrl> ctrl(m.max_batch);
+  int64_t block_no = 0;
+  while (!act.empty()) {
+    const int na = (int)act.size();
+    const int ce = o.check_every;
+    for (int it = 0; it < ce; ++it) {
+      const bool first = it == 0, check = it == ce - 1;
+      const bool sample = first && (block_no % 4 == 0);
+      if (sample) HIPCHK(hipEventRecord(m.ev0, m.stream));
+      HIPCHK(launch_x_pass(v, m.d_slots, na, check, false, first, m.stream));
+      if (sample) HIPCHK(hipEventRecord(m.ev1, m.stream));
+      HIPCHK(launch_small_passes(v, m.d_slots, na, check, false, first, m.stream));
+      if (m.step2 || check) HIPCHK(launch_scalar_pass(v, m.d_slots, na, check, false, first, ce, m.stream));
+      m.stats.x_pass_launches += 1;
+      if (sample) {
+        HIPCHK(hipEventSynchronize(m.ev1));
+        float ms = 0.f;
+        HIPCHK(hipEventElapsedTime(&ms, m.ev0, m.ev1));
+        m.stats.x_pass_ms += ms;
+        m.stats.x_pass_sampled += 1;
+        m.stats.x_pass_lp_iters += na;
+      }
+    }
+    ++block_no;
+    HIPCHK(hipMemcpyAsync(ctrl.data(), v.ctrl, sizeof(Ctrl) * m.max_batch, hipMemcpyDeviceToHost, m.stream));
+    HIPCHK(hipStreamSynchronize(m.stream));
+    m.stats.lp_iterations += (int64_t)na * ce;
+    std::vector<int32_t> still;
+    for (int s : act)
+      if (ctrl[s].active) still.push_back(s);
+    if (still.size() != act.size() && !still.empty())
+      HIPCHK(hipMemcpyAsync(m.d_slots, still.data(), still.size() * sizeof(int32_t), hipMemcpyHostToDevice, m.stream));
+    act.swap(still);
+  }
+  HIPCHK(hipMemcpyAsync(ctrl.data(), v.ctrl, sizeof(Ctrl) * m.max_batch, hipMemcpyDeviceToHost, m.stream));
+  HIPCHK(hipStreamSynchronize(m.stream));
+  for (int b = 0; b < B; ++b) {
+    if (status[b] == NEP_LP_INFEASIBLE) continue;
+    const Ctrl &c = ctrl[slots[b]];
+    status[b] = c.status;
+    iters[b] = c.k;
+    pobj[b] = c.pobj;
+    obj[b] = c.status == NEP_LP_OPTIMAL ? c.lagr : c.best_lagr;
+    if (c.status == NEP_LP_INFEASIBLE) obj[b] = INF;
+  }
+  m.stats.solve_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  return NEP_OK;
+}
+
+}  // namespace
+
+// =============================================================================================
+// C ABI
+// =============================================================================================
+extern "C" {
+
+int nep_api_version(void) { return NEP_API_VERSION; }
+const char *nep_last_error(void) { return g_err.c_str(); }
+
+int nep_model_create(const nep_model_desc *desc, int32_t max_batch, void *hip_stream, void **out_model) {
+  if (!desc || !out_model) return fail(NEP_ERR_ARG, "null argument");
+  if (max_batch <= 0) return fail(NEP_ERR_ARG, "max_batch must be positive");
+  std::unique_ptr<Model> m(new Model());
+  int rc = build(*m, *desc);
+  if (rc) return rc;
+  rc = setup_device(*m, max_batch, hip_stream);
+  if (rc) return rc;
+  rc = setup_dense(*m, *desc);
+  if (rc) return rc;
+  *out_model = m.release();
+  return NEP_OK;
+}
+
+void nep_model_destroy(void *model) { delete static_cast<Model *>(model); }
+
+int nep_model_get_info(void *model, nep_model_info *info) {
+  if (!model || !info) return fail(NEP_ERR_ARG, "null argument");
+  const Model &m = *static_cast<Model *>(model);
+  info->n_int = m.il.n_int;
+  info->n_rows = m.R;
+  info->n_tiles = m.T;
+  info->max_batch = m.max_batch;
+  info->x_entries = (int64_t)m.R * m.N;
+  // B_iter = 4 (2P + 2FN + 2N + 2m), P = x entries iterated, m = dual rows
+  info->bytes_per_iter = 4 * (2 * (int64_t)m.R * m.N + 2 * (int64_t)m.F * m.N + 2 * (int64_t)m.N + 2 * (int64_t)m.dl.n_dual);
+  info->step_size = m.eta;
+  return NEP_OK;
+}
+
+int nep_lp_solve_batch(void *model, int32_t B, const int32_t *slots, const double *lb_int, const double *ub_int,
+                       const nep_lp_opts *opts, double *obj, double *primal_obj, int32_t *status, int64_t *iters) {
+  if (!model || !slots || !obj || !primal_obj || !status || !iters) return fail(NEP_ERR_ARG, "null argument");
+  return solve_batch(*static_cast<Model *>(model), B, slots, lb_int, ub_int, opts, obj, primal_obj, status, iters);
+}
+
+int nep_lp_get_solution(void *model, int32_t slot, double *z_int, float *x_dense) {
+  if (!model) return fail(NEP_ERR_ARG, "null model");
+  Model &m = *static_cast<Model *>(model);
+  if (slot < 0 || slot >= m.max_batch) return fail(NEP_ERR_ARG, "slot out of range");
+  if (z_int)
+    HIPCHK(hipMemcpyAsync(z_int, m.v.zi + (size_t)slot * m.v.sint, m.il.n_int * sizeof(double), hipMemcpyDeviceToHost,
+                          m.stream));
+  if (x_dense) {
+    std::vector<float> xb((size_t)m.R * m.NP);
+    HIPCHK(hipMemcpyAsync(xb.data(), m.v.x + (size_t)slot * m.v.sx, xb.size() * sizeof(float), hipMemcpyDeviceToHost,
+                          m.stream));
+    HIPCHK(hipStreamSynchronize(m.stream));
+    const int N = m.N, F = m.F;
+    for (int r = 0; r < m.R; ++r) {
+      const int f = m.row_f[r], src = m.row_src[r];
+      const float *xr = &xb[(size_t)r * m.NP];
+      for (int i = 0; i < N; ++i) {
+        const bool member = src >= 0 ? (i == src) : (m.W[(size_t)f * N + i] == 0.0);
+        if (!member) continue;
+        std::memcpy(&x_dense[((size_t)i * F + f) * N], xr, N * sizeof(float));   // [i][f][j]
+      }
+    }
+  }
+  HIPCHK(hipStreamSynchronize(m.stream));
+  return NEP_OK;
+}
+
+int nep_lp_get_rows(void *model, int32_t slot, float *xbar, int32_t *row_f, int32_t *row_src) {
+  if (!model) return fail(NEP_ERR_ARG, "null model");
+  Model &m = *static_cast<Model *>(model);
+  if (slot < 0 || slot >= m.max_batch) return fail(NEP_ERR_ARG, "slot out of range");
+  if (xbar) {
+    HIPCHK(hipMemcpy2DAsync(xbar, m.N * sizeof(float), m.v.x + (size_t)slot * m.v.sx, m.NP * sizeof(float),
+                            m.N * sizeof(float), m.R, hipMemcpyDeviceToHost, m.stream));
+    HIPCHK(hipStreamSynchronize(m.stream));
+  }
+  if (row_f) std::memcpy(row_f, m.row_f.data(), m.R * sizeof(int32_t));
+  if (row_src) std::memcpy(row_src, m.row_src.data(), m.R * sizeof(int32_t));
+  return NEP_OK;
+}
+
+int nep_lp_copy_state(void *model, int32_t src, int32_t dst) {
+  if (!model) return fail(NEP_ERR_ARG, "null model");
+  Model &m = *static_cast<Model *>(model);
+  if (src < 0 || dst < 0 || src >= m.max_batch || dst >= m.max_batch) return fail(NEP_ERR_ARG, "slot out of range");
+  if (src == dst) return NEP_OK;
+  const DeviceView &v = m.v;
+  HIPCHK(hipMemcpyAsync(v.x + dst * v.sx, v.x + src * v.sx, v.sx * sizeof(float), hipMemcpyDeviceToDevice, m.stream));
+  HIPCHK(hipMemcpyAsync(v.zi + dst * v.sint, v.zi + src * v.sint, v.sint * sizeof(double), hipMemcpyDeviceToDevice,
+                        m.stream));
+  HIPCHK(hipMemcpyAsync(v.y + dst * v.sdual, v.y + src * v.sdual, v.sdual * sizeof(double), hipMemcpyDeviceToDevice,
+                        m.stream));
+  HIPCHK(hipMemcpyAsync(v.kty + dst * v.skty, v.kty + src * v.skty, v.skty * sizeof(float), hipMemcpyDeviceToDevice,
+                        m.stream));
+  HIPCHK(hipMemcpyAsync(v.ctrl + dst, v.ctrl + src, sizeof(Ctrl), hipMemcpyDeviceToDevice, m.stream));
+  HIPCHK(hipStreamSynchronize(m.stream));
+  return NEP_OK;
+}
+
+int nep_lp_get_diag(void *model, int32_t slot, double *out16) {
+  if (!model || !out16) return fail(NEP_ERR_ARG, "null argument");
+  Model &m = *static_cast<Model *>(model);
+  if (slot < 0 || slot >= m.max_batch) return fail(NEP_ERR_ARG, "slot out of range");
+  Ctrl c;
+  HIPCHK(hipMemcpy(&c, m.v.ctrl + slot, sizeof(Ctrl), hipMemcpyDeviceToHost));
+  const double vals[16] = {c.pobj, c.lagr, c.best_lagr, c.pres, c.gap, c.omega, c.tau, c.sigma, c.eta,
+                           (double)c.k, (double)c.k_since_restart, (double)c.status, (double)c.active,
+                           c.last_restart_fpr, c.prev_fpr, m.sigma_max};
+  std::memcpy(out16, vals, sizeof(vals));
+  return NEP_OK;
+}
+
+int nep_debug_state(void *model, int32_t slot, double *y, double *kz, float *kty, double *lb, double *ub) {
+  if (!model) return fail(NEP_ERR_ARG, "null model");
+  Model &m = *static_cast<Model *>(model);
+  const DeviceView &v = m.v;
+  if (y) HIPCHK(hipMemcpy(y, v.y + slot * v.sdual, v.sdual * sizeof(double), hipMemcpyDeviceToHost));
+  if (kz) HIPCHK(hipMemcpy(kz, v.kz + slot * v.sdual, v.sdual * sizeof(double), hipMemcpyDeviceToHost));
+  if (kty) HIPCHK(hipMemcpy(kty, v.kty + slot * v.skty, v.skty * sizeof(float), hipMemcpyDeviceToHost));
+  if (lb) HIPCHK(hipMemcpy(lb, v.lb + slot * v.sint, v.sint * sizeof(double), hipMemcpyDeviceToHost));
+  if (ub) HIPCHK(hipMemcpy(ub, v.ub + slot * v.sint, v.sint * sizeof(double), hipMemcpyDeviceToHost));
+  return NEP_OK;
+}
+
+int nep_debug_build(const nep_model_desc *desc, double *eta, double *rho, double *gam, double *rownorm, int32_t *dims) {
+  if (!desc) return fail(NEP_ERR_ARG, "null argument");
+  Model m;
+  int rc = build(m, *desc);
+  if (rc) return rc;
+  if (eta) *eta = m.eta;
+  if (rho) std::memcpy(rho, m.rho.data(), m.rho.size() * sizeof(double));
+  if (gam) std::memcpy(gam, m.gam.data(), m.gam.size() * sizeof(double));
+  if (rownorm) std::memcpy(rownorm, m.rownorm.data(), m.rownorm.size() * sizeof(double));
+  if (dims) {
+    dims[0] = m.R; dims[1] = m.T; dims[2] = m.il.n_int; dims[3] = m.dl.n_dual;
+  }
+  return NEP_OK;
+}
+
+int nep_get_stats(void *model, nep_stats *stats) {
+  if (!model || !stats) return fail(NEP_ERR_ARG, "null argument");
+  *stats = static_cast<Model *>(model)->stats;
+  return NEP_OK;
+}
+
+void nep_reset_stats(void *model) {
+  if (model) static_cast<Model *>(model)->stats = nep_stats{};
+}
+
+}  // extern "C"

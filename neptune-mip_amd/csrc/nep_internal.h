@@ -1,0 +1,90 @@
+// nep_internal.h — shared host/device layout of the NEPTUNE LP engine (MI355X / gfx950).
+//
+// One model = one structured LP family (a reference step model, neptune_step1.py / neptune_step2.py)
+// and `max_batch` LP slots (B&B nodes).  Layout in HBM (per slot unless noted):
+//
+//   x     [R][NP] f32   routing rows x̄[r, j]; row r = (function f, source i) or the pooled
+//                       zero-workload sources of f (exact aggregation)
+//   xa    [R][NP] f32   restart anchor of x
+//   mask  [F][NP] u8    destination j allowed for function f at this node (c_ub[f,j] > 0)
+//   zi    [n_int] f64   small primal: c, (mf, mt, a, d), n        + anchor zia, bounds lb/ub
+//   y     [n_dual] f64  duals of the dualised rows                + anchor ya, activity kz
+//   kty   [F*NP + NP + 4] f32  packed duals the x pass needs: y1+y2 per (f,j), y5 per j, yS
+//   part  [T][2][NP] f32  per-tile partial column sums (C1/C2 activity) and CPU sums (C5)
+//   tpart [T][NTS] f64  per-tile scalars (score row, objective, Lagrangian, movement, distance)
+//   npart [FB][3][NP] f64 per-(function block, node) partial sums: memory, Σ_f c, CPU
+//   bpart [FB*JB+JB][NBS] f64 per-block scalars of the small-variable kernels
+//   ctrl  Ctrl          step sizes, primal weight, restart state, status
+// Static (shared by all slots): row_f/src/m/w/wobj/wsc [R], tiles, D [N][NP] f32, cpr [F][NP] f32,
+// gamma [n_int], rho / lo / hi / rownorm [n_dual], cost_int [n_int].
+#pragma once
+#include <cstdint>
+
+namespace nep {
+
+constexpr int kWave = 64;
+constexpr int kTileWaves = 4;            // waves per x-pass workgroup
+constexpr int kTileThreads = kWave * kTileWaves;
+
+// per-tile scalar partials
+enum { TS_SCORE = 0, TS_POBJ, TS_LAGR, TS_MOVE, TS_DIST, TS_EMPTY, NTS };
+// per-j-block scalar partials
+enum {
+  BS_SUMC_NEW = 0,   // sum over (f,j) of c'            (step-2 rows D3/D4)
+  BS_SCORE_N,        // score-row n part of the new n   (step-2 MU/MDU)
+  BS_LAGR,           // Lagrangian: small vars + row terms
+  BS_POBJ,           // objective of the small vars
+  BS_RES,            // max normalised primal violation
+  BS_MOVE_Z, BS_MOVE_Y, BS_DIST_Z, BS_DIST_Y,
+  NBS
+};
+
+struct Ctrl {
+  double eta, omega, tau, sigma;
+  double last_restart_fpr, prev_fpr;
+  double pobj, lagr, best_lagr, pres, gap;
+  double omega_lo, omega_hi;
+  int64_t k, k_since_restart, k_total_at_restart;
+  int32_t status, active, restart_pending, pad;
+};
+
+// row-family offsets inside y / kz / rho / lo / hi
+struct DualLayout {
+  int o1, o2, o3, o5, o6, o7, oD1, oD2, oD3a, oD3b, oD4, oS;
+  int n_dual;
+};
+// small-primal offsets inside zi
+struct IntLayout {
+  int oc, omf, omt, oa, od, on;
+  int n_int;
+};
+
+struct DeviceView {
+  // sizes
+  int N, NP, F, R, T, JB, FB, FPB, CPL;
+  int has_n, step2, variant;
+  double M, eps, sigma4, cost_n, score_n_coef, w_dis;
+  DualLayout dl;
+  IntLayout il;
+  // static
+  const int32_t *row_f, *row_src;
+  const float *row_m, *row_w, *row_wobj, *row_wsc;
+  const int32_t *tile_row0, *tile_nrows, *tile_f, *ftile_ptr;
+  const float *D, *cpr;
+  const double *gam, *rho, *lo, *hi, *rownorm, *cost_int, *mem_f;
+  // per slot (base pointers; slot stride below)
+  float *x, *xa;
+  uint8_t *mask;
+  double *zi, *zia, *lb, *ub;
+  double *y, *ya, *kz;
+  float *kty;
+  float *part;
+  double *tpart, *bpart, *npart;
+  Ctrl *ctrl;
+  int64_t sx, smask, sint, sdual, skty, spart, stpart, sbpart, snpart;   // per-slot strides (elements)
+  // check/solve parameters
+  double tol, cutoff;
+  int64_t max_iters;
+};
+
+}  // namespace nep

@@ -1,0 +1,267 @@
+#!/usr/bin/env python3
+"""Dev-only prototype: PDHG on the NEPTUNE LP with the C4 rows kept in the primal set
+(per-source simplex projection) — the algorithm the HIP kernels implement.
+
+Works on the oracle CSR (C4 rows detected and removed) so iteration counts and accuracy can be
+compared against HiGHS before any kernel is written.
+"""
+import sys
+import time
+
+import numpy as np
+import scipy.sparse as sp
+
+sys.path.insert(0, "/root/repo")
+sys.path.insert(0, "/root/repo/neptune-mip_amd")
+
+
+def simplex_groups(m):
+    """Find the C4 rows (lo == hi == 1, all coefs 1, on x only) -> groups of x columns."""
+    A = m["A"].tocsr()
+    nx = m["layout"].nx
+    N = m["layout"].N
+    g = []
+    keep = []
+    for r in range(A.shape[0]):
+        s, e = A.indptr[r], A.indptr[r + 1]
+        cols = A.indices[s:e]
+        if m["lo"][r] == 1 and m["hi"][r] == 1 and len(cols) == N and cols.max() < nx and np.all(A.data[s:e] == 1):
+            g.append(np.sort(cols))
+        else:
+            keep.append(r)
+    return np.array(g), np.array(keep)
+
+
+def proj_simplex(V, mask):
+    """Rows of V onto {x >= 0, sum x = 1, x[~mask] = 0}."""
+    Vm = np.where(mask, V, -np.inf)
+    U = -np.sort(-Vm, axis=1)
+    css = np.cumsum(np.where(np.isfinite(U), U, 0), axis=1)
+    k = np.arange(1, V.shape[1] + 1)
+    cond = (U - (css - 1) / k > 0) & np.isfinite(U)
+    rho = cond.sum(axis=1)
+    theta = (css[np.arange(V.shape[0]), rho - 1] - 1) / rho
+    return np.where(mask, np.maximum(V - theta[:, None], 0), 0.0)
+
+
+class Prob:
+    def __init__(self, m, lb=None, ub=None, scale="ruiz", ruiz_iters=10):
+        self.m = m
+        L = m["layout"]
+        self.nx = L.nx
+        lb = m["lb"].copy() if lb is None else lb.copy()
+        ub = m["ub"].copy() if ub is None else ub.copy()
+        groups, keep = simplex_groups(m)
+        self.groups = groups                      # [R, N] column ids of x
+        A = m["A"].tocsr()[keep]
+        lo, hi = m["lo"][keep], m["hi"][keep]
+        n = A.shape[1]
+        # x <= 1 implied by the simplex
+        ub[:self.nx] = np.minimum(ub[:self.nx], 1.0)
+        # presolve: c ub 0 -> x column masked (C1: sum_i x <= M c)
+        self.mask = np.ones(groups.shape, bool)
+        c0 = L.c0
+        F, N = L.F, L.N
+        ucm = ub[c0:c0 + F * N].reshape(F, N).copy()
+        if L.has_n:
+            un = ub[L.n0:L.n0 + N]
+            ucm[:, un <= 0] = 0
+            ub[c0:c0 + F * N] = np.minimum(ub[c0:c0 + F * N], ucm.ravel())
+        fj_mask = ucm > 0
+        # groups are ordered f-major then i: group g -> f = g // N
+        gf = np.arange(groups.shape[0]) // N
+        self.mask = fj_mask[gf]
+        xm = np.zeros(n, bool)
+        xm[groups.ravel()] = ~self.mask.ravel()
+        ub[xm] = 0.0
+        self.lb, self.ub, self.lo, self.hi, self.c = lb, ub, lo, hi, m["c"].copy()
+        # scaling: rows + non-x columns (x columns fixed at 1 so the simplex stays a simplex)
+        dr = np.ones(A.shape[0])
+        dc = np.ones(n)
+        K = A.copy()
+        isx = np.zeros(n, bool)
+        isx[:self.nx] = True
+        if scale in ("ruiz", "ruiz_x"):
+            for _ in range(ruiz_iters):
+                rmax = np.sqrt(abs(K).max(axis=1).toarray().ravel())
+                cmax = np.sqrt(abs(K).max(axis=0).toarray().ravel())
+                rmax[rmax == 0] = 1
+                cmax[cmax == 0] = 1
+                if scale == "ruiz":
+                    cmax[isx] = 1
+                K = sp.diags(1 / rmax) @ K @ sp.diags(1 / cmax)
+                dr /= rmax
+                dc /= cmax
+            Ka = abs(K)
+            rn = np.sqrt(np.asarray(Ka.sum(axis=1)).ravel())
+            cn = np.sqrt(np.asarray(Ka.sum(axis=0)).ravel())
+            rn[rn == 0] = 1
+            cn[cn == 0] = 1
+            if scale == "ruiz":
+                cn[isx] = 1
+            K = sp.diags(1 / rn) @ K @ sp.diags(1 / cn)
+            dr /= rn
+            dc /= cn
+        self.K = K.tocsr()
+        self.rowmax = abs(A).max(axis=1).toarray().ravel()
+        self.KT = self.K.T.tocsr()
+        self.dr, self.dc = dr, dc
+        self.cs = self.c * dc
+        self.los, self.his = lo * dr, hi * dr
+        self.lbs, self.ubs = lb / dc, ub / dc
+        self.xsc = dc[:self.nx][groups]           # x column scales per group (1 unless ruiz_x)
+
+    def proj(self, z):
+        out = np.clip(z, self.lbs, self.ubs)
+        X = z[self.groups] * self.xsc             # back to unscaled x
+        X = proj_simplex(X, self.mask)
+        out[self.groups] = X / self.xsc
+        return out
+
+    def lagrangian(self, y):
+        """Valid lower bound for any sign-correct y (x kept in the simplex)."""
+        rc = self.cs - self.KT @ y
+        rcx = rc[self.groups] / self.xsc
+        rcx = np.where(self.mask, rcx, np.inf)
+        val = rcx.min(axis=1).sum()
+        other = np.ones(len(rc), bool)
+        other[self.groups.ravel()] = False
+        r = rc[other]
+        val += np.sum(np.where(r > 0, self.lbs[other] * r, self.ubs[other] * r))
+        val += np.sum(np.where(y > 0, np.where(np.isfinite(self.los), self.los, 0) * y,
+                               np.where(np.isfinite(self.his), self.his, 0) * y))
+        bad = ((y > 0) & ~np.isfinite(self.los)) | ((y < 0) & ~np.isfinite(self.his))
+        if bad.any():
+            return -np.inf
+        return val
+
+
+OMEGA0, OMIN, OMAX = None, 1e-2, 1e2
+HALPERN = True
+
+
+def power_norm(K, iters=80):
+    v = np.random.default_rng(0).standard_normal(K.shape[1])
+    for _ in range(iters):
+        v = K.T @ (K @ v)
+        nv = np.linalg.norm(v)
+        v /= nv
+    return np.sqrt(nv)
+
+
+def solve(P, tol=1e-7, max_iter=100000, reflect=1.0, check_every=64, verbose=False, z_init=None, y_init=None,
+          dtype=np.float64):
+    K, KT = P.K, P.KT
+    eta = 0.998 / power_norm(K)
+    n, m = K.shape[1], K.shape[0]
+    cnorm = np.linalg.norm(P.cs)
+    bvec = np.concatenate([P.los[np.isfinite(P.los)], P.his[np.isfinite(P.his)]])
+    bnorm = np.linalg.norm(bvec)
+    omega = OMEGA0 if OMEGA0 else (cnorm / bnorm if cnorm > 1e-10 and bnorm > 1e-10 else 1.0)
+    omega = min(max(omega, OMIN), OMAX)
+    z = P.proj(np.zeros(n) if z_init is None else z_init / P.dc)
+    y = np.zeros(m) if y_init is None else y_init / P.dr
+    z0, y0 = z.copy(), y.copy()
+    k_since, total = 0, 0
+    last_err, prev_err = None, np.inf
+
+    def T(z, y):
+        tau, sig = eta / omega, eta * omega
+        zn = P.proj(z - tau * (P.cs - KT @ y))
+        v = y - sig * (K @ (2 * zn - z))
+        yn = v - sig * np.clip(v / sig, -P.his, -P.los)
+        return zn, yn
+
+    best = None
+    while total < max_iter:
+        zn, yn = T(z, y)
+        kk = k_since
+        if HALPERN:
+            z_next = (kk + 1) / (kk + 2) * ((1 + reflect) * zn - reflect * z) + z0 / (kk + 2)
+            y_next = (kk + 1) / (kk + 2) * ((1 + reflect) * yn - reflect * y) + y0 / (kk + 2)
+        else:
+            z_next, y_next = zn, yn
+        total += 1
+        k_since += 1
+        if total % check_every == 0:
+            zu = zn * P.dc
+            pobj = P.c @ zu
+            Az = P.K @ zn / P.dr
+            lo, hi = P.lo, P.hi
+            viol = np.maximum(np.where(np.isfinite(lo), lo - Az, 0), 0) + np.maximum(np.where(np.isfinite(hi), Az - hi, 0), 0)
+            scale_r = np.maximum(np.maximum(1, np.maximum(np.where(np.isfinite(lo), abs(lo), 0), np.where(np.isfinite(hi), abs(hi), 0))), P.rowmax)
+            pres = np.max(viol / scale_r)
+            lb_val = P.lagrangian(yn)
+            gap = pobj - lb_val
+            if verbose:
+                print(f"{total:7d} pres={pres:.2e} p={pobj:.10g} L={lb_val:.10g} gap={gap:.2e} w={omega:.3g}")
+            if pres <= tol and gap <= tol * max(1.0, abs(lb_val)):
+                return zu, yn * P.dr, total, pobj, lb_val
+            fpr = np.sqrt(omega * np.sum((zn - z) ** 2) + np.sum((yn - y) ** 2) / omega)
+            if last_err is None:
+                last_err = fpr
+            restart = (fpr <= 0.2 * last_err) or (fpr <= 0.8 * last_err and fpr > prev_err) or (k_since >= 0.36 * total)
+            prev_err = fpr
+            if restart:
+                dz = np.linalg.norm(zn - z0)
+                dy = np.linalg.norm(yn - y0)
+                if dz > 1e-10 and dy > 1e-10:
+                    omega = np.exp(0.5 * np.log(dy / dz) + 0.5 * np.log(omega))
+                    omega = min(max(omega, OMIN), OMAX)
+                z0, y0 = zn.copy(), yn.copy()
+                z_next, y_next = zn, yn
+                k_since = 0
+                last_err = fpr
+                prev_err = np.inf
+        z, y = z_next, y_next
+    zu = zn * P.dc
+    return zu, yn * P.dr, total, P.c @ zu, P.lagrangian(yn)
+
+
+if __name__ == "__main__":
+    import argparse
+    from core.utils.synthetic import synthetic_payload
+    from oracle.inputs import data_to_solver_input
+    from oracle.formulation import build_model
+    from oracle.solve import solve as hsolve
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--N", type=int, default=16)
+    ap.add_argument("--F", type=int, default=8)
+    ap.add_argument("--rho", type=float, default=0.1)
+    ap.add_argument("--nodes", type=int, default=4)
+    ap.add_argument("--variant", default="MinDelayAndUtilization")
+    ap.add_argument("--scale", default="ruiz")
+    ap.add_argument("--tol", type=float, default=1e-7)
+    ap.add_argument("-v", action="store_true")
+    ap.add_argument("--omega0", type=float, default=None)
+    ap.add_argument("--plain", action="store_true")
+    ap.add_argument("--reflect", type=float, default=1.0)
+    ap.add_argument("--omin", type=float, default=1e-2)
+    ap.add_argument("--omax", type=float, default=1e2)
+    a = ap.parse_args()
+    OMEGA0, OMIN, OMAX = a.omega0, a.omin, a.omax
+    HALPERN = not a.plain
+    p = synthetic_payload(a.N, a.F, seed=1, rho=a.rho)
+    data = data_to_solver_input(p, with_db=False)
+    m = build_model(data, a.variant, step=1, alpha=0.5)
+    rng = np.random.default_rng(0)
+    L = m["layout"]
+    for t in range(a.nodes):
+        lb, ub = m["lb"].copy(), m["ub"].copy()
+        if t > 0:
+            nfix = rng.integers(1, 6)
+            idx = rng.choice(np.arange(L.c0, L.c0 + L.F * L.N), size=nfix, replace=False)
+            v = rng.integers(0, 2, size=nfix)
+            lb[idx] = v
+            ub[idx] = v
+        t0 = time.time()
+        st, ref, _ = hsolve(m, relax=True, lb=lb, ub=ub)
+        th = time.time() - t0
+        if ref is None:
+            print(f"node {t}: infeasible (HiGHS)")
+            continue
+        P = Prob(m, lb, ub, scale=a.scale)
+        t0 = time.time()
+        z, y, it, pobj, lval = solve(P, tol=a.tol, verbose=a.v, reflect=a.reflect)
+        print(f"node {t}: iters={it} p={pobj:.10g} L={lval:.10g} ref={ref:.10g} |L-ref|={abs(lval-ref):.1e} "
+              f"({time.time()-t0:.1f}s; highs {th:.2f}s)")
