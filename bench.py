@@ -1,0 +1,274 @@
+#!/usr/bin/env python3
+"""bench.py — LP-relaxations/sec (+ certified objective gap) on the synthetic 512-node x
+256-function NEPTUNE instance (BASELINE.json `metric`; generator of SURVEY.md §8(d)).
+
+Workload.  One *step* = one batch of B branch-and-bound node LP relaxations of the step-1
+NeptuneMinDelayAndUtilization model (reference `core/solvers/neptune/neptune_step1.py:67-77`,
+rows `neptune/utils/constraints_step1.py`, objective `neptune/utils/objectives.py:30-52`).
+Every node is a child of the root LP: it carries `--fix` seeded c[f,j] fixings (0 or 1, the
+branching decisions of a B&B) and is warm-started from the root's primal/dual state, as a B&B
+child is from its parent (`--cold` starts every node from zero instead).  A node counts only if
+the engine certifies it: primal objective - Lagrangian bound <= tol*max(1,|bound|) and every row
+residual <= tol.  The root LP is solved once before the timed region.  The
+instance tensors live on the device before the timer starts; node bounds are uploaded inside
+the step, as the B&B host does per node batch.
+
+Multi-GPU (`torch.distributed.run`, one rank per GPU): every rank holds the same instance and
+solves its own B nodes per step (subtree sharding); the only exchange is the
+B&B bound all-reduce(MIN) of 8 bytes per step.  value = certified LPs of all ranks / max-over-
+ranks wall time ("scaling": "weak").
+
+Roofline.  The dominant kernel is the fused routing-row pass `x_pass` (csrc/nep_kernels.hip).
+Its algorithmic bytes per LP iteration are 8*P (x read + x write, fp32), P = R*N routing entries
+after exact zero-workload source aggregation.  `achieved` = those bytes x the LPs one sampled
+launch carries / that launch's HIP-event duration on the engine's own stream, averaged over one
+steady-state launch per 64-iteration block (nep_get_stats).  `traffic` is read from
+profiles/traffic.json (a separate rocprofv3 --pmc pass) when it was measured on
+this exact workload, else null.
+
+CPU baseline.  The oracle (HiGHS on the reference's formulation restated as one CSR, oracle/)
+timed on rank 0's host, bounded by `--cpu-budget` seconds (see `cpu_baseline`).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(REPO, "neptune-mip_amd")
+for _p in (PKG, REPO):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md "HBM")
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--nodes", type=int, default=512)
+    ap.add_argument("--functions", type=int, default=256)
+    ap.add_argument("--batch", type=int, default=16, help="node LPs per step per GPU")
+    ap.add_argument("--fix", type=int, default=2, help="c[f,j] fixings per node LP")
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--tol", type=float, default=1e-6)
+    ap.add_argument("--max-iters", type=int, default=200000)
+    ap.add_argument("--check-every", type=int, default=64)
+    ap.add_argument("--cold", action="store_true", help="cold-start every node LP")
+    ap.add_argument("--cpu-budget", type=float, default=25.0, help="seconds for the CPU baseline (0 = skip)")
+    ap.add_argument("--traffic", default=os.path.join(REPO, "profiles", "traffic.json"))
+    return ap.parse_args()
+
+
+def log(msg):
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
+def node_bounds(n_int, F, N, B, k, seed):
+    """B children of the root: k distinct c[f,j] fixed to 0/1 each (seeded)."""
+    import numpy as np
+    rng = np.random.default_rng(seed)
+    lb = np.full((B, n_int), -np.inf)
+    ub = np.full((B, n_int), np.inf)
+    for b in range(B):
+        idx = rng.choice(F * N, size=k, replace=False)
+        val = rng.integers(0, 2, size=k).astype(np.float64)
+        lb[b, idx] = val
+        ub[b, idx] = val
+    return lb, ub
+
+
+def cpu_baseline(N, F, seed, fix, budget):
+    """The reference formulation of the same generator, solved by the oracle (HiGHS LP, one thread).
+
+    The literal reference model at 512x256 has 67 M columns and 269 M nonzeros: building it alone
+    exceeds any bounded budget.  So the sample is the same node-LP workload
+    (same generator, same kind of fixings) at growing sizes until the budget is spent; the
+    measured times are fitted as t ~ (N^2 F)^p and extrapolated to the benchmark size.  The
+    measured points are reported in `sample`."""
+    import numpy as np
+    from oracle.formulation import build_model
+    from oracle.inputs import data_to_solver_input as oracle_input
+    from oracle.solve import solve as oracle_solve
+    from core.utils.synthetic import synthetic_payload
+
+    pts = []
+    spent = 0.0
+    for n in (16, 24, 32, 48, 64, 96, 128):
+        f = max(1, n // 2)
+        t0 = time.perf_counter()
+        p = synthetic_payload(n, f, seed=seed)
+        d = oracle_input(p, workload_coeff=1, with_db=False)
+        m = build_model(d, "MinDelayAndUtilization", step=1, alpha=p["solver"]["args"]["alpha"])
+        nx = n * n * f
+        lb, ub = node_bounds(f * n + n, f, n, 1, fix, seed=seed)
+        rl, ru = m["lb"].copy(), m["ub"].copy()
+        fin = np.isfinite(lb[0])
+        rl[nx:][fin] = lb[0][fin]
+        ru[nx:][fin] = ub[0][fin]
+        t1 = time.perf_counter()
+        st, obj, _ = oracle_solve(m, relax=True, lb=rl, ub=ru)
+        t_lp = time.perf_counter() - t1
+        spent += time.perf_counter() - t0
+        pts.append((n, f, t_lp, st))
+        log(f"cpu baseline: {n}x{f} node LP by HiGHS in {t_lp:.2f}s (status {st})")
+        # the next size costs roughly 2^3-3.4x: stop before the budget would be exceeded
+        if spent + 4.0 * (time.perf_counter() - t0) > budget:
+            break
+    xs = np.log([a * a * b for a, b, _, _ in pts[-3:]])
+    ys = np.log([t for _, _, t, _ in pts[-3:]])
+    p_exp = float(np.polyfit(xs, ys, 1)[0]) if len(pts) >= 2 else 1.0
+    n_l, f_l, t_l, _ = pts[-1]
+    t_ext = t_l * ((N * N * F) / (n_l * n_l * f_l)) ** p_exp
+    sample = ("HiGHS (oracle/solve.py, scipy %s) on the reference formulation (oracle/formulation.py), "
+              "1 thread, one node LP with %d c-fixings per size, same generator; measured %s; "
+              "fit t ~ (N^2 F)^%.2f over the last %d sizes, extrapolated to %dx%d (%.0f s per LP)"
+              % (__import__("scipy").__version__, fix,
+                 ", ".join(f"{a}x{b}: {t:.2f}s" for a, b, t, _ in pts), p_exp, min(3, len(pts)), N, F, t_ext))
+    return {"value": 1.0 / t_ext, "unit": "LP-relaxations/s", "cores": 1, "kind": "port", "sample": sample,
+            "extrapolated": True, "measured": [{"nodes": a, "functions": b, "seconds": t, "status": s}
+                                               for a, b, t, s in pts]}
+
+
+def main():
+    a = parse()
+    import numpy as np
+    import torch
+
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local = int(os.environ.get("LOCAL_RANK", 0))
+    dist = world > 1
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if dist:
+        import torch.distributed as td
+        td.init_process_group("nccl", device_id=dev)
+
+    from core.engine.lp import LPModel, LP_OPTIMAL
+    from core.utils import data_to_solver_input
+    from core.utils.synthetic import synthetic_payload
+
+    N, F, B = a.nodes, a.functions, a.batch
+    payload = synthetic_payload(N, F, seed=a.seed)
+    data = data_to_solver_input(payload, with_db=False)
+    alpha = payload["solver"]["args"]["alpha"]
+    root = B
+    t_build = time.perf_counter()
+    m = LPModel(data, "MinDelayAndUtilization", step=1, alpha=alpha, max_batch=B + 1)
+    log(f"rank {rank}: model {N}x{F}: R={m.info.n_rows} rows, P={m.info.x_entries} routing entries, "
+        f"{m.info.n_tiles} tiles, built in {time.perf_counter() - t_build:.1f}s")
+    P = m.info.x_entries
+    t_root = time.perf_counter()
+    rr = m.solve([root], tol=a.tol, max_iters=a.max_iters, check_every=a.check_every)
+    root_obj, root_status, root_iters = float(rr["obj"][0]), int(rr["status"][0]), int(rr["iters"][0])
+    log(f"rank {rank}: root LP status {root_status} obj {root_obj:.10g} after {root_iters} iterations "
+        f"({time.perf_counter() - t_root:.2f}s)")
+    if root_status != LP_OPTIMAL:
+        raise RuntimeError(f"root LP not certified: status {root_status} after {root_iters} iterations")
+
+    def step(s):
+        lb, ub = node_bounds(m.n_int, F, N, B, a.fix, seed=(a.seed * 1000003 + rank) * 7919 + s)
+        if not a.cold:
+            for b in range(B):
+                m.copy_state(root, b)
+        r = m.solve(np.arange(B), lb, ub, tol=a.tol, max_iters=a.max_iters, check_every=a.check_every,
+                    warm_start=not a.cold)
+        best = torch.tensor([float(np.min(r["obj"]))], dtype=torch.float64, device=dev)
+        if dist:
+            td.all_reduce(best, op=td.ReduceOp.MIN)     # B&B bound exchange (8 B)
+        ok = r["status"] == LP_OPTIMAL
+        gap = np.abs(r["primal_obj"] - r["obj"]) / np.maximum(1.0, np.abs(r["obj"]))
+        return int(ok.sum()), int(r["iters"].sum()), float(np.max(np.where(ok, gap, 0.0))), r
+
+    for s in range(a.warmup):
+        k, it, _, _ = step(-1 - s)
+        log(f"rank {rank}: warmup step {s}: {k}/{B} certified, {it} iterations")
+    m.reset_stats()
+    if dist:
+        td.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    n_ok = n_it = 0
+    gmax = 0.0
+    statuses = []
+    for s in range(a.steps):
+        k, it, g, r = step(s)
+        n_ok += k
+        n_it += it
+        gmax = max(gmax, g)
+        statuses += r["status"].tolist()
+        log(f"rank {rank}: step {s}: {k}/{B} certified, {it} iterations, {time.perf_counter() - t0:.2f}s")
+    torch.cuda.synchronize()
+    if dist:
+        td.barrier()
+    wall = time.perf_counter() - t0
+    st = m.stats()
+
+    tot = torch.tensor([wall, n_ok, n_it, gmax], dtype=torch.float64, device=dev)
+    if dist:
+        mx = tot.clone()
+        td.all_reduce(mx, op=td.ReduceOp.MAX)
+        sm = tot.clone()
+        td.all_reduce(sm, op=td.ReduceOp.SUM)
+        wall, gmax = float(mx[0]), float(mx[3])
+        n_ok, n_it = int(sm[1]), int(sm[2])
+    if rank != 0:
+        m.close()
+        if dist:
+            td.destroy_process_group()
+        return
+
+    per_lp = 8.0 * P                                     # x read + write, fp32
+    launch_ms = st["x_pass_ms"] / max(1, st["x_pass_sampled"])
+    lps_per_launch = st["x_pass_lp_iters"] / max(1, st["x_pass_sampled"])
+    achieved = per_lp * lps_per_launch / (launch_ms * 1e-3) / 1e9 if launch_ms > 0 else 0.0
+    workload = f"synthetic_{N}x{F}_step1_MDU_bnb_children_B{B}_fix{a.fix}_{'cold' if a.cold else 'warm'}"
+    traffic = None
+    if os.path.exists(a.traffic):
+        with open(a.traffic) as fh:
+            t = json.load(fh)
+        if t.get("workload") == workload:
+            traffic = t.get("bytes_per_launch")
+    cpu = None
+    if world == 1 and a.cpu_budget > 0:
+        cpu = cpu_baseline(N, F, a.seed, a.fix, a.cpu_budget)
+    attempted = len(statuses) * world
+    out = {
+        "metric": "LP-relaxations/sec + objective gap vs reference, 512-node×256-function",
+        "value": n_ok / wall,
+        "unit": "LP-relaxations/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": wall / a.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32 x-state, f64 duals/reductions/certificate",
+        "data": "synthetic (SURVEY.md §8(d) generator, seed %d)" % a.seed,
+        "config": {"workload": workload, "nodes": N, "functions": F, "lp_per_step_per_gpu": B,
+                   "fixings_per_lp": a.fix, "tol": a.tol, "routing_entries_P": P,
+                   "parallelism": f"bnb-subtrees x{world}"},
+        "objective_gap": {"certified_max": gmax, "tol": a.tol,
+                          "note": "(primal obj - Lagrangian bound)/max(1,|bound|) per certified LP; "
+                                  "HiGHS parity on the reference's own models: tests/test_gpu_lp.py"},
+        "lp": {"certified": n_ok, "attempted": attempted, "iterations": n_it,
+               "mean_iters": n_it / max(1, attempted), "root_obj": root_obj, "root_iters": root_iters},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "kernel": "x_pass", "algorithmic_bytes_per_launch": per_lp * lps_per_launch,
+                     "avg_launch_ms": launch_ms, "sampled_launches": st["x_pass_sampled"]},
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(out), flush=True)
+    m.close()
+    if dist:
+        td.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,227 @@
+"""Batched best-first branch-and-bound over the MI355X LP engine.
+
+This is the tree search SCIP runs inside `pywraplp.Solver.Solve()` (reference
+`core/solvers/solver.py:35-40`) on the NEPTUNE step models, rebuilt around batched GPU LP
+relaxations: open nodes, heuristic completions and leaves are all LPs solved by `LPModel.solve`
+(nep_lp_solve_batch), up to `batch` of them per call.  The host keeps only the tree.
+
+Branching variables: the placement binaries c[f,j] and the node binaries n[j] of the engine's
+integer vector (include/neptune_lp.h).  moved_from / moved_to / allocated / deallocated follow
+from c — with c integral their LP optimum is integral — and are never branched on.
+
+Exactness:
+  * a node's value is the engine's certified Lagrangian bound, a valid lower bound even when PDHG
+    stopped at its iteration limit, so pruning never discards the optimum;
+  * an incumbent is only ever a *leaf* — every c and n fixed — whose LP the engine certified
+    optimal; with c and n fixed, that LP's optimum is the MIP objective of the placement;
+  * the search ends with the queue empty: the incumbent is optimal within `gap` (relative).
+"""
+import heapq
+import itertools
+import math
+import time
+
+import numpy as np
+
+from .lp import LP_CUTOFF, LP_INFEASIBLE, LP_OPTIMAL
+
+OPTIMAL, INFEASIBLE, LIMIT = "OPTIMAL", "INFEASIBLE", "LIMIT"
+
+
+class BnBResult:
+    """Outcome of one search: status, incumbent objective / integer vector / dense routing."""
+
+    def __init__(self):
+        self.status = INFEASIBLE
+        self.objective = None
+        self.z = None            # engine integer vector of the incumbent
+        self.x = None            # routing x[i][f][j] of the incumbent (float32)
+        self.bound = -math.inf   # best proven lower bound
+        self.nodes = 0
+        self.leaves = 0
+        self.lps = 0
+        self.lp_iterations = 0
+        self.unresolved = 0      # leaves whose LP hit the iteration limit (not used as incumbents)
+        self.seconds = 0.0
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k in ("status", "objective", "bound", "nodes", "leaves", "lps",
+                                              "lp_iterations", "unresolved", "seconds")}
+
+
+class BranchAndBound:
+    """Best-first B&B with batched node LPs.
+
+    lp            core.engine.lp.LPModel of the step model (max_batch >= batch)
+    workload      W [F, N] (to weigh the pooled zero-workload routing rows when computing flows)
+    fn_mem/node_mem  memory data for the rounding heuristic's capacity check (C3)
+    upper_bound   a-priori bound on any feasible objective: LPs whose Lagrangian exceeds it are
+                  stopped early (infeasible nodes have an unbounded Lagrangian)
+    """
+
+    def __init__(self, lp, workload, fn_mem, node_mem, batch=16, tol=1e-7, gap=1e-6, max_iters=100000,
+                 node_limit=20000, time_limit=None, upper_bound=math.inf, flow_tol=1e-4, log=None):
+        self.lp = lp
+        self.N, self.F = lp.N, lp.F
+        L = lp.layout()
+        self.c0, self.c1 = L["c"]
+        self.n_range = L["n"]
+        W = np.asarray(workload, np.float64).reshape(self.F, self.N)
+        self.zero_src = (W == 0).sum(axis=1).astype(np.float64)
+        self.fn_mem = np.asarray(fn_mem, np.float64).reshape(self.F)
+        self.node_mem = np.asarray(node_mem, np.float64).reshape(self.N)
+        self.batch = min(int(batch), lp.max_batch)
+        self.tol, self.gap, self.max_iters = tol, gap, max_iters
+        self.node_limit, self.time_limit = node_limit, time_limit
+        self.ub0 = upper_bound
+        self.flow_tol = flow_tol
+        self.log = log or (lambda *_: None)
+        self.branch_vars = list(range(self.c0, self.c1))
+        if self.n_range is not None:
+            self.branch_vars += list(range(*self.n_range))
+        self._nb = len(self.branch_vars)
+
+    # ---------------------------------------------------------------------------------------
+    def _gap_abs(self, inc):
+        return self.gap * max(1.0, abs(inc)) if math.isfinite(inc) else 0.0
+
+    def _flows(self, slot):
+        """flow[f, j] = sum over sources of x[i, f, j] (pooled rows weighted by their size)."""
+        xb, rf, rs = self.lp.rows(slot)
+        w = np.where(rs >= 0, 1.0, self.zero_src[rf])
+        flow = np.zeros((self.F, self.N))
+        np.add.at(flow, rf, w[:, None] * xb.astype(np.float64))
+        return flow
+
+    def _complete(self, fix):
+        return len(fix) >= self._nb
+
+    def _round(self, fix, flow):
+        """Heuristic completion of a node: c = 1 where fixed to 1 or carrying flow, n = any c.
+        Returns a full fixing dict, or None when it is visibly infeasible."""
+        F, N, c0 = self.F, self.N, self.c0
+        c = np.zeros(F * N)
+        free = np.ones(F * N, bool)
+        for k, v in fix.items():
+            if c0 <= k < self.c1:
+                c[k - c0] = v
+                free[k - c0] = False
+        c[free & (flow.ravel() > self.flow_tol)] = 1.0
+        cm = c.reshape(F, N)
+        if (cm.sum(axis=1) < 1).any():
+            return None
+        if ((self.fn_mem[:, None] * cm).sum(axis=0) > self.node_mem + 1e-9).any():
+            return None
+        leaf = {c0 + k: float(c[k]) for k in range(F * N)}
+        if self.n_range is not None:
+            n0 = self.n_range[0]
+            nv = (cm.sum(axis=0) >= 1).astype(np.float64)
+            for j in range(N):
+                if fix.get(n0 + j, nv[j]) != nv[j]:
+                    return None
+                leaf[n0 + j] = float(nv[j])
+        return leaf
+
+    def _branch_var(self, fix, z, flow):
+        """n[j] receiving flow (largest inflow), then c[f,j] carrying flow (largest), then any free
+        n / c by LP value.  None when every branching variable is fixed."""
+        F, N, c0 = self.F, self.N, self.c0
+        if self.n_range is not None:
+            n0 = self.n_range[0]
+            inflow = flow.sum(axis=0)
+            cand = [j for j in range(N) if (n0 + j) not in fix and inflow[j] > self.flow_tol]
+            if cand:
+                return n0 + max(cand, key=lambda j: (inflow[j], -j))
+        fl = flow.ravel()
+        cand = [k for k in range(F * N) if (c0 + k) not in fix and fl[k] > self.flow_tol]
+        if cand:
+            return c0 + max(cand, key=lambda k: (fl[k], -k))
+        free = [v for v in self.branch_vars if v not in fix]
+        if not free:
+            return None
+        return max(free, key=lambda v: (z[v], -v))
+
+    # ---------------------------------------------------------------------------------------
+    def solve(self):
+        t0 = time.time()
+        res = BnBResult()
+        lp, n_int = self.lp, self.lp.n_int
+        inc = math.inf
+        seq = itertools.count()
+        heap = [(-math.inf, 0, next(seq), {}, False)]   # (bound, -depth, seq, fixings, is_leaf)
+        pending_leaves = []
+        seen_leaves = set()
+        limit_hit = False
+        while heap or pending_leaves:
+            if res.nodes >= self.node_limit or (self.time_limit and time.time() - t0 > self.time_limit):
+                limit_hit = True
+                break
+            batch = []
+            while pending_leaves and len(batch) < self.batch:
+                batch.append((-math.inf, pending_leaves.pop(), True))
+            while heap and len(batch) < self.batch:
+                bnd, _, _, fix, is_leaf = heapq.heappop(heap)
+                if bnd >= inc - self._gap_abs(inc):
+                    continue
+                batch.append((bnd, fix, is_leaf))
+            if not batch:
+                continue
+            B = len(batch)
+            lb = np.full((B, n_int), -np.inf)
+            ub = np.full((B, n_int), np.inf)
+            for b, (_, fix, _) in enumerate(batch):
+                if fix:
+                    idx = np.fromiter(fix.keys(), np.int64, len(fix))
+                    val = np.fromiter(fix.values(), np.float64, len(fix))
+                    lb[b, idx] = val
+                    ub[b, idx] = val
+            cutoff = min(inc, self.ub0)
+            r = lp.solve(np.arange(B), lb, ub, tol=self.tol, max_iters=self.max_iters,
+                         cutoff=cutoff if math.isfinite(cutoff) else math.inf)
+            res.lps += B
+            res.lp_iterations += int(r["iters"].sum())
+            for b, (pbound, fix, is_leaf) in enumerate(batch):
+                st = int(r["status"][b])
+                if st in (LP_INFEASIBLE, LP_CUTOFF):
+                    continue
+                bound = max(pbound, float(r["obj"][b]))
+                if is_leaf:
+                    res.leaves += 1
+                    if st != LP_OPTIMAL:
+                        res.unresolved += 1
+                        continue
+                    val = float(r["primal_obj"][b])
+                    if val < inc - self._gap_abs(inc):
+                        inc = val
+                        res.objective = val
+                        res.z, res.x = lp.solution(b, dense_x=True)
+                        self.log(f"incumbent {val:.10g} (lps {res.lps}, nodes {res.nodes})")
+                    continue
+                if bound >= inc - self._gap_abs(inc):
+                    continue
+                res.nodes += 1
+                z, _ = lp.solution(b, dense_x=False)
+                flow = self._flows(b)
+                leaf = self._round(fix, flow)
+                if leaf is not None:
+                    key = tuple(sorted(k for k, v in leaf.items() if v > 0.5))
+                    if key not in seen_leaves:
+                        seen_leaves.add(key)
+                        pending_leaves.append(leaf)
+                var = self._branch_var(fix, z, flow)
+                if var is None:
+                    continue
+                for v in (1.0, 0.0):
+                    child = dict(fix)
+                    child[var] = v
+                    heapq.heappush(heap, (bound, -len(child), next(seq), child, self._complete(child)))
+        if heap:
+            res.bound = min(min(h[0] for h in heap), inc)
+        else:
+            res.bound = inc
+        if res.objective is None:
+            res.status = LIMIT if limit_hit else INFEASIBLE
+        else:
+            res.status = LIMIT if limit_hit else OPTIMAL
+        res.seconds = time.time() - t0
+        return res

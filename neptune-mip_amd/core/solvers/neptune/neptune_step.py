@@ -1,0 +1,207 @@
+"""NEPTUNE step models on the MI355X engine.
+
+Reference classes (same names, constructor keywords and side effects on `Data`):
+  NeptuneStepBase / NeptuneStep1CPU*     `core/solvers/neptune/neptune_step1.py:5-77`
+  NeptuneStep2Base / NeptuneStep2*       `core/solvers/neptune/neptune_step2.py:5-93`
+The reference enumerates the model row by row through pywraplp (`neptune/utils/variables.py`,
+`constraints_step1.py`, `constraints_step2.py`, `objectives.py`) and hands it to SCIP.  Here the
+same model is built structurally by the engine (`nep_model_create`, csrc/nep_host.cpp build(); row
+map in DESIGN.md §2) and solved by the batched GPU branch-and-bound (core/engine/bnb.py).
+
+results() returns the dense x[i][f][j] and c[f][j] matrices of the reference's
+`output_x_and_c` (`neptune/utils/output.py:5-15`); step 1 stores them in data.prev_x / prev_c
+(`neptune_step1.py:21-27`) and the utilisation variants data.prev_n (:55-60).
+"""
+import math
+
+import numpy as np
+
+from ...engine import lp as _lp
+from ...engine.bnb import OPTIMAL, BranchAndBound
+from ..solver import Solver
+
+
+def make_lp(data, variant, step, max_batch, **kw):
+    """The engine model of one step (indirection kept so tests can substitute the CPU oracle)."""
+    return _lp.LPModel(data, variant, step=step, max_batch=max_batch, **kw)
+
+
+class NeptuneStepBase(Solver):
+    VARIANT = None
+
+    def __init__(self, batch=16, node_limit=20000, time_limit=None, lp_tol=1e-7, **kwargs):
+        super().__init__(**kwargs)
+        self.batch = batch
+        self.node_limit = node_limit
+        self.time_limit = time_limit
+        self.lp_tol = lp_tol
+        self.result = None
+        self.x_matrix = None
+        self.c_matrix = None
+        self.n_vector = None
+
+    # the model is structured: nothing to enumerate (reference variables.py / constraints_*.py)
+    def init_vars(self):
+        pass
+
+    def init_constraints(self):
+        pass
+
+    def init_objective(self):
+        pass
+
+    def step_id(self):
+        return _lp.STEP1
+
+    def model_kwargs(self):
+        return {}
+
+    def upper_bound(self):
+        return math.inf
+
+    def solve(self):
+        self.init_objective()
+        data = self.data
+        N, F = len(data.nodes), len(data.functions)
+        model = make_lp(data, self.VARIANT, self.step_id(), self.batch, **self.model_kwargs())
+        try:
+            ub = self.upper_bound()
+            bnb = BranchAndBound(model, data.workload_matrix, data.function_memory_matrix, data.node_memory_matrix,
+                                 batch=self.batch, tol=self.lp_tol, node_limit=self.node_limit,
+                                 time_limit=self.time_limit,
+                                 upper_bound=ub * (1 + 1e-6) + 1e-6 if math.isfinite(ub) else ub, log=self.log)
+            res = bnb.solve()
+            layout = model.layout()
+        finally:
+            model.close()
+        self.result = res
+        if res.objective is not None:
+            self._value = float(res.objective)
+            self.x_matrix = np.asarray(res.x, np.float64)
+            c0, c1 = layout["c"]
+            self.c_matrix = np.asarray(res.z[c0:c1], np.float64).reshape(F, N)
+            if layout.get("n") is not None:
+                self.n_vector = np.asarray(res.z[layout["n"][0]:layout["n"][1]], np.float64)
+        else:
+            # no feasible placement: the reference reads zeros back from the failed solve
+            self._value = 0.0
+            self.x_matrix = np.zeros((N, F, N))
+            self.c_matrix = np.zeros((F, N))
+            self.n_vector = np.zeros(N)
+        self.log(f"Problem solved with status {res.status} and value {self._value} "
+                 f"({res.nodes} nodes, {res.lps} LPs, {res.seconds:.2f}s)")
+        return res.status == OPTIMAL
+
+    def results(self):
+        self.data.prev_x = self.x_matrix
+        self.data.prev_c = self.c_matrix
+        return self.x_matrix, self.c_matrix
+
+
+def _max_delay_per_source(data):
+    D = np.asarray(data.node_delay_matrix, np.float64)
+    return D.max(axis=1)
+
+
+class NeptuneStep1CPUBase(NeptuneStepBase):
+    pass
+
+
+class NeptuneStep1CPUMinUtilization(NeptuneStep1CPUBase):
+    VARIANT = "MinUtilization"
+
+    def upper_bound(self):
+        return float(len(self.data.nodes))
+
+    def results(self):
+        x, c = super().results()
+        self.data.prev_n = self.n_vector
+        return x, c
+
+
+class NeptuneStep1CPUMinDelay(NeptuneStep1CPUBase):
+    VARIANT = "MinDelay"
+
+    def upper_bound(self):
+        W = np.asarray(self.data.workload_matrix, np.float64)
+        return float((W * _max_delay_per_source(self.data)[None, :]).sum())
+
+
+class NeptuneStep1CPUMinDelayAndUtilization(NeptuneStep1CPUMinUtilization):
+    VARIANT = "MinDelayAndUtilization"
+
+    def __init__(self, alpha=0.5, **kwargs):
+        super().__init__(**kwargs)
+        self.alpha = alpha
+
+    def load_data(self, data):
+        data.alpha = self.alpha
+        super().load_data(data)
+
+    def model_kwargs(self):
+        return {"alpha": self.alpha}
+
+    def upper_bound(self):
+        W = np.asarray(self.data.workload_matrix, np.float64)
+        D = np.asarray(self.data.node_delay_matrix, np.float64)
+        md = np.asarray(self.data.max_delay_matrix, np.float64)
+        ub = float(self.alpha)
+        if W.sum():
+            mwd = sum(W[f, i] * max(d for d in D[i] if d <= md[f])
+                      for f in range(W.shape[0]) for i in range(W.shape[1]))
+            if mwd > 0:
+                ub += (1 - self.alpha) * float((W * D.max(axis=1)[None, :]).sum()) / mwd
+        return ub
+
+
+class NeptuneStep2Base(NeptuneStepBase):
+    def __init__(self, mode=str, soften_step1_sol=1.3, **kwargs):
+        super().__init__(**kwargs)
+        self.mode = mode
+        assert mode in ["delete", "create"]
+        self.soften_step1_sol = soften_step1_sol
+
+    def step_id(self):
+        return _lp.STEP2_DELETE if self.mode == "delete" else _lp.STEP2_CREATE
+
+    def model_kwargs(self):
+        d = self.data
+        kw = {"soften_step1_sol": self.soften_step1_sol, "max_score": float(getattr(d, "max_score", 0.0) or 0.0)}
+        prev = getattr(d, "prev_x", None)
+        if prev is not None and np.size(prev):
+            # constraints_step2.py:66-68: sum D[i,j] W[f,i] prev_x[i,f,j]
+            D = np.asarray(d.node_delay_matrix, np.float64)
+            W = np.asarray(d.workload_matrix, np.float64)
+            kw["prev_network_delay"] = float(np.einsum("ij,fi,ifj->", D, W, np.asarray(prev, np.float64)))
+        return kw
+
+    def upper_bound(self):
+        # minimize_disruption (objectives.py:55-63): w * sum(moved) with at most one move per (f, j),
+        # allocated / deallocated <= 0
+        FN = len(self.data.nodes) * len(self.data.functions)
+        return float(FN) * FN
+
+    def results(self):
+        # neptune_step2.py:43-51: no side effects on data (the prints are logs only)
+        return self.x_matrix, self.c_matrix
+
+
+class NeptuneStep2MinUtilization(NeptuneStep2Base):
+    VARIANT = "MinUtilization"
+
+
+class NeptuneStep2MinDelay(NeptuneStep2Base):
+    VARIANT = "MinDelay"
+
+
+class NeptuneStep2MinDelayAndUtilization(NeptuneStep2MinUtilization):
+    VARIANT = "MinDelayAndUtilization"
+
+    def __init__(self, alpha=0.5, **kwargs):
+        super().__init__(**kwargs)
+        self.alpha = alpha
+
+    def model_kwargs(self):
+        kw = super().model_kwargs()
+        kw["alpha"] = self.alpha
+        return kw

@@ -19,13 +19,13 @@
 
 namespace nep {
 hipError_t launch_x_pass(const DeviceView &v, const int32_t *slots, int nslots, bool check, bool init, bool first,
-                         hipStream_t s);
+                         bool plain, int it, hipStream_t s);
 hipError_t launch_small_passes(const DeviceView &v, const int32_t *slots, int nslots, bool check, bool init,
-                               bool first, hipStream_t s);
+                               bool first, bool plain, int it, hipStream_t s);
 hipError_t launch_scalar_pass(const DeviceView &v, const int32_t *slots, int nslots, bool check, bool init,
-                              bool first, int iters_done, hipStream_t s);
+                              bool first, bool plain, int it, int iters_done, int block_len, hipStream_t s);
 hipError_t launch_init_slot(const DeviceView &v, const int32_t *slots, int nslots, bool warm, double eta,
-                            hipStream_t s);
+                            double omega0, hipStream_t s);
 }  // namespace nep
 
 using namespace nep;
@@ -68,7 +68,12 @@ struct Model {
   std::vector<double> nat_lb, nat_ub, cost_int;
   std::vector<double> lo, hi, rownorm, rho, gam;
   std::vector<double> mem_f;
-  double eta = 0, sigma_max = 0;
+  // non-x part of K (COO) and, per function, the total routed flow (= N sources x 1): kept for the
+  // per-node row-activity test of presolve()
+  std::vector<int> Kr, Kc;
+  std::vector<double> Kv, ftot;
+  bool x_coef_nonneg = true;   // every x coefficient outside C1/C2 is >= 0 (W, cpr, D >= 0)
+  double eta = 0, sigma_max = 0, omega0 = 1.0;
   // device
   hipStream_t stream = nullptr;
   bool own_stream = false;
@@ -378,6 +383,14 @@ int build(Model &m, const nep_model_desc &d) {
     m.rownorm[k] = rn;
   }
   for (size_t e = 0; e < K.v.size(); ++e) m.rownorm[K.r[e]] = std::max(m.rownorm[K.r[e]], std::fabs(K.v[e]));
+  m.Kr = K.r;
+  m.Kc = K.c;
+  m.Kv = K.v;
+  m.ftot.assign(F, 0.0);
+  for (int r = 0; r < m.R; ++r) m.ftot[m.row_f[r]] += m.row_m[r];
+  for (size_t k = 0; k < (size_t)N * N && m.x_coef_nonneg; ++k) m.x_coef_nonneg = D[k] >= 0.0;
+  for (size_t k = 0; k < (size_t)F * N && m.x_coef_nonneg; ++k)
+    m.x_coef_nonneg = m.W[k] >= 0.0 && !(cpr[k] < 0.0);
 
   // Ruiz equilibration (10 sweeps, inf-norm) + Pock-Chambolle (alpha = 1) on rows and the
   // non-x columns; x columns keep scale 1 so every routing row stays a plain simplex.
@@ -456,6 +469,30 @@ int build(Model &m, const nep_model_desc &d) {
     m.sigma_max = std::sqrt(std::max(lam, 1e-30));
     m.eta = 0.95 / m.sigma_max;
   }
+
+  // initial primal weight (PDLP): ||c~||_2 / ||b~||_2 in the scaled space.  The NEPTUNE objectives
+  // are tiny per unit of flow (e.g. (1-alpha) W D / MWD ~ 1e-4, objectives.py:30-52) while the row
+  // bounds are node capacities ~1e2, so the balanced weight is far below 1; starting at 1 costs
+  // tens of thousands of iterations before the restarts find it.
+  {
+    double cn2 = 0.0, bn2 = 0.0;
+    for (int r = 0; r < m.R; ++r) {
+      const int src = m.row_src[r];
+      if (src < 0 || m.row_wobj[r] == 0.f) continue;
+      for (int j = 0; j < N; ++j) {
+        const double cx = (double)m.row_wobj[r] * D[(size_t)src * N + j];
+        cn2 += m.row_m[r] * cx * cx;
+      }
+    }
+    for (int k = 0; k < il.n_int; ++k) cn2 += std::pow(m.gam[k] * m.cost_int[k], 2);
+    for (int k = 0; k < o; ++k) {
+      double b = 0.0;
+      if (std::isfinite(m.lo[k])) b = std::max(b, std::fabs(m.lo[k]));
+      if (std::isfinite(m.hi[k])) b = std::max(b, std::fabs(m.hi[k]));
+      bn2 += std::pow(m.rho[k] * b, 2);
+    }
+    m.omega0 = (cn2 > 0.0 && bn2 > 0.0) ? std::sqrt(cn2) / std::sqrt(bn2) : 1.0;
+  }
   return NEP_OK;
 }
 
@@ -532,6 +569,7 @@ int setup_dense(Model &m, const nep_model_desc &d) {
   if ((rc = dalloc(m, &v.y, (size_t)B * v.sdual))) return rc;
   if ((rc = dalloc(m, &v.ya, (size_t)B * v.sdual))) return rc;
   if ((rc = dalloc(m, &v.kz, (size_t)B * v.sdual))) return rc;
+  if ((rc = dalloc(m, &v.kza, (size_t)B * v.sdual))) return rc;
   if ((rc = dalloc(m, &v.kty, (size_t)B * v.skty))) return rc;
   if ((rc = dalloc(m, &v.part, (size_t)B * v.spart))) return rc;
   if ((rc = dalloc(m, &v.tpart, (size_t)B * v.stpart))) return rc;
@@ -576,7 +614,39 @@ bool presolve(const Model &m, const double *lbi, const double *ubi, std::vector<
     }
     if (cnt == 0) ok = false;   // every routing row of f would be empty (C4 infeasible)
   }
-  return ok;
+  if (!ok) return false;
+  // row-activity test over the node's box: the activity range of each dualised row, from the
+  // small variables' bounds and the x part's range (flow into (f, j) is in [0, N] when j is
+  // allowed for f, else 0; the CPU and score rows have non-negative x coefficients).  A row whose
+  // range misses [lo, hi] proves the node LP infeasible — e.g. step-2 delete mode with more fixed
+  // placements than the old allocation (constraints_step2.py:36-44), memory over-committed by
+  // fixed placements (constraints_step1.py:18-23), an open node with every placement closed (:69-78).
+  const int o = m.dl.n_dual;
+  std::vector<double> amin(o, 0.0), amax(o, 0.0);
+  for (int f = 0; f < F; ++f)
+    for (int j = 0; j < N; ++j) {
+      const double fx = mask[(size_t)f * NP + j] ? m.ftot[f] : 0.0;
+      amax[m.dl.o1 + f * N + j] += fx;
+      amax[m.dl.o2 + f * N + j] += fx;
+    }
+  for (int j = 0; j < N; ++j) {
+    amax[m.dl.o5 + j] = INF;
+    if (!m.x_coef_nonneg) amin[m.dl.o5 + j] = -INF;
+  }
+  if (m.step2) {
+    amax[m.dl.oS] = INF;
+    if (!m.x_coef_nonneg) amin[m.dl.oS] = -INF;
+  }
+  for (size_t e = 0; e < m.Kv.size(); ++e) {
+    const double a = m.Kv[e] * lb[m.Kc[e]], b = m.Kv[e] * ub[m.Kc[e]];
+    amin[m.Kr[e]] += std::min(a, b);
+    amax[m.Kr[e]] += std::max(a, b);
+  }
+  for (int k = 0; k < o; ++k) {
+    if (amin[k] > m.hi[k] + 1e-9 * std::max(1.0, std::fabs(m.hi[k]))) return false;
+    if (amax[k] < m.lo[k] - 1e-9 * std::max(1.0, std::fabs(m.lo[k]))) return false;
+  }
+  return true;
 }
 
 int solve_batch(Model &m, int B, const int32_t *slots, const double *lbi, const double *ubi, const nep_lp_opts *opts,
@@ -624,37 +694,46 @@ int solve_batch(Model &m, int B, const int32_t *slots, const double *lbi, const 
   if (!act.empty()) {
     HIPCHK(hipMemcpyAsync(m.d_slots, act.data(), act.size() * sizeof(int32_t), hipMemcpyHostToDevice, m.stream));
     const int na = (int)act.size();
-    HIPCHK(launch_init_slot(v, m.d_slots, na, o.warm_start != 0, m.eta, m.stream));
-    HIPCHK(launch_x_pass(v, m.d_slots, na, false, true, true, m.stream));
-    HIPCHK(launch_small_passes(v, m.d_slots, na, false, true, true, m.stream));
-    HIPCHK(launch_scalar_pass(v, m.d_slots, na, false, true, true, 0, m.stream));
+    HIPCHK(launch_init_slot(v, m.d_slots, na, o.warm_start != 0, m.eta, m.omega0, m.stream));
+    HIPCHK(launch_x_pass(v, m.d_slots, na, false, true, true, true, 0, m.stream));
+    HIPCHK(launch_small_passes(v, m.d_slots, na, false, true, true, true, 0, m.stream));
+    HIPCHK(launch_scalar_pass(v, m.d_slots, na, false, true, true, true, 0, 0, o.check_every, m.stream));
   }
   std::vector<Ctrl> ctrl(m.max_batch);
+  // Block of `ce` iterations: it == 0 is the certificate iteration (a plain PDHG step whose input
+  // dual is the previous block's plain output, so it satisfies the row sign constraints and its
+  // Lagrangian is a valid bound); restarts decided there take effect at it == 1; it == ce - 1 is
+  // plain again; the others are reflected Halpern steps.
   int64_t block_no = 0;
   while (!act.empty()) {
     const int na = (int)act.size();
     const int ce = o.check_every;
+    // one steady-state x-pass launch per block is bracketed by HIP events on the model's stream;
+    // the events are read after the block's own stream sync, so sampling adds no synchronisation
+    const int sample_it = ce >= 4 ? 2 : -1;
     for (int it = 0; it < ce; ++it) {
-      const bool first = it == 0, check = it == ce - 1;
-      const bool sample = first && (block_no % 4 == 0);
+      const bool check = it == 0, first = it == 1;
+      const bool plain = ce < 4 || it == 0 || it == ce - 1;
+      const bool sample = it == sample_it;
+      const int done = check ? (block_no == 0 ? 1 : ce) : 0;
       if (sample) HIPCHK(hipEventRecord(m.ev0, m.stream));
-      HIPCHK(launch_x_pass(v, m.d_slots, na, check, false, first, m.stream));
+      HIPCHK(launch_x_pass(v, m.d_slots, na, check, false, first, plain, it, m.stream));
       if (sample) HIPCHK(hipEventRecord(m.ev1, m.stream));
-      HIPCHK(launch_small_passes(v, m.d_slots, na, check, false, first, m.stream));
-      if (m.step2 || check) HIPCHK(launch_scalar_pass(v, m.d_slots, na, check, false, first, ce, m.stream));
+      HIPCHK(launch_small_passes(v, m.d_slots, na, check, false, first, plain, it, m.stream));
+      if (m.step2 || check)
+        HIPCHK(launch_scalar_pass(v, m.d_slots, na, check, false, first, plain, it, done, ce, m.stream));
       m.stats.x_pass_launches += 1;
-      if (sample) {
-        HIPCHK(hipEventSynchronize(m.ev1));
-        float ms = 0.f;
-        HIPCHK(hipEventElapsedTime(&ms, m.ev0, m.ev1));
-        m.stats.x_pass_ms += ms;
-        m.stats.x_pass_sampled += 1;
-        m.stats.x_pass_lp_iters += na;
-      }
     }
     ++block_no;
     HIPCHK(hipMemcpyAsync(ctrl.data(), v.ctrl, sizeof(Ctrl) * m.max_batch, hipMemcpyDeviceToHost, m.stream));
     HIPCHK(hipStreamSynchronize(m.stream));
+    if (sample_it >= 0) {
+      float ms = 0.f;
+      HIPCHK(hipEventElapsedTime(&ms, m.ev0, m.ev1));
+      m.stats.x_pass_ms += ms;
+      m.stats.x_pass_sampled += 1;
+      m.stats.x_pass_lp_iters += na;
+    }
     m.stats.lp_iterations += (int64_t)na * ce;
     std::vector<int32_t> still;
     for (int s : act)

@@ -8,7 +8,7 @@
 //   xa    [R][NP] f32   restart anchor of x
 //   mask  [F][NP] u8    destination j allowed for function f at this node (c_ub[f,j] > 0)
 //   zi    [n_int] f64   small primal: c, (mf, mt, a, d), n        + anchor zia, bounds lb/ub
-//   y     [n_dual] f64  duals of the dualised rows                + anchor ya, activity kz
+//   y     [n_dual] f64  duals of the dualised rows   + anchor ya, activity kz (iterate) / kza (anchor)
 //   kty   [F*NP + NP + 4] f32  packed duals the x pass needs: y1+y2 per (f,j), y5 per j, yS
 //   part  [T][2][NP] f32  per-tile partial column sums (C1/C2 activity) and CPU sums (C5)
 //   tpart [T][NTS] f64  per-tile scalars (score row, objective, Lagrangian, movement, distance)
@@ -44,7 +44,7 @@ struct Ctrl {
   double last_restart_fpr, prev_fpr;
   double pobj, lagr, best_lagr, pres, gap;
   double omega_lo, omega_hi;
-  int64_t k, k_since_restart, k_total_at_restart;
+  int64_t k, k_since_restart, ks_base;   // ks_base: Halpern counter at the block's first iteration
   int32_t status, active, restart_pending, pad;
 };
 
@@ -76,7 +76,7 @@ struct DeviceView {
   float *x, *xa;
   uint8_t *mask;
   double *zi, *zia, *lb, *ub;
-  double *y, *ya, *kz;
+  double *y, *ya, *kz, *kza;             // duals, anchor, activity K z of the iterate and of the anchor
   float *kty;
   float *part;
   double *tpart, *bpart, *npart;

@@ -1,11 +1,16 @@
 // nep_kernels.hip — gfx950 kernels of one PDHG iteration on a batch of NEPTUNE LP relaxations.
 //
-// Iteration (diagonally preconditioned PDHG, primal set keeps every routing row on its simplex):
-//   x̄'  = Π_simplex( x̄ − τ (cost_x − Kᵀ_x y) )          x_pass      (HBM-bound: x read + write)
-//   z'   = clip( z − τ γ² (cost_z − Kᵀ_z y) )             fj_pass / node_pass / scalar_pass
-//   y'   = prox( y − σ ρ² K(2·[x̄',z'] − [x̄,z]) )           fj_pass / node_pass / scalar_pass
-// K·[x̄', z'] is produced in the same passes that write x̄' and z' (column sums, CPU sums, score
-// row) and the previous activity is kept in `kz`, so K(2z'−z) = 2·Kz' − Kz costs no extra pass.
+// Iteration = one PDHG operator T (diagonally preconditioned; the primal set keeps every routing
+// row on its simplex), wrapped in reflected restarted Halpern iterations (r2HPDHG):
+//   x̂  = Π_simplex( x̄ − τ (cost_x − Kᵀ_x y) )           x_pass      (HBM-bound)
+//   ẑ  = clip( z − τ γ² (cost_z − Kᵀ_z y) )              fj_pass / node_pass / scalar_pass
+//   ŷ  = prox( y − σ ρ² K(2·[x̂,ẑ] − [x̄,z]) )             fj_pass / node_pass / scalar_pass
+//   w' = λ_k (2·T(w) − w) + (1 − λ_k) w_anchor,  λ_k = (k+1)/(k+2), k = iterations since restart
+// ("plain" iterations take w' = T(w): the certificate iteration and the one before it, so the
+// certificate's dual is a T output and satisfies the row sign constraints).
+// K·[x̂, ẑ] is produced in the same passes that write the iterate (column sums, CPU sums, score
+// row); the iterate's activity K w is kept in `kz` (and the anchor's in `kza`, K is linear), so
+// K(2ẑ − z) = 2·Kẑ − Kz costs no extra pass.
 //
 // Reference rows (core/solvers/neptune/utils): C1/C2 constraints_step1.py:5-15 (column sums),
 // C3 :18-23, C4 :27-34 (the simplex), C5 :57-65 (CPU), C6/C7 :69-78; step 2 D1-D4
@@ -70,7 +75,8 @@ __device__ __forceinline__ double row_viol(double a, double lo, double hi) {
 // reductions), writes x̄' and accumulates the tile's column sums for the C1/C2/C5 rows.
 // ---------------------------------------------------------------------------------------------
 template <int CPL, bool CHECK, bool INIT>
-__global__ __launch_bounds__(kTileThreads) void x_pass(DeviceView v, const int32_t *__restrict__ slots, int first) {
+__global__ __launch_bounds__(kTileThreads) void x_pass(DeviceView v, const int32_t *__restrict__ slots, int first,
+                                                       int plain, int it) {
   constexpr int E = 4 * CPL;
   extern __shared__ __attribute__((aligned(16))) float lds[];   // [2][kTileWaves][NP]
   __shared__ double lds_s[kTileWaves][NTS];
@@ -81,6 +87,12 @@ __global__ __launch_bounds__(kTileThreads) void x_pass(DeviceView v, const int32
   const int NP = v.NP, F = v.F;
   const float tau = INIT ? 0.f : (float)ctrl->tau;
   const bool restart = INIT || (first && ctrl->restart_pending);
+  const bool halp = !INIT && !plain;
+  float lam = 1.f;
+  if (halp) {
+    const double ks = (double)(ctrl->ks_base + it);
+    lam = (float)((ks + 1.0) / (ks + 2.0));
+  }
   const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x >> 6;
   const int f = v.tile_f[tile], row0 = v.tile_row0[tile], nrows = v.tile_nrows[tile];
   float *__restrict__ x = v.x + slot * v.sx;
@@ -182,30 +194,37 @@ __global__ __launch_bounds__(kTileThreads) void x_pass(DeviceView v, const int32
     for (int e = 0; e < E; ++e) xn[e] = mk[e] ? fmaxf(vv[e] - theta, 0.f) : 0.f;
 
     float *arow = xa + (int64_t)r * NP;
-    if (CHECK && !restart) {
-      double dd = 0.0;
+    // anchor row: needed by the Halpern combination and by the certificate's restart distance
+    float xav[E];
+    if ((halp || CHECK) && !restart) {
 #pragma unroll
       for (int q = 0; q < CPL; ++q) {
         const int j0 = 4 * (lane + kWave * q);
-        if (j0 < NP) {
-          const float4 a = *reinterpret_cast<const float4 *>(arow + j0);
-          const float av[4] = {a.x, a.y, a.z, a.w};
-#pragma unroll
-          for (int e = 0; e < 4; ++e) { const double t = (double)xn[4 * q + e] - av[e]; dd += t * t; }
-        }
+        float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (j0 < NP) a = *reinterpret_cast<const float4 *>(arow + j0);
+        xav[4 * q] = a.x; xav[4 * q + 1] = a.y; xav[4 * q + 2] = a.z; xav[4 * q + 3] = a.w;
       }
+    } else {
+#pragma unroll
+      for (int e = 0; e < E; ++e) xav[e] = INIT ? xn[e] : xv[e];
+    }
+    if (CHECK && !restart) {
+      double dd = 0.0;
+#pragma unroll
+      for (int e = 0; e < E; ++e) { const double t = (double)xn[e] - xav[e]; dd += t * t; }
       s_dist += dd;
     }
+    float xw[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) xw[e] = halp ? lam * (2.f * xn[e] - xv[e]) + (1.f - lam) * xav[e] : xn[e];
 #pragma unroll
     for (int q = 0; q < CPL; ++q) {
       const int j0 = 4 * (lane + kWave * q);
       if (j0 < NP) {
-        *reinterpret_cast<float4 *>(xrow + j0) = make_float4(xn[4 * q], xn[4 * q + 1], xn[4 * q + 2], xn[4 * q + 3]);
-        if (restart) {
-          const float *src4 = INIT ? xn : xv;
+        *reinterpret_cast<float4 *>(xrow + j0) = make_float4(xw[4 * q], xw[4 * q + 1], xw[4 * q + 2], xw[4 * q + 3]);
+        if (restart)
           *reinterpret_cast<float4 *>(arow + j0) =
-              make_float4(src4[4 * q], src4[4 * q + 1], src4[4 * q + 2], src4[4 * q + 3]);
-        }
+              make_float4(xav[4 * q], xav[4 * q + 1], xav[4 * q + 2], xav[4 * q + 3]);
       }
     }
     float sc = 0.f;
@@ -272,21 +291,53 @@ struct SmallAcc {
   double lagr = 0, pobj = 0, res = 0, mvz = 0, mvy = 0, dsz = 0, dsy = 0;
 };
 
+// Halpern weight of the current iteration for a slot (1 on plain iterations: w' = T(w))
+__device__ __forceinline__ double halpern_lambda(const Ctrl *ctrl, bool halp, int it) {
+  if (!halp) return 1.0;
+  const double ks = (double)(ctrl->ks_base + it);
+  return (ks + 1.0) / (ks + 2.0);
+}
+
+// Dual half-step of one row.  Returns the new *iterate* y'; `act` is the row activity at the T
+// output (K·[x̂, ẑ]).  On a Halpern iteration y' = λ(2ŷ − y) + (1 − λ)y_anchor and the iterate's
+// activity kz follows the same combination.
 template <bool CHECK, bool INIT>
-__device__ __forceinline__ double dual_step(const DeviceView &v, double *y, double *ya, double *kz, int row,
-                                            double act, double yold, double sigma, bool copy_anchor, SmallAcc &a) {
+__device__ __forceinline__ double dual_step(const DeviceView &v, double *y, double *ya, double *kz, double *kza,
+                                            int row, double act, double yold, double sigma, bool copy_anchor,
+                                            bool halp, double lam, SmallAcc &a) {
   const double lo = v.lo[row], hi = v.hi[row];
-  if (copy_anchor) ya[row] = yold;
-  double ynew = yold;
+  const double kold = kz[row];
+  double yanc, kanc;
+  if (INIT) {
+    yanc = yold;
+    kanc = act;
+  } else if (copy_anchor) {
+    yanc = yold;
+    kanc = kold;
+  } else {
+    yanc = ya[row];
+    kanc = kza[row];
+  }
+  if (copy_anchor) {
+    ya[row] = yanc;
+    kza[row] = kanc;
+  }
+  double ynew = yold, knew = act;
   if (!INIT) {
     const double rr = v.rho[row];
-    ynew = dual_prox(yold, sigma * rr * rr, 2.0 * act - kz[row], lo, hi);
-    y[row] = ynew;
-    const double t = (ynew - yold) / rr;
+    const double yT = dual_prox(yold, sigma * rr * rr, 2.0 * act - kold, lo, hi);
+    const double t = (yT - yold) / rr;
     a.mvy += t * t;
-    if (CHECK) { const double u = (ynew - ya[row]) / rr; a.dsy += u * u; }
+    if (CHECK) { const double u = (yT - yanc) / rr; a.dsy += u * u; }
+    if (halp) {
+      ynew = lam * (2.0 * yT - yold) + (1.0 - lam) * yanc;
+      knew = lam * (2.0 * act - kold) + (1.0 - lam) * kanc;
+    } else {
+      ynew = yT;
+    }
+    y[row] = ynew;
   }
-  kz[row] = act;
+  kz[row] = knew;
   if (CHECK) {
     a.lagr += row_lagr(yold, lo, hi);
     a.res = fmax(a.res, row_viol(act, lo, hi) / v.rownorm[row]);
@@ -294,19 +345,22 @@ __device__ __forceinline__ double dual_step(const DeviceView &v, double *y, doub
   return ynew;
 }
 
+// Primal half-step of one small variable.  Stores the new iterate, returns the T output ẑ (the
+// value every row activity and the certificate use).
 template <bool CHECK>
 __device__ __forceinline__ double primal_step(const DeviceView &v, double *zi, double *zia, const double *lb,
                                               const double *ub, int k, double rc, double tau, bool copy_anchor,
-                                              SmallAcc &a) {
+                                              bool halp, double lam, SmallAcc &a) {
   const double old = zi[k];
   if (copy_anchor) zia[k] = old;
+  const double zanc = copy_anchor ? old : zia[k];
   const double g = v.gam[k];
   const double nz = fmin(fmax(old - tau * g * g * rc, lb[k]), ub[k]);
-  zi[k] = nz;
+  zi[k] = halp ? lam * (2.0 * nz - old) + (1.0 - lam) * zanc : nz;
   const double t = (nz - old) / g;
   a.mvz += t * t;
   if (CHECK) {
-    const double u = (nz - zia[k]) / g;
+    const double u = (nz - zanc) / g;
     a.dsz += u * u;
     a.lagr += rc > 0 ? lb[k] * rc : ub[k] * rc;
     a.pobj += v.cost_int[k] * nz;
@@ -333,7 +387,8 @@ __device__ __forceinline__ void write_bpart(double *bp, const SmallAcc &a, doubl
 }
 
 template <bool CHECK, bool INIT>
-__global__ __launch_bounds__(kWave) void fj_pass(DeviceView v, const int32_t *__restrict__ slots, int first) {
+__global__ __launch_bounds__(kWave) void fj_pass(DeviceView v, const int32_t *__restrict__ slots, int first, int plain,
+                                                 int it) {
   const int jb = blockIdx.x, fb = blockIdx.y;
   const int slot = slots[blockIdx.z];
   Ctrl *ctrl = v.ctrl + slot;
@@ -346,9 +401,12 @@ __global__ __launch_bounds__(kWave) void fj_pass(DeviceView v, const int32_t *__
   const IntLayout &il = v.il;
   const double tau = INIT ? 0.0 : ctrl->tau, sigma = ctrl->sigma;
   const bool copy_anchor = INIT || (first && ctrl->restart_pending);
+  const bool halp = !INIT && !plain;
+  const double lam = halpern_lambda(ctrl, halp, it);
   double *zi = v.zi + slot * v.sint, *zia = v.zia + slot * v.sint;
   const double *lb = v.lb + slot * v.sint, *ub = v.ub + slot * v.sint;
   double *y = v.y + slot * v.sdual, *ya = v.ya + slot * v.sdual, *kz = v.kz + slot * v.sdual;
+  double *kza = v.kza + slot * v.sdual;
   float *kty = v.kty + slot * v.skty;
   const float *part = v.part + slot * v.spart;
   SmallAcc a;
@@ -376,16 +434,18 @@ __global__ __launch_bounds__(kWave) void fj_pass(DeviceView v, const int32_t *__
         kty_c += -yd1 + yd2 - yD3a + yD3b + v.sigma4 * yD4;
       }
       const double cn = primal_step<CHECK>(v, zi, zia, lb, ub, il.oc + idx, v.cost_int[il.oc + idx] - kty_c, tau,
-                                           copy_anchor, a);
-      const double y1n = dual_step<CHECK, INIT>(v, y, ya, kz, dl.o1 + idx, S - v.M * cn, y1, sigma, copy_anchor, a);
-      const double y2n = dual_step<CHECK, INIT>(v, y, ya, kz, dl.o2 + idx, S - cn, y2, sigma, copy_anchor, a);
+                                           copy_anchor, halp, lam, a);
+      const double y1n = dual_step<CHECK, INIT>(v, y, ya, kz, kza, dl.o1 + idx, S - v.M * cn, y1, sigma, copy_anchor,
+                                                halp, lam, a);
+      const double y2n = dual_step<CHECK, INIT>(v, y, ya, kz, kza, dl.o2 + idx, S - cn, y2, sigma, copy_anchor, halp,
+                                                lam, a);
       if (v.step2) {
         const double mfn = primal_step<CHECK>(v, zi, zia, lb, ub, il.omf + idx, v.cost_int[il.omf + idx] - yd1, tau,
-                                              copy_anchor, a);
+                                              copy_anchor, halp, lam, a);
         const double mtn = primal_step<CHECK>(v, zi, zia, lb, ub, il.omt + idx, v.cost_int[il.omt + idx] - yd2, tau,
-                                              copy_anchor, a);
-        dual_step<CHECK, INIT>(v, y, ya, kz, dl.oD1 + idx, mfn - cn, yd1, sigma, copy_anchor, a);
-        dual_step<CHECK, INIT>(v, y, ya, kz, dl.oD2 + idx, mtn + cn, yd2, sigma, copy_anchor, a);
+                                              copy_anchor, halp, lam, a);
+        dual_step<CHECK, INIT>(v, y, ya, kz, kza, dl.oD1 + idx, mfn - cn, yd1, sigma, copy_anchor, halp, lam, a);
+        dual_step<CHECK, INIT>(v, y, ya, kz, kza, dl.oD2 + idx, mtn + cn, yd2, sigma, copy_anchor, halp, lam, a);
       }
       memc += v.mem_f[f] * cn;
       sumc += cn;
@@ -401,7 +461,8 @@ __global__ __launch_bounds__(kWave) void fj_pass(DeviceView v, const int32_t *__
 
 // node_pass: one wave per (slot, block of 64 nodes j): rows C3 (memory), C5 (CPU), n, C6/C7.
 template <bool CHECK, bool INIT>
-__global__ __launch_bounds__(kWave) void node_pass(DeviceView v, const int32_t *__restrict__ slots, int first) {
+__global__ __launch_bounds__(kWave) void node_pass(DeviceView v, const int32_t *__restrict__ slots, int first,
+                                                   int plain, int it) {
   const int jb = blockIdx.x;
   const int slot = slots[blockIdx.y];
   Ctrl *ctrl = v.ctrl + slot;
@@ -414,9 +475,12 @@ __global__ __launch_bounds__(kWave) void node_pass(DeviceView v, const int32_t *
   const IntLayout &il = v.il;
   const double tau = INIT ? 0.0 : ctrl->tau, sigma = ctrl->sigma;
   const bool copy_anchor = INIT || (first && ctrl->restart_pending);
+  const bool halp = !INIT && !plain;
+  const double lam = halpern_lambda(ctrl, halp, it);
   double *zi = v.zi + slot * v.sint, *zia = v.zia + slot * v.sint;
   const double *lb = v.lb + slot * v.sint, *ub = v.ub + slot * v.sint;
   double *y = v.y + slot * v.sdual, *ya = v.ya + slot * v.sdual, *kz = v.kz + slot * v.sdual;
+  double *kza = v.kza + slot * v.sdual;
   float *kty = v.kty + slot * v.skty;
   SmallAcc a;
   double score_n = 0.0;
@@ -428,17 +492,18 @@ __global__ __launch_bounds__(kWave) void node_pass(DeviceView v, const int32_t *
       sumc += np_[(int64_t)fb * 3 * NP + NP + j];
       U += np_[(int64_t)fb * 3 * NP + 2 * NP + j];
     }
-    dual_step<CHECK, INIT>(v, y, ya, kz, dl.o3 + j, memc, y[dl.o3 + j], sigma, copy_anchor, a);
-    const double y5n = dual_step<CHECK, INIT>(v, y, ya, kz, dl.o5 + j, U, y[dl.o5 + j], sigma, copy_anchor, a);
+    dual_step<CHECK, INIT>(v, y, ya, kz, kza, dl.o3 + j, memc, y[dl.o3 + j], sigma, copy_anchor, halp, lam, a);
+    const double y5n = dual_step<CHECK, INIT>(v, y, ya, kz, kza, dl.o5 + j, U, y[dl.o5 + j], sigma, copy_anchor, halp,
+                                              lam, a);
     kty[(int64_t)F * NP + j] = (float)y5n;
     if (v.has_n) {
       const double y6 = y[dl.o6 + j], y7 = y[dl.o7 + j];
       const double yS = v.step2 ? y[dl.oS] : 0.0;
       const double kty_n = -v.M * y6 - y7 + v.score_n_coef * yS;
       const double nn = primal_step<CHECK>(v, zi, zia, lb, ub, il.on + j, v.cost_int[il.on + j] - kty_n, tau,
-                                           copy_anchor, a);
-      dual_step<CHECK, INIT>(v, y, ya, kz, dl.o6 + j, sumc - v.M * nn, y6, sigma, copy_anchor, a);
-      dual_step<CHECK, INIT>(v, y, ya, kz, dl.o7 + j, sumc - nn, y7, sigma, copy_anchor, a);
+                                           copy_anchor, halp, lam, a);
+      dual_step<CHECK, INIT>(v, y, ya, kz, kza, dl.o6 + j, sumc - v.M * nn, y6, sigma, copy_anchor, halp, lam, a);
+      dual_step<CHECK, INIT>(v, y, ya, kz, kza, dl.o7 + j, sumc - nn, y7, sigma, copy_anchor, halp, lam, a);
       score_n = v.score_n_coef * nn;
     }
   }
@@ -452,7 +517,7 @@ __global__ __launch_bounds__(kWave) void node_pass(DeviceView v, const int32_t *
 // ---------------------------------------------------------------------------------------------
 template <bool CHECK, bool INIT>
 __global__ __launch_bounds__(256) void scalar_pass(DeviceView v, const int32_t *__restrict__ slots, int first,
-                                                   int iters_done) {
+                                                   int plain, int it, int iters_done, int block_len) {
   __shared__ double red[256];
   __shared__ double tot[NTS + NBS];
   const int slot = slots[blockIdx.x];
@@ -490,8 +555,11 @@ __global__ __launch_bounds__(256) void scalar_pass(DeviceView v, const int32_t *
   double *zi = v.zi + slot * v.sint, *zia = v.zia + slot * v.sint;
   const double *lb = v.lb + slot * v.sint, *ub = v.ub + slot * v.sint;
   double *y = v.y + slot * v.sdual, *ya = v.ya + slot * v.sdual, *kz = v.kz + slot * v.sdual;
+  double *kza = v.kza + slot * v.sdual;
   const double tau = INIT ? 0.0 : ctrl->tau, sigma = ctrl->sigma;
   const bool copy_anchor = INIT || (first && ctrl->restart_pending);
+  const bool halp = !INIT && !plain;
+  const double lam = halpern_lambda(ctrl, halp, it);
   SmallAcc a;
   a.lagr = tot[TS_LAGR] + tot[NTS + BS_LAGR];
   a.pobj = tot[TS_POBJ] + tot[NTS + BS_POBJ];
@@ -507,13 +575,14 @@ __global__ __launch_bounds__(256) void scalar_pass(DeviceView v, const int32_t *
     const double yD3a = y[dl.oD3a], yD3b = y[dl.oD3b], yD4 = y[dl.oD4], yS = y[dl.oS];
     // allocated (a): D3a coef -1, D4 coef +1 ; deallocated (d): D3b coef -1, D4 coef +1
     const double an = primal_step<CHECK>(v, zi, zia, lb, ub, il.oa, v.cost_int[il.oa] - (-yD3a + yD4), tau,
-                                         copy_anchor, a);
+                                         copy_anchor, halp, lam, a);
     const double dn = primal_step<CHECK>(v, zi, zia, lb, ub, il.od, v.cost_int[il.od] - (-yD3b + yD4), tau,
-                                         copy_anchor, a);
-    dual_step<CHECK, INIT>(v, y, ya, kz, dl.oD3a, -sumc - an, yD3a, sigma, copy_anchor, a);
-    dual_step<CHECK, INIT>(v, y, ya, kz, dl.oD3b, sumc - dn, yD3b, sigma, copy_anchor, a);
-    dual_step<CHECK, INIT>(v, y, ya, kz, dl.oD4, dn + an + v.sigma4 * sumc, yD4, sigma, copy_anchor, a);
-    dual_step<CHECK, INIT>(v, y, ya, kz, dl.oS, score, yS, sigma, copy_anchor, a);
+                                         copy_anchor, halp, lam, a);
+    dual_step<CHECK, INIT>(v, y, ya, kz, kza, dl.oD3a, -sumc - an, yD3a, sigma, copy_anchor, halp, lam, a);
+    dual_step<CHECK, INIT>(v, y, ya, kz, kza, dl.oD3b, sumc - dn, yD3b, sigma, copy_anchor, halp, lam, a);
+    dual_step<CHECK, INIT>(v, y, ya, kz, kza, dl.oD4, dn + an + v.sigma4 * sumc, yD4, sigma, copy_anchor, halp, lam,
+                           a);
+    dual_step<CHECK, INIT>(v, y, ya, kz, kza, dl.oS, score, yS, sigma, copy_anchor, halp, lam, a);
     float *kty = v.kty + slot * v.skty;
     kty[(int64_t)v.F * v.NP + v.NP] = (float)y[dl.oS];
   }
@@ -521,6 +590,7 @@ __global__ __launch_bounds__(256) void scalar_pass(DeviceView v, const int32_t *
     ctrl->restart_pending = 0;
     ctrl->k = 0;
     ctrl->k_since_restart = 0;
+    ctrl->ks_base = -block_len;   // the first certificate iteration brings it to 0
     ctrl->last_restart_fpr = -1.0;
     ctrl->prev_fpr = INFINITY;
     return;
@@ -562,15 +632,18 @@ __global__ __launch_bounds__(256) void scalar_pass(DeviceView v, const int32_t *
       ctrl->tau = ctrl->eta / nw;
       ctrl->sigma = ctrl->eta * nw;
     }
-    ctrl->restart_pending = 1;   // consumed by the first passes of the next block
+    ctrl->restart_pending = 1;   // consumed by the passes of the block's next iteration (it == 1)
     ctrl->k_since_restart = 0;
+    ctrl->ks_base = -1;          // Halpern counter: 0 at the iteration that sets the anchor
     ctrl->last_restart_fpr = fpr;
     ctrl->prev_fpr = INFINITY;
+  } else {
+    ctrl->ks_base += block_len;
   }
 }
 
 // cold / warm initialisation of a slot (x̄ ← 0 for cold; the init passes project it)
-__global__ void init_slot(DeviceView v, const int32_t *__restrict__ slots, int warm, double eta) {
+__global__ void init_slot(DeviceView v, const int32_t *__restrict__ slots, int warm, double eta, double omega0) {
   const int slot = slots[blockIdx.y];
   Ctrl *ctrl = v.ctrl + slot;
   const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -590,10 +663,10 @@ __global__ void init_slot(DeviceView v, const int32_t *__restrict__ slots, int w
     zi[i] = fmin(fmax(z0, lb[i]), ub[i]);
   }
   if (tid == 0) {
-    if (!warm) ctrl->omega = 1.0;
+    if (!warm) ctrl->omega = omega0;
     ctrl->eta = eta;
-    ctrl->omega_lo = 1e-2;
-    ctrl->omega_hi = 1e2;
+    ctrl->omega_lo = omega0 * 1e-5;
+    ctrl->omega_hi = omega0 * 1e5;
     ctrl->tau = eta / ctrl->omega;
     ctrl->sigma = eta * ctrl->omega;
     ctrl->status = 1;
@@ -609,58 +682,61 @@ __global__ void init_slot(DeviceView v, const int32_t *__restrict__ slots, int w
 // ------------------------------------------------------------------------------------------
 template <int CPL>
 static hipError_t launch_x_cpl(const DeviceView &v, const int32_t *slots, int nslots, bool check, bool init,
-                               bool first, hipStream_t s) {
+                               bool first, bool plain, int it, hipStream_t s) {
   dim3 grid(v.T, nslots), block(kTileThreads);
   const size_t lds = (size_t)2 * kTileWaves * v.NP * sizeof(float);
-  const int fi = first ? 1 : 0;
-  if (init) hipLaunchKernelGGL((x_pass<CPL, false, true>), grid, block, lds, s, v, slots, fi);
-  else if (check) hipLaunchKernelGGL((x_pass<CPL, true, false>), grid, block, lds, s, v, slots, fi);
-  else hipLaunchKernelGGL((x_pass<CPL, false, false>), grid, block, lds, s, v, slots, fi);
+  const int fi = first ? 1 : 0, pl = plain ? 1 : 0;
+  if (init) hipLaunchKernelGGL((x_pass<CPL, false, true>), grid, block, lds, s, v, slots, fi, pl, it);
+  else if (check) hipLaunchKernelGGL((x_pass<CPL, true, false>), grid, block, lds, s, v, slots, fi, pl, it);
+  else hipLaunchKernelGGL((x_pass<CPL, false, false>), grid, block, lds, s, v, slots, fi, pl, it);
   return hipGetLastError();
 }
 
 hipError_t launch_x_pass(const DeviceView &v, const int32_t *slots, int nslots, bool check, bool init, bool first,
-                         hipStream_t s) {
+                         bool plain, int it, hipStream_t s) {
   switch (v.CPL) {
-    case 1: return launch_x_cpl<1>(v, slots, nslots, check, init, first, s);
-    case 2: return launch_x_cpl<2>(v, slots, nslots, check, init, first, s);
-    case 4: return launch_x_cpl<4>(v, slots, nslots, check, init, first, s);
-    case 8: return launch_x_cpl<8>(v, slots, nslots, check, init, first, s);
+    case 1: return launch_x_cpl<1>(v, slots, nslots, check, init, first, plain, it, s);
+    case 2: return launch_x_cpl<2>(v, slots, nslots, check, init, first, plain, it, s);
+    case 4: return launch_x_cpl<4>(v, slots, nslots, check, init, first, plain, it, s);
+    case 8: return launch_x_cpl<8>(v, slots, nslots, check, init, first, plain, it, s);
     default: return hipErrorInvalidValue;
   }
 }
 
 hipError_t launch_small_passes(const DeviceView &v, const int32_t *slots, int nslots, bool check, bool init,
-                               bool first, hipStream_t s) {
-  const int fi = first ? 1 : 0;
+                               bool first, bool plain, int it, hipStream_t s) {
+  const int fi = first ? 1 : 0, pl = plain ? 1 : 0;
   dim3 g1(v.JB, v.FB, nslots), g2(v.JB, nslots), block(kWave);
   if (init) {
-    hipLaunchKernelGGL((fj_pass<false, true>), g1, block, 0, s, v, slots, fi);
-    hipLaunchKernelGGL((node_pass<false, true>), g2, block, 0, s, v, slots, fi);
+    hipLaunchKernelGGL((fj_pass<false, true>), g1, block, 0, s, v, slots, fi, pl, it);
+    hipLaunchKernelGGL((node_pass<false, true>), g2, block, 0, s, v, slots, fi, pl, it);
   } else if (check) {
-    hipLaunchKernelGGL((fj_pass<true, false>), g1, block, 0, s, v, slots, fi);
-    hipLaunchKernelGGL((node_pass<true, false>), g2, block, 0, s, v, slots, fi);
+    hipLaunchKernelGGL((fj_pass<true, false>), g1, block, 0, s, v, slots, fi, pl, it);
+    hipLaunchKernelGGL((node_pass<true, false>), g2, block, 0, s, v, slots, fi, pl, it);
   } else {
-    hipLaunchKernelGGL((fj_pass<false, false>), g1, block, 0, s, v, slots, fi);
-    hipLaunchKernelGGL((node_pass<false, false>), g2, block, 0, s, v, slots, fi);
+    hipLaunchKernelGGL((fj_pass<false, false>), g1, block, 0, s, v, slots, fi, pl, it);
+    hipLaunchKernelGGL((node_pass<false, false>), g2, block, 0, s, v, slots, fi, pl, it);
   }
   return hipGetLastError();
 }
 
 hipError_t launch_scalar_pass(const DeviceView &v, const int32_t *slots, int nslots, bool check, bool init,
-                              bool first, int iters_done, hipStream_t s) {
+                              bool first, bool plain, int it, int iters_done, int block_len, hipStream_t s) {
   dim3 grid(nslots), block(256);
-  const int fi = first ? 1 : 0;
-  if (init) hipLaunchKernelGGL((scalar_pass<false, true>), grid, block, 0, s, v, slots, fi, iters_done);
-  else if (check) hipLaunchKernelGGL((scalar_pass<true, false>), grid, block, 0, s, v, slots, fi, iters_done);
-  else hipLaunchKernelGGL((scalar_pass<false, false>), grid, block, 0, s, v, slots, fi, iters_done);
+  const int fi = first ? 1 : 0, pl = plain ? 1 : 0;
+  if (init)
+    hipLaunchKernelGGL((scalar_pass<false, true>), grid, block, 0, s, v, slots, fi, pl, it, iters_done, block_len);
+  else if (check)
+    hipLaunchKernelGGL((scalar_pass<true, false>), grid, block, 0, s, v, slots, fi, pl, it, iters_done, block_len);
+  else
+    hipLaunchKernelGGL((scalar_pass<false, false>), grid, block, 0, s, v, slots, fi, pl, it, iters_done, block_len);
   return hipGetLastError();
 }
 
 hipError_t launch_init_slot(const DeviceView &v, const int32_t *slots, int nslots, bool warm, double eta,
-                            hipStream_t s) {
+                            double omega0, hipStream_t s) {
   dim3 grid(256, nslots), block(256);
-  hipLaunchKernelGGL(init_slot, grid, block, 0, s, v, slots, warm ? 1 : 0, eta);
+  hipLaunchKernelGGL(init_slot, grid, block, 0, s, v, slots, warm ? 1 : 0, eta, omega0);
   return hipGetLastError();
 }
 

@@ -1,0 +1,85 @@
+"""Test-only stand-in for `core.engine.lp.LPModel` backed by the ORACLE: every node LP is HiGHS on
+the reference's model restated as one CSR (oracle/formulation.py).  Lets the CPU suite run the
+product's branch-and-bound (core/engine/bnb.py) and step orchestration (core/solvers) without a
+GPU.  Routing rows are the literal per-(f, i) rows (no zero-workload pooling)."""
+import math
+
+import numpy as np
+
+from oracle.formulation import build_model
+from oracle.solve import solve as oracle_solve
+
+LP_OPTIMAL, LP_ITERATION_LIMIT, LP_INFEASIBLE, LP_CUTOFF = 0, 1, 2, 3
+
+
+class OracleLP:
+    def __init__(self, data, variant, step=1, alpha=0.5, soften_step1_sol=1.3, max_score=0.0,
+                 prev_network_delay=0.0, max_batch=1):
+        self.N, self.F = len(data.nodes), len(data.functions)
+        self.variant = variant
+        self.step = int(step)
+        prev_x = getattr(data, "prev_x", None)
+        if prev_x is None or not np.size(prev_x):
+            prev_x = np.zeros((self.N, self.F, self.N))
+        self.m = build_model(data, variant, step=1 if self.step == 1 else 2,
+                             mode="delete" if self.step == 2 else "create", alpha=alpha,
+                             soften_step1_sol=soften_step1_sol, max_score=max_score, prev_x=prev_x)
+        self.nx = self.N * self.N * self.F
+        self.n_int = self.m["A"].shape[1] - self.nx
+        self.max_batch = max_batch
+        self._sol = {}
+        self.calls = 0
+
+    def layout(self):
+        FN, N = self.F * self.N, self.N
+        has_n = self.variant != "MinDelay"
+        if self.step == 1:
+            return {"c": (0, FN), "n": (FN, FN + N) if has_n else None}
+        out = {"c": (0, FN), "moved_from": (FN, 2 * FN), "moved_to": (2 * FN, 3 * FN),
+               "allocated": (3 * FN, 3 * FN + 1), "deallocated": (3 * FN + 1, 3 * FN + 2)}
+        out["n"] = (3 * FN + 2, 3 * FN + 2 + N) if has_n else None
+        return out
+
+    def solve(self, slots, lb=None, ub=None, tol=1e-7, cutoff=math.inf, max_iters=0, check_every=64,
+              warm_start=False):
+        slots = np.asarray(slots).reshape(-1)
+        B = len(slots)
+        obj = np.zeros(B)
+        status = np.zeros(B, np.int32)
+        for b, s in enumerate(slots):
+            self.calls += 1
+            rl, ru = self.m["lb"].copy(), self.m["ub"].copy()
+            if lb is not None:
+                fin = np.isfinite(lb[b])
+                rl[self.nx:][fin] = np.maximum(rl[self.nx:][fin], lb[b][fin])
+            if ub is not None:
+                fin = np.isfinite(ub[b])
+                ru[self.nx:][fin] = np.minimum(ru[self.nx:][fin], ub[b][fin])
+            if (rl > ru).any():
+                st, val, x = 2, None, None
+            else:
+                st, val, x = oracle_solve(self.m, relax=True, lb=rl, ub=ru)
+            if val is None:
+                status[b], obj[b] = LP_INFEASIBLE, math.inf
+                self._sol[int(s)] = None
+                continue
+            obj[b] = val
+            status[b] = LP_CUTOFF if val > cutoff else LP_OPTIMAL
+            self._sol[int(s)] = x
+        return {"obj": obj, "primal_obj": obj.copy(), "status": status, "iters": np.zeros(B, np.int64)}
+
+    def rows(self, slot):
+        x = self._sol[int(slot)]
+        xb = x[:self.nx].reshape(self.F * self.N, self.N).astype(np.float32)
+        rf = np.repeat(np.arange(self.F), self.N).astype(np.int32)
+        rs = np.tile(np.arange(self.N), self.F).astype(np.int32)
+        return xb, rf, rs
+
+    def solution(self, slot, dense_x=True):
+        x = self._sol[int(slot)]
+        z = x[self.nx:].copy()
+        xd = x[:self.nx].reshape(self.F, self.N, self.N).transpose(1, 0, 2).astype(np.float32) if dense_x else None
+        return z, xd
+
+    def close(self):
+        self._sol = {}

@@ -210,6 +210,12 @@ class RefModel:
         self.rho, self.gam = rho, gam
         self.sigma_max = self._power()
         self.eta = 0.95 / self.sigma_max
+        # initial primal weight ||c~|| / ||b~|| (scaled space), as nep_host.cpp build()
+        cx = self.row_wobj[:, None] * np.where(self.row_src[:, None] >= 0, D[np.maximum(self.row_src, 0)], 0.0)
+        cn2 = (self.row_m[:, None] * cx * cx).sum() + ((gam * self.cost_int) ** 2).sum()
+        bmag = np.maximum(np.where(np.isfinite(lo), np.abs(lo), 0.0), np.where(np.isfinite(hi), np.abs(hi), 0.0))
+        bn2 = ((rho * bmag) ** 2).sum()
+        self.omega0 = float(np.sqrt(cn2) / np.sqrt(bn2)) if cn2 > 0 and bn2 > 0 else 1.0
 
     def _score_coef(self, D):
         out = np.zeros((self.R, self.N))
@@ -289,24 +295,36 @@ def proj_simplex_rows(V, mask):
 
 
 def solve(m, lbi=None, ubi=None, tol=1e-7, max_iters=100000, check_every=64, verbose=False):
-    """Same algorithm as the kernels, fp64.  Returns dict(status, obj, pobj, iters, x, z, y)."""
+    """Same algorithm as the kernels, fp64: blocks of `check_every` iterations; iteration 0 of a block
+    is the certificate iteration (a plain PDHG step whose input dual is the previous block's plain
+    output), restarts take effect at iteration 1, the last iteration is plain, the others are
+    reflected Halpern steps w' = lam (2 T(w) - w) + (1 - lam) w_anchor.
+    Returns dict(status, obj, pobj, iters, x, z, y)."""
     ok, lb, ub, fmask = m.presolve(lbi, ubi)
     if not ok:
         return dict(status=2, obj=INF, pobj=np.nan, iters=0)
     mask = fmask[m.row_f]
+    ce = check_every
     x = proj_simplex_rows(np.zeros((m.R, m.N)), mask)
     z = np.clip(np.zeros(m.n_int), lb, ub)
     y = np.zeros(m.n_dual)
     kz = m.K(x, z)
-    xa, za, ya = x.copy(), z.copy(), y.copy()
-    omega, eta = 1.0, m.eta
-    k = 0
-    k_since = 0
+    xa, za, ya, kza = x.copy(), z.copy(), y.copy(), kz.copy()
+    omega, eta = m.omega0, m.eta
+    om_lo, om_hi = m.omega0 * 1e-5, m.omega0 * 1e5
+    k = k_since = 0
+    ks_base = -ce
+    restart_pending = False
     last_fpr, prev_fpr = -1.0, INF
     best = -INF
     cost_x = m.row_wobj[:, None] * np.where(m.row_src[:, None] >= 0, m.D32[np.maximum(m.row_src, 0)], 0.0)
+    block = 0
     while True:
-        for it in range(check_every):
+        for it in range(ce):
+            check, first = it == 0, it == 1
+            plain = ce < 4 or it == 0 or it == ce - 1
+            if first and restart_pending:
+                xa, za, ya, kza = x.copy(), z.copy(), y.copy(), kz.copy()
             tau, sig = eta / omega, eta * omega
             gx, gz = m.KT(y)
             rcx = cost_x - gx
@@ -320,7 +338,6 @@ def solve(m, lbi=None, ubi=None, tol=1e-7, max_iters=100000, check_every=64, ver
                 a = V + s * m.hi
                 b = V + s * m.lo
             yn = np.where(a < 0, a, np.where(b > 0, b, 0.0))
-            check = it == check_every - 1
             if check:
                 lag = np.where(mask, rcx, INF).min(axis=1).sum()
                 lag += np.where(rcz > 0, lb * rcz, ub * rcz).sum()
@@ -335,27 +352,42 @@ def solve(m, lbi=None, ubi=None, tol=1e-7, max_iters=100000, check_every=64, ver
                 mvy = (((yn - y) / m.rho) ** 2).sum()
                 dsz = ((xn - xa) ** 2).sum() + (((zn - za) / m.gam) ** 2).sum()
                 dsy = (((yn - ya) / m.rho) ** 2).sum()
-            x, z, y, kz = xn, zn, yn, act
-        k += check_every
-        k_since += check_every
-        best = max(best, lag)
-        gap = pobj - lag
-        if verbose:
-            print(f"{k:7d} res={res:.2e} p={pobj:.10g} L={lag:.10g} gap={gap:.2e} w={omega:.3g}")
-        if np.isfinite(lag) and res <= tol and gap <= tol * max(1.0, abs(lag)):
-            return dict(status=0, obj=lag, pobj=pobj, iters=k, x=x, z=z, y=y)
-        if k >= max_iters:
-            return dict(status=1, obj=best, pobj=pobj, iters=k, x=x, z=z, y=y)
-        fpr = np.sqrt(omega * mvz + mvy / omega)
-        if last_fpr < 0:
-            last_fpr = fpr
-        restart = fpr <= 0.2 * last_fpr or (fpr <= 0.8 * last_fpr and fpr > prev_fpr) or k_since >= 0.36 * k
-        prev_fpr = fpr
-        if restart:
-            dz, dy = np.sqrt(dsz), np.sqrt(dsy)
-            if dz > 1e-10 and dy > 1e-10:
-                omega = float(np.clip(np.exp(0.5 * np.log(dy / dz) + 0.5 * np.log(omega)), 1e-2, 1e2))
-            xa, za, ya = x.copy(), z.copy(), y.copy()
-            k_since = 0
-            last_fpr = fpr
-            prev_fpr = INF
+            if plain:
+                x, z, y, kz = xn, zn, yn, act
+            else:
+                ks = ks_base + it
+                lam = (ks + 1.0) / (ks + 2.0)
+                x = lam * (2 * xn - x) + (1 - lam) * xa
+                z = lam * (2 * zn - z) + (1 - lam) * za
+                y = lam * (2 * yn - y) + (1 - lam) * ya
+                kz = lam * (2 * act - kz) + (1 - lam) * kza
+            if check:
+                k += 1 if block == 0 else ce
+                k_since += 1 if block == 0 else ce
+                restart_pending = False
+                best = max(best, lag)
+                gap = pobj - lag
+                if verbose:
+                    print(f"{k:7d} res={res:.2e} p={pobj:.10g} L={lag:.10g} gap={gap:.2e} w={omega:.3g}")
+                if np.isfinite(lag) and res <= tol and gap <= tol * max(1.0, abs(lag)):
+                    return dict(status=0, obj=lag, pobj=pobj, iters=k, x=x, z=z, y=y)
+                if k >= max_iters:
+                    return dict(status=1, obj=best, pobj=pobj, iters=k, x=x, z=z, y=y)
+                fpr = np.sqrt(omega * mvz + mvy / omega)
+                if last_fpr < 0:
+                    last_fpr = fpr
+                restart = (fpr <= 0.2 * last_fpr or (fpr <= 0.8 * last_fpr and fpr > prev_fpr)
+                           or k_since >= 0.36 * k)
+                prev_fpr = fpr
+                if restart:
+                    dz, dy = np.sqrt(dsz), np.sqrt(dsy)
+                    if dz > 1e-10 and dy > 1e-10:
+                        omega = float(np.clip(np.exp(0.5 * np.log(dy / dz) + 0.5 * np.log(omega)), om_lo, om_hi))
+                    restart_pending = True
+                    k_since = 0
+                    ks_base = -1
+                    last_fpr = fpr
+                    prev_fpr = INF
+                else:
+                    ks_base += ce
+        block += 1

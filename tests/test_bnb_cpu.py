@@ -1,0 +1,72 @@
+"""The product's branch-and-bound (core/engine/bnb.py) and two-step orchestration (core/solvers/neptune)
+run on CPU with the ORACLE as node-LP backend (tests/oracle_lp.py): they must reproduce the MIP
+optima HiGHS found on the reference's own recorded models, and the responses of the reference
+flow (scores; placements where the optimum is unique).  The GPU twin is tests/test_gpu_solvers.py."""
+import numpy as np
+import pytest
+
+from golden_util import golden, model, payload
+from gpu_cases import VARIANT
+from oracle_lp import OracleLP
+
+G = golden()
+SMALL = [(name, k) for name, v in G.items() if "models" in v
+         for k, m in enumerate(v["models"]) if m["n_vars"] <= 400]
+FLOW = [name for name, v in G.items() if "response" in v and max(m["n_vars"] for m in v["models"]) <= 400]
+
+
+def _data(name):
+    from core.utils import data_to_solver_input
+    p = payload(name)
+    return p, data_to_solver_input(p, workload_coeff=p.get("workload_coeff", 1), with_db=False)
+
+
+def _close(a, b):
+    return abs(a - b) <= 1e-6 * max(1.0, abs(b))
+
+
+@pytest.mark.parametrize("name,k", SMALL)
+def test_bnb_matches_recorded_mip(name, k):
+    from core.engine.bnb import INFEASIBLE, OPTIMAL, BranchAndBound
+    p, data = _data(name)
+    rec = G[name]["models"][k]
+    variant = VARIANT[p["solver"]["type"]]
+    args = p["solver"].get("args", {})
+    kw = dict(alpha=args.get("alpha", 0.5), soften_step1_sol=args.get("soften_step1_sol", 1.3))
+    step = 1
+    if k > 0:
+        N, F = len(data.nodes), len(data.functions)
+        m1 = model(name, 0)
+        data.prev_x = m1["mip_x"][:N * N * F].reshape(F, N, N).transpose(1, 0, 2)
+        kw["max_score"] = float(m1["mip_objective"])
+        step = 2 if rec["mode"] == "step2_delete" else 3
+    lp = OracleLP(data, variant, step=step, max_batch=8, **kw)
+    res = BranchAndBound(lp, data.workload_matrix, data.function_memory_matrix, data.node_memory_matrix,
+                         batch=8, node_limit=20000).solve()
+    if rec["status"] == 0:
+        assert res.status == OPTIMAL, res.as_dict()
+        assert _close(res.objective, rec["mip_objective"]), (res.objective, rec["mip_objective"])
+    else:
+        assert res.status == INFEASIBLE, res.as_dict()
+
+
+@pytest.mark.parametrize("name", FLOW)
+def test_solver_flow_matches_reference(name, monkeypatch):
+    import core.solvers as S
+    from core.solvers.neptune import neptune_step
+    monkeypatch.setattr(neptune_step, "make_lp",
+                        lambda data, variant, step, max_batch, **kw: OracleLP(data, variant, step=step,
+                                                                              max_batch=max_batch, **kw))
+    p, data = _data(name)
+    solver = S.SOLVERS[p["solver"]["type"]](**p["solver"].get("args", {}))
+    solver.load_data(data)
+    solver.solve()
+    x, c = solver.results()
+    score = solver.score()
+    ref = G[name]["response"]
+    assert _close(score["step1"], ref["score"]["step1"]), (score, ref["score"])
+    assert _close(score["step2"], ref["score"]["step2"]), (score, ref["score"])
+    done = [m for m in G[name]["models"] if m["status"] == 0]
+    if done and done[-1].get("mip_tied") is False:
+        assert c == ref["cpu_allocations"]
+        assert set(x) == set(ref["cpu_routing_rules"])
