@@ -2,29 +2,31 @@
 """bench.py — LP-relaxations/sec (+ certified objective gap) on the synthetic 512-node x
 256-function NEPTUNE instance (BASELINE.json `metric`; generator of SURVEY.md §8(d)).
 
-Workload.  One *step* = one batch of B branch-and-bound node LP relaxations of the step-1
-NeptuneMinDelayAndUtilization model (reference `core/solvers/neptune/neptune_step1.py:67-77`,
-rows `neptune/utils/constraints_step1.py`, objective `neptune/utils/objectives.py:30-52`).
-Every node is a child of the root LP: it carries `--fix` seeded c[f,j] fixings (0 or 1, the
-branching decisions of a B&B) and is warm-started from the root's primal/dual state, as a B&B
-child is from its parent (`--cold` starts every node from zero instead).  A node counts only if
-the engine certifies it: primal objective - Lagrangian bound <= tol*max(1,|bound|) and every row
-residual <= tol.  The root LP is solved once before the timed region.  The
-instance tensors live on the device before the timer starts; node bounds are uploaded inside
-the step, as the B&B host does per node batch.
+Workload.  Branch-and-bound node LP relaxations of the step-1 NeptuneMinDelayAndUtilization model
+(reference `core/solvers/neptune/neptune_step1.py:67-77`, rows `neptune/utils/constraints_step1.py`,
+objective `neptune/utils/objectives.py:30-52`).  Every node is a child of the root LP: it carries
+`--fix` seeded c[f,j] fixings (0 or 1, the branching decisions of a B&B) and is warm-started from
+the root's primal/dual state, as a B&B child is from its parent (`--cold`: from zero).  The engine
+keeps `--batch` node LPs in flight per GPU (nep_lp_submit / nep_lp_advance): a slot whose LP
+finishes takes the next node at once, as a B&B with an open-node queue does.  One *step* =
+`--batch` completed node LPs.  A node counts as an LP relaxation only if the engine certifies it:
+primal objective - Lagrangian bound <= tol*max(1,|bound|) and every row residual <= tol
+(DESIGN.md §4); nodes that stop at `--max-iters` are reported, not counted.  The root LP is solved
+before the timed region; the instance tensors live on the device before the timer starts; node
+bounds are uploaded inside the step, as the B&B host does per node.
 
 Multi-GPU (`torch.distributed.run`, one rank per GPU): every rank holds the same instance and
-solves its own B nodes per step (subtree sharding); the only exchange is the
-B&B bound all-reduce(MIN) of 8 bytes per step.  value = certified LPs of all ranks / max-over-
-ranks wall time ("scaling": "weak").
+solves its own node stream (subtree sharding); the only exchange is the B&B
+bound all-reduce(MIN) of 8 bytes per step.  value = certified LPs of all ranks / max-over-ranks
+wall time ("scaling": "weak").
 
-Roofline.  The dominant kernel is the fused routing-row pass `x_pass` (csrc/nep_kernels.hip).
-Its algorithmic bytes per LP iteration are 8*P (x read + x write, fp32), P = R*N routing entries
-after exact zero-workload source aggregation.  `achieved` = those bytes x the LPs one sampled
-launch carries / that launch's HIP-event duration on the engine's own stream, averaged over one
-steady-state launch per 64-iteration block (nep_get_stats).  `traffic` is read from
-profiles/traffic.json (a separate rocprofv3 --pmc pass) when it was measured on
-this exact workload, else null.
+Roofline.  The dominant kernel is `x_pass` (csrc/nep_kernels.hip).  Its algorithmic bytes per LP
+iteration are 8*P (x read + x write, fp32), P = R*N routing entries after exact zero-workload
+source aggregation.  `achieved` = those bytes x the LPs one sampled launch carries / that launch's
+HIP-event duration on the engine's own stream, averaged over one steady-state launch per
+64-iteration block (nep_get_stats).  `traffic` is read from profiles/traffic.json (separate
+rocprofv3 --pmc passes, tools/traffic.py) when it was measured on this exact
+workload, else null.
 
 CPU baseline.  The oracle (HiGHS on the reference's formulation restated as one CSR, oracle/)
 timed on rank 0's host, bounded by `--cpu-budget` seconds (see `cpu_baseline`).
@@ -44,23 +46,29 @@ for _p in (PKG, REPO):
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md "HBM")
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--nodes", type=int, default=512)
     ap.add_argument("--functions", type=int, default=256)
-    ap.add_argument("--batch", type=int, default=16, help="node LPs per step per GPU")
+    ap.add_argument("--batch", type=int, default=16, help="node LPs in flight per GPU (= completed LPs per step)")
     ap.add_argument("--fix", type=int, default=2, help="c[f,j] fixings per node LP")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--tol", type=float, default=1e-6)
-    ap.add_argument("--max-iters", type=int, default=200000)
+    ap.add_argument("--max-iters", type=int, default=100000, help="per node LP")
+    ap.add_argument("--root-max-iters", type=int, default=400000)
     ap.add_argument("--check-every", type=int, default=64)
     ap.add_argument("--cold", action="store_true", help="cold-start every node LP")
     ap.add_argument("--cpu-budget", type=float, default=25.0, help="seconds for the CPU baseline (0 = skip)")
     ap.add_argument("--traffic", default=os.path.join(REPO, "profiles", "traffic.json"))
-    return ap.parse_args()
+    return ap.parse_args(argv)
+
+
+def workload_name(a):
+    return (f"synthetic_{a.nodes}x{a.functions}_step1_MDU_bnb_children_stream_B{a.batch}_fix{a.fix}_"
+            f"{'cold' if a.cold else 'warm'}")
 
 
 def log(msg):
@@ -133,6 +141,45 @@ def cpu_baseline(N, F, seed, fix, budget):
                                                for a, b, t, s in pts]}
 
 
+class NodeStream:
+    """B&B child LPs of the root, `batch` of them in flight on the engine (nep_lp_submit/advance):
+    a slot whose LP finishes takes the next node at once."""
+
+    def __init__(self, m, root, a, rank):
+        self.m, self.root, self.a, self.rank = m, root, a, rank
+        self.counter = 0
+        self.done = []          # (status, obj, primal_obj, iters) per completed node
+
+    def _start(self, slot):
+        from core.engine.lp import LP_INFEASIBLE
+        a = self.a
+        while True:
+            seed = (a.seed * 1000003 + self.rank) * 7919 + self.counter
+            self.counter += 1
+            lb, ub = node_bounds(self.m.n_int, a.functions, a.nodes, 1, a.fix, seed)
+            if not a.cold:
+                self.m.copy_state(self.root, slot)
+            st = self.m.submit([slot], lb, ub, tol=a.tol, max_iters=a.max_iters, check_every=a.check_every,
+                               warm_start=not a.cold)
+            if int(st[0]) != LP_INFEASIBLE:
+                return
+            self.done.append((LP_INFEASIBLE, float("inf"), float("nan"), 0))
+
+    def fill(self):
+        for s in range(self.a.batch):
+            self._start(s)
+
+    def run(self, n):
+        """Advance until n more node LPs completed; finished slots are refilled immediately."""
+        target = len(self.done) + n
+        while len(self.done) < target:
+            r = self.m.advance(1)
+            for i, s in enumerate(r["slots"]):
+                self.done.append((int(r["status"][i]), float(r["obj"][i]), float(r["primal_obj"][i]),
+                                  int(r["iters"][i])))
+                self._start(int(s))
+
+
 def main():
     a = parse()
     import numpy as np
@@ -160,62 +207,57 @@ def main():
     t_build = time.perf_counter()
     m = LPModel(data, "MinDelayAndUtilization", step=1, alpha=alpha, max_batch=B + 1)
     log(f"rank {rank}: model {N}x{F}: R={m.info.n_rows} rows, P={m.info.x_entries} routing entries, "
-        f"{m.info.n_tiles} tiles, built in {time.perf_counter() - t_build:.1f}s")
+        f"built in {time.perf_counter() - t_build:.1f}s")
     P = m.info.x_entries
     t_root = time.perf_counter()
-    rr = m.solve([root], tol=a.tol, max_iters=a.max_iters, check_every=a.check_every)
+    rr = m.solve([root], tol=a.tol, max_iters=a.root_max_iters, check_every=a.check_every)
     root_obj, root_status, root_iters = float(rr["obj"][0]), int(rr["status"][0]), int(rr["iters"][0])
     log(f"rank {rank}: root LP status {root_status} obj {root_obj:.10g} after {root_iters} iterations "
         f"({time.perf_counter() - t_root:.2f}s)")
     if root_status != LP_OPTIMAL:
         raise RuntimeError(f"root LP not certified: status {root_status} after {root_iters} iterations")
 
-    def step(s):
-        lb, ub = node_bounds(m.n_int, F, N, B, a.fix, seed=(a.seed * 1000003 + rank) * 7919 + s)
-        if not a.cold:
-            for b in range(B):
-                m.copy_state(root, b)
-        r = m.solve(np.arange(B), lb, ub, tol=a.tol, max_iters=a.max_iters, check_every=a.check_every,
-                    warm_start=not a.cold)
-        best = torch.tensor([float(np.min(r["obj"]))], dtype=torch.float64, device=dev)
+    stream = NodeStream(m, root, a, rank)
+    stream.fill()
+
+    def step():
+        stream.run(B)
+        ok = [o for st, o, _, _ in stream.done if st == LP_OPTIMAL]
+        best = torch.tensor([min(ok) if ok else float("inf")], dtype=torch.float64, device=dev)
         if dist:
             td.all_reduce(best, op=td.ReduceOp.MIN)     # B&B bound exchange (8 B)
-        ok = r["status"] == LP_OPTIMAL
-        gap = np.abs(r["primal_obj"] - r["obj"]) / np.maximum(1.0, np.abs(r["obj"]))
-        return int(ok.sum()), int(r["iters"].sum()), float(np.max(np.where(ok, gap, 0.0))), r
 
     for s in range(a.warmup):
-        k, it, _, _ = step(-1 - s)
-        log(f"rank {rank}: warmup step {s}: {k}/{B} certified, {it} iterations")
+        step()
+        log(f"rank {rank}: warmup step {s}: {len(stream.done)} node LPs completed")
     m.reset_stats()
+    i0 = len(stream.done)
     if dist:
         td.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    n_ok = n_it = 0
-    gmax = 0.0
-    statuses = []
     for s in range(a.steps):
-        k, it, g, r = step(s)
-        n_ok += k
-        n_it += it
-        gmax = max(gmax, g)
-        statuses += r["status"].tolist()
-        log(f"rank {rank}: step {s}: {k}/{B} certified, {it} iterations, {time.perf_counter() - t0:.2f}s")
+        step()
+        log(f"rank {rank}: step {s}: {len(stream.done) - i0} node LPs completed, {time.perf_counter() - t0:.2f}s")
     torch.cuda.synchronize()
     if dist:
         td.barrier()
     wall = time.perf_counter() - t0
     st = m.stats()
+    res = stream.done[i0:]
+    n_ok = sum(1 for r in res if r[0] == LP_OPTIMAL)
+    n_it = sum(r[3] for r in res)
+    gmax = max([abs(p - o) / max(1.0, abs(o)) for s_, o, p, _ in res if s_ == LP_OPTIMAL] or [0.0])
+    n_done = len(res)
 
-    tot = torch.tensor([wall, n_ok, n_it, gmax], dtype=torch.float64, device=dev)
+    tot = torch.tensor([wall, n_ok, n_it, gmax, n_done], dtype=torch.float64, device=dev)
     if dist:
         mx = tot.clone()
         td.all_reduce(mx, op=td.ReduceOp.MAX)
         sm = tot.clone()
         td.all_reduce(sm, op=td.ReduceOp.SUM)
         wall, gmax = float(mx[0]), float(mx[3])
-        n_ok, n_it = int(sm[1]), int(sm[2])
+        n_ok, n_it, n_done = int(sm[1]), int(sm[2]), int(sm[4])
     if rank != 0:
         m.close()
         if dist:
@@ -226,7 +268,7 @@ def main():
     launch_ms = st["x_pass_ms"] / max(1, st["x_pass_sampled"])
     lps_per_launch = st["x_pass_lp_iters"] / max(1, st["x_pass_sampled"])
     achieved = per_lp * lps_per_launch / (launch_ms * 1e-3) / 1e9 if launch_ms > 0 else 0.0
-    workload = f"synthetic_{N}x{F}_step1_MDU_bnb_children_B{B}_fix{a.fix}_{'cold' if a.cold else 'warm'}"
+    workload = workload_name(a)
     traffic = None
     if os.path.exists(a.traffic):
         with open(a.traffic) as fh:
@@ -236,7 +278,6 @@ def main():
     cpu = None
     if world == 1 and a.cpu_budget > 0:
         cpu = cpu_baseline(N, F, a.seed, a.fix, a.cpu_budget)
-    attempted = len(statuses) * world
     out = {
         "metric": "LP-relaxations/sec + objective gap vs reference, 512-node×256-function",
         "value": n_ok / wall,
@@ -250,14 +291,14 @@ def main():
         "vs_baseline": None,
         "dtype": "f32 x-state, f64 duals/reductions/certificate",
         "data": "synthetic (SURVEY.md §8(d) generator, seed %d)" % a.seed,
-        "config": {"workload": workload, "nodes": N, "functions": F, "lp_per_step_per_gpu": B,
-                   "fixings_per_lp": a.fix, "tol": a.tol, "routing_entries_P": P,
-                   "parallelism": f"bnb-subtrees x{world}"},
+        "config": {"workload": workload, "nodes": N, "functions": F, "lp_in_flight_per_gpu": B,
+                   "fixings_per_lp": a.fix, "tol": a.tol, "max_iters_per_lp": a.max_iters,
+                   "routing_entries_P": P, "parallelism": f"bnb-subtrees x{world}"},
         "objective_gap": {"certified_max": gmax, "tol": a.tol,
                           "note": "(primal obj - Lagrangian bound)/max(1,|bound|) per certified LP; "
                                   "HiGHS parity on the reference's own models: tests/test_gpu_lp.py"},
-        "lp": {"certified": n_ok, "attempted": attempted, "iterations": n_it,
-               "mean_iters": n_it / max(1, attempted), "root_obj": root_obj, "root_iters": root_iters},
+        "lp": {"certified": n_ok, "completed": n_done, "iterations": n_it,
+               "mean_iters": n_it / max(1, n_done), "root_obj": root_obj, "root_iters": root_iters},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": "x_pass", "algorithmic_bytes_per_launch": per_lp * lps_per_launch,

@@ -7,6 +7,7 @@
  *   core/solvers/solver.py:15-20  load_data -> init_vars / init_constraints   -> nep_model_desc
  *   core/solvers/solver.py:35-40  init_objective(); Solver.Solve(); status == OPTIMAL
  *                                 (SCIP solves one LP relaxation per B&B node) -> nep_lp_solve_batch
+ *                                                                               (nep_lp_submit/advance)
  *   core/solvers/solver.py:45-46  score() = Objective().Value()               -> obj / primal_obj
  *   neptune/utils/output.py:5-21  x[i,f,j].solution_value(), c[f,j], n[j]     -> nep_lp_get_solution
  * The model rows/columns are exactly those of neptune/utils/variables.py, constraints_step1.py,
@@ -31,7 +32,7 @@
 extern "C" {
 #endif
 
-#define NEP_API_VERSION 1
+#define NEP_API_VERSION 2
 
 /* variants: neptune.py:41-66 (NeptuneMinDelay / MinUtilization / MinDelayAndUtilization) */
 enum { NEP_MIN_DELAY = 0, NEP_MIN_UTILIZATION = 1, NEP_MIN_DELAY_AND_UTILIZATION = 2 };
@@ -44,7 +45,7 @@ enum { NEP_OK = 0, NEP_ERR_ARG = -1, NEP_ERR_HIP = -2, NEP_ERR_NOMEM = -3, NEP_E
 enum {
   NEP_LP_OPTIMAL = 0,          /* certified: gap(primal obj, Lagrangian bound) and residuals <= tol */
   NEP_LP_ITERATION_LIMIT = 1,  /* obj still holds a VALID lower bound (Lagrangian) */
-  NEP_LP_INFEASIBLE = 2,       /* proven by presolve (empty routing row, crossed bounds) */
+  NEP_LP_INFEASIBLE = 2,       /* proven by presolve (empty routing row, crossed bounds, row activity) */
   NEP_LP_CUTOFF = 3,           /* Lagrangian bound exceeded opts.cutoff: node can be pruned */
   NEP_LP_NUMERICAL = 4
 };
@@ -83,7 +84,7 @@ typedef struct {
 typedef struct {
   int32_t n_int;               /* length of z_int */
   int32_t n_rows;              /* R: routing rows after exact zero-workload source aggregation */
-  int32_t n_tiles;             /* x-pass workgroups per LP */
+  int32_t n_tiles;             /* x-pass workgroups per LP (one per function) */
   int32_t max_batch;
   int64_t x_entries;           /* R*N per LP */
   int64_t bytes_per_iter;      /* algorithmic HBM bytes of one PDHG iteration of one LP */
@@ -95,7 +96,7 @@ typedef struct {
   double x_pass_ms;            /* summed HIP-event duration of the sampled x-pass launches */
   int64_t x_pass_sampled;      /* number of sampled launches in x_pass_ms */
   int64_t x_pass_lp_iters;     /* LP-iterations carried by the sampled launches */
-  double solve_ms;             /* wall time inside nep_lp_solve_batch (device-synchronised) */
+  double solve_ms;             /* wall time inside nep_lp_solve_batch / nep_lp_advance (device-synchronised) */
   int64_t lp_iterations;       /* PDHG iterations summed over LPs */
 } nep_stats;
 
@@ -103,17 +104,34 @@ int nep_model_create(const nep_model_desc *desc, int32_t max_batch, void *hip_st
 void nep_model_destroy(void *model);
 int nep_model_get_info(void *model, nep_model_info *info);
 
-/* Solve B node LPs in slots[0..B-1].  lb_int/ub_int: host [B][n_int] bounds on z_int (branching
- * fixings; pass NULL for the root bounds).  Outputs (host, length B): obj = certified LP value
- * (Lagrangian lower bound), primal_obj = objective of the primal iterate, status, iters. */
+/* Solve B node LPs in slots[0..B-1] to completion.  lb_int/ub_int: host [B][n_int] bounds on z_int
+ * (branching fixings; pass NULL for the root bounds).  Outputs (host, length B): obj = certified LP
+ * value (Lagrangian lower bound), primal_obj = objective of the primal iterate, status, iters.
+ * Equivalent to nep_lp_submit + nep_lp_advance until no slot iterates. */
 int nep_lp_solve_batch(void *model, int32_t B, const int32_t *slots, const double *lb_int, const double *ub_int,
                        const nep_lp_opts *opts, double *obj, double *primal_obj, int32_t *status, int64_t *iters);
+
+/* Streaming form, for a branch-and-bound that keeps every slot busy.
+ * nep_lp_submit: start n node LPs in free slots (host presolve, then the slot's initialisation on
+ *   the device).  status[b] = NEP_LP_INFEASIBLE when presolve proves node b infeasible (it does not
+ *   iterate), NEP_LP_ITERATION_LIMIT when it starts iterating.  opts apply to every LP in flight;
+ *   check_every cannot change while any slot iterates.
+ * nep_lp_advance: run blocks of check_every PDHG iterations on every iterating slot until at least
+ *   min_done of them finished (min_done <= 0: exactly one block).  The finished slots and their
+ *   results go to the first *n_done entries of the outputs (each sized max_batch).
+ * nep_lp_active: number of iterating slots. */
+int nep_lp_submit(void *model, int32_t n, const int32_t *slots, const double *lb_int, const double *ub_int,
+                  const nep_lp_opts *opts, int32_t *status);
+int nep_lp_advance(void *model, int32_t min_done, int32_t *n_done, int32_t *done_slots, double *obj,
+                   double *primal_obj, int32_t *status, int64_t *iters);
+int nep_lp_active(void *model);
 
 /* z_int (host, n_int) and optionally the dense routing x[i][f][j] (host float, N*F*N) of a slot. */
 int nep_lp_get_solution(void *model, int32_t slot, double *z_int, float *x_dense);
 /* aggregated routing rows (host float, R*N) and the row map (row_f, row_src; src = -1: pooled
  * zero-workload sources of function f, each routed identically). */
 int nep_lp_get_rows(void *model, int32_t slot, float *xbar, int32_t *row_f, int32_t *row_src);
+/* copy a slot's primal/dual state to another (not iterating) slot: warm start of a child node */
 int nep_lp_copy_state(void *model, int32_t src_slot, int32_t dst_slot);
 
 int nep_get_stats(void *model, nep_stats *stats);
@@ -124,7 +142,7 @@ int nep_lp_get_diag(void *model, int32_t slot, double *out16);
 /* device state of a slot (any pointer may be NULL): duals [n_dual], row activities [n_dual],
  * packed f32 duals of the x pass [F*NP+NP+4], node bounds [n_int] */
 int nep_debug_state(void *model, int32_t slot, double *y, double *kz, float *kty, double *lb, double *ub);
-/* host-only model build (no device work): step size, scalings, row norms, dims = {R, tiles, n_int,
+/* host-only model build (no device work): step size, scalings, row norms, dims = {R, F, n_int,
  * n_dual}.  Lets the CPU test-suite check the model build without a GPU. */
 int nep_debug_build(const nep_model_desc *desc, double *eta, double *rho, double *gam, double *rownorm,
                     int32_t *dims);

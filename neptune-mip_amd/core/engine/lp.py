@@ -18,6 +18,7 @@ STEP1, STEP2_DELETE, STEP2_CREATE = 1, 2, 3
 LP_OPTIMAL, LP_ITERATION_LIMIT, LP_INFEASIBLE, LP_CUTOFF, LP_NUMERICAL = 0, 1, 2, 3, 4
 VARIANTS = {"MinDelay": MIN_DELAY, "MinUtilization": MIN_UTILIZATION,
             "MinDelayAndUtilization": MIN_DELAY_AND_UTILIZATION}
+API_VERSION = 2
 
 _dp = ctypes.POINTER(ctypes.c_double)
 
@@ -55,6 +56,7 @@ class Stats(ctypes.Structure):
 
 # every entry point declared in include/neptune_lp.h
 EXPORTS = ("nep_model_create", "nep_model_destroy", "nep_model_get_info", "nep_lp_solve_batch",
+           "nep_lp_submit", "nep_lp_advance", "nep_lp_active",
            "nep_lp_get_solution", "nep_lp_get_rows", "nep_lp_copy_state", "nep_get_stats", "nep_reset_stats",
            "nep_last_error", "nep_api_version", "nep_lp_get_diag", "nep_debug_build", "nep_debug_state")
 
@@ -71,12 +73,16 @@ def load_library(path=None):
         raise EngineUnavailable(f"MI355X LP engine not built: {p} missing (run __graft_entry__.build())")
     lib = ctypes.CDLL(p)
     vp, i32, i64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64
+    pi32, pi64 = ctypes.POINTER(i32), ctypes.POINTER(i64)
     lib.nep_model_create.argtypes = [ctypes.POINTER(ModelDesc), i32, vp, ctypes.POINTER(vp)]
     lib.nep_model_destroy.argtypes = [vp]
     lib.nep_model_destroy.restype = None
     lib.nep_model_get_info.argtypes = [vp, ctypes.POINTER(ModelInfo)]
     lib.nep_lp_solve_batch.argtypes = [vp, i32, ctypes.POINTER(i32), _dp, _dp, ctypes.POINTER(LpOpts), _dp, _dp,
                                        ctypes.POINTER(i32), ctypes.POINTER(i64)]
+    lib.nep_lp_submit.argtypes = [vp, i32, pi32, _dp, _dp, ctypes.POINTER(LpOpts), pi32]
+    lib.nep_lp_advance.argtypes = [vp, i32, pi32, pi32, _dp, _dp, pi32, pi64]
+    lib.nep_lp_active.argtypes = [vp]
     lib.nep_lp_get_solution.argtypes = [vp, i32, _dp, ctypes.POINTER(ctypes.c_float)]
     lib.nep_lp_get_rows.argtypes = [vp, i32, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(i32),
                                     ctypes.POINTER(i32)]
@@ -89,6 +95,8 @@ def load_library(path=None):
     lib.nep_debug_state.argtypes = [vp, i32, _dp, _dp, ctypes.POINTER(ctypes.c_float), _dp, _dp]
     lib.nep_last_error.restype = ctypes.c_char_p
     lib.nep_api_version.restype = ctypes.c_int
+    if lib.nep_api_version() != API_VERSION:
+        raise EngineUnavailable(f"{p}: API version {lib.nep_api_version()} != {API_VERSION} (rebuild the engine)")
     if path is None:
         _lib = lib
     return lib
@@ -177,14 +185,18 @@ class LPModel:
         except Exception:
             pass
 
+    def _bounds(self, B, lb, ub):
+        lbp = None if lb is None else np.ascontiguousarray(np.asarray(lb, np.float64).reshape(B, self.n_int))
+        ubp = None if ub is None else np.ascontiguousarray(np.asarray(ub, np.float64).reshape(B, self.n_int))
+        return lbp, ubp
+
     def solve(self, slots, lb=None, ub=None, tol=1e-7, cutoff=math.inf, max_iters=200000, check_every=64,
               warm_start=False):
         """Solve len(slots) node LPs.  lb/ub: [B, n_int] bounds on the integer vector (None = root).
         Returns dict of numpy arrays: obj (certified LP value = Lagrangian bound), primal_obj, status, iters."""
         slots = np.ascontiguousarray(np.asarray(slots, dtype=np.int32).reshape(-1))
         B = len(slots)
-        lbp = None if lb is None else np.ascontiguousarray(np.asarray(lb, np.float64).reshape(B, self.n_int))
-        ubp = None if ub is None else np.ascontiguousarray(np.asarray(ub, np.float64).reshape(B, self.n_int))
+        lbp, ubp = self._bounds(B, lb, ub)
         obj = np.zeros(B)
         pobj = np.zeros(B)
         status = np.zeros(B, np.int32)
@@ -194,6 +206,43 @@ class LPModel:
             self._h, B, _ptr(slots, ctypes.c_int32), _ptr(lbp), _ptr(ubp), ctypes.byref(opts), _ptr(obj), _ptr(pobj),
             _ptr(status, ctypes.c_int32), _ptr(iters, ctypes.c_int64)), "nep_lp_solve_batch")
         return {"obj": obj, "primal_obj": pobj, "status": status, "iters": iters}
+
+    # streaming form (nep_lp_submit / nep_lp_advance): a B&B keeps every slot busy
+    def submit(self, slots, lb=None, ub=None, tol=1e-7, cutoff=math.inf, max_iters=200000, check_every=64,
+               warm_start=False):
+        """Start node LPs in free slots; returns their presolve status (LP_INFEASIBLE: proven
+        infeasible, not started; LP_ITERATION_LIMIT: iterating)."""
+        slots = np.ascontiguousarray(np.asarray(slots, dtype=np.int32).reshape(-1))
+        B = len(slots)
+        lbp, ubp = self._bounds(B, lb, ub)
+        status = np.zeros(B, np.int32)
+        opts = LpOpts(float(tol), float(cutoff), int(max_iters), int(check_every), 1 if warm_start else 0)
+        _check(self._lib, self._lib.nep_lp_submit(self._h, B, _ptr(slots, ctypes.c_int32), _ptr(lbp), _ptr(ubp),
+                                                  ctypes.byref(opts), _ptr(status, ctypes.c_int32)),
+               "nep_lp_submit")
+        return status
+
+    def advance(self, min_done=1):
+        """Iterate until at least `min_done` LPs finished (0: one block of check_every iterations).
+        Returns the finished slots and their results."""
+        mb = self.max_batch
+        n = ctypes.c_int32(0)
+        slots = np.zeros(mb, np.int32)
+        obj = np.zeros(mb)
+        pobj = np.zeros(mb)
+        status = np.zeros(mb, np.int32)
+        iters = np.zeros(mb, np.int64)
+        _check(self._lib, self._lib.nep_lp_advance(self._h, int(min_done), ctypes.byref(n),
+                                                   _ptr(slots, ctypes.c_int32), _ptr(obj), _ptr(pobj),
+                                                   _ptr(status, ctypes.c_int32), _ptr(iters, ctypes.c_int64)),
+               "nep_lp_advance")
+        k = n.value
+        return {"slots": slots[:k], "obj": obj[:k], "primal_obj": pobj[:k], "status": status[:k],
+                "iters": iters[:k]}
+
+    def active(self):
+        """Number of slots iterating (submitted and not yet finished)."""
+        return int(self._lib.nep_lp_active(self._h))
 
     def solution(self, slot, dense_x=True):
         z = np.zeros(self.n_int)

@@ -1,10 +1,12 @@
 // nep_host.cpp — host runtime of the NEPTUNE LP engine: model build (exact zero-workload
 // aggregation, coefficients, diagonal scaling, step size), per-node presolve, the batched PDHG
-// solve loop on one HIP stream, solution export, and the extern "C" ABI of include/neptune_lp.h.
+// solve loop on one HIP stream (batch and streaming forms), solution export, and the extern "C"
+// ABI of include/neptune_lp.h.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <chrono>
+#include <climits>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -20,10 +22,10 @@
 namespace nep {
 hipError_t launch_x_pass(const DeviceView &v, const int32_t *slots, int nslots, bool check, bool init, bool first,
                          bool plain, int it, hipStream_t s);
-hipError_t launch_small_passes(const DeviceView &v, const int32_t *slots, int nslots, bool check, bool init,
-                               bool first, bool plain, int it, hipStream_t s);
+hipError_t launch_node_pass(const DeviceView &v, const int32_t *slots, int nslots, bool check, bool init, bool first,
+                            bool plain, int it, hipStream_t s);
 hipError_t launch_scalar_pass(const DeviceView &v, const int32_t *slots, int nslots, bool check, bool init,
-                              bool first, bool plain, int it, int iters_done, int block_len, hipStream_t s);
+                              bool first, bool plain, int it, int block_len, hipStream_t s);
 hipError_t launch_init_slot(const DeviceView &v, const int32_t *slots, int nslots, bool warm, double eta,
                             double omega0, hipStream_t s);
 }  // namespace nep
@@ -59,11 +61,12 @@ struct Model {
   // problem
   int N = 0, F = 0, NP = 0, variant = 0, step = 1, has_n = 0, step2 = 0;
   double alpha = 0.5, M = 1e6, eps = 1e-6, sigma4 = -1, cost_n = 0, score_n_coef = 0, w_dis = 0;
-  int R = 0, T = 0, JB = 0, FB = 0, FPB = 8, CPL = 1, max_batch = 1;
+  int R = 0, JB = 0, CPL = 1, max_batch = 1;
   DualLayout dl{};
   IntLayout il{};
-  std::vector<int> row_f, row_src, tile_row0, tile_nrows, tile_f, ftile_ptr;
+  std::vector<int> row_f, row_src, frow;
   std::vector<float> row_m, row_w, row_wobj, row_wsc;
+  std::vector<RowInfo> rows;
   std::vector<double> W;            // [F*N]
   std::vector<double> nat_lb, nat_ub, cost_int;
   std::vector<double> lo, hi, rownorm, rho, gam;
@@ -79,9 +82,14 @@ struct Model {
   bool own_stream = false;
   DeviceView v{};
   std::vector<void *> allocs;
-  int32_t *d_slots = nullptr;
+  int32_t *d_slots = nullptr;   // the slots currently iterating (mirror of `act`)
+  int32_t *d_new = nullptr;     // slots being initialised by nep_lp_submit
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   nep_stats stats{};
+  // streaming state
+  std::vector<int32_t> act;     // slots currently iterating
+  std::vector<uint8_t> busy;    // per slot: iterating
+  nep_lp_opts run{};            // options of the LPs in flight
   ~Model() {
     if (stream) (void)hipStreamSynchronize(stream);
     for (void *p : allocs) (void)hipFree(p);
@@ -219,26 +227,14 @@ int build(Model &m, const nep_model_desc &d) {
     }
   }
 
-  // tiles: consecutive rows of one function, at most 16 rows (4 per wave)
-  const int TR = 16;
-  m.ftile_ptr.assign(F + 1, 0);
-  {
-    int r = 0;
-    for (int f = 0; f < F; ++f) {
-      int r0 = r;
-      while (r < m.R && m.row_f[r] == f) ++r;
-      for (int t0 = r0; t0 < r; t0 += TR) {
-        m.tile_row0.push_back(t0);
-        m.tile_nrows.push_back(std::min(TR, r - t0));
-        m.tile_f.push_back(f);
-      }
-      m.ftile_ptr[f + 1] = (int)m.tile_f.size();
-    }
-  }
-  m.T = (int)m.tile_f.size();
+  // rows of one function are consecutive: frow[f] .. frow[f+1] (one x-pass workgroup each)
+  m.frow.assign(F + 1, 0);
+  for (int r = 0; r < m.R; ++r) m.frow[m.row_f[r] + 1] += 1;
+  for (int f = 0; f < F; ++f) m.frow[f + 1] += m.frow[f];
+  m.rows.resize(m.R);
+  for (int r = 0; r < m.R; ++r)
+    m.rows[r] = RowInfo{m.row_m[r], m.row_w[r], m.row_wobj[r], m.row_wsc[r], m.row_src[r], m.row_f[r], 0, 0};
   m.JB = (N + kWave - 1) / kWave;
-  m.FPB = 8;
-  m.FB = (F + m.FPB - 1) / m.FPB;
 
   // integer-variable layout (variables.py order minus x)
   const int FN = F * N;
@@ -498,6 +494,7 @@ int build(Model &m, const nep_model_desc &d) {
 
 int setup_device(Model &m, int max_batch, void *stream) {
   m.max_batch = max_batch;
+  m.busy.assign(max_batch, 0);
   if (stream) {
     m.stream = (hipStream_t)stream;
   } else {
@@ -507,22 +504,14 @@ int setup_device(Model &m, int max_batch, void *stream) {
   HIPCHK(hipEventCreate(&m.ev0));
   HIPCHK(hipEventCreate(&m.ev1));
   DeviceView &v = m.v;
-  v.N = m.N; v.NP = m.NP; v.F = m.F; v.R = m.R; v.T = m.T; v.JB = m.JB; v.FB = m.FB; v.FPB = m.FPB; v.CPL = m.CPL;
+  v.N = m.N; v.NP = m.NP; v.F = m.F; v.R = m.R; v.JB = m.JB; v.CPL = m.CPL;
   v.has_n = m.has_n; v.step2 = m.step2; v.variant = m.variant;
   v.M = m.M; v.eps = m.eps; v.sigma4 = m.sigma4; v.cost_n = m.cost_n; v.score_n_coef = m.score_n_coef;
   v.w_dis = m.w_dis;
   v.dl = m.dl; v.il = m.il;
   int rc;
-  if ((rc = upload(m, &v.row_f, m.row_f))) return rc;
-  if ((rc = upload(m, &v.row_src, m.row_src))) return rc;
-  if ((rc = upload(m, &v.row_m, m.row_m))) return rc;
-  if ((rc = upload(m, &v.row_w, m.row_w))) return rc;
-  if ((rc = upload(m, &v.row_wobj, m.row_wobj))) return rc;
-  if ((rc = upload(m, &v.row_wsc, m.row_wsc))) return rc;
-  if ((rc = upload(m, &v.tile_row0, m.tile_row0))) return rc;
-  if ((rc = upload(m, &v.tile_nrows, m.tile_nrows))) return rc;
-  if ((rc = upload(m, &v.tile_f, m.tile_f))) return rc;
-  if ((rc = upload(m, &v.ftile_ptr, m.ftile_ptr))) return rc;
+  if ((rc = upload(m, &v.rows, m.rows))) return rc;
+  if ((rc = upload(m, &v.frow, m.frow))) return rc;
   if ((rc = upload(m, &v.gam, m.gam))) return rc;
   if ((rc = upload(m, &v.rho, m.rho))) return rc;
   if ((rc = upload(m, &v.lo, m.lo))) return rc;
@@ -555,10 +544,9 @@ int setup_dense(Model &m, const nep_model_desc &d) {
   v.sint = m.il.n_int;
   v.sdual = m.dl.n_dual;
   v.skty = (int64_t)F * NP + NP + 4;
-  v.spart = (int64_t)m.T * 2 * NP;
-  v.stpart = (int64_t)m.T * NTS;
-  v.sbpart = (int64_t)(m.FB * m.JB + m.JB) * NBS;
-  v.snpart = (int64_t)m.FB * 3 * NP;
+  v.stpart = (int64_t)F * NTS;
+  v.sbpart = (int64_t)(F + m.JB) * NBS;
+  v.snpart = (int64_t)F * 3 * NP;
   if ((rc = dalloc(m, &v.x, (size_t)B * v.sx))) return rc;
   if ((rc = dalloc(m, &v.xa, (size_t)B * v.sx))) return rc;
   if ((rc = dalloc(m, &v.mask, (size_t)B * v.smask))) return rc;
@@ -571,12 +559,12 @@ int setup_dense(Model &m, const nep_model_desc &d) {
   if ((rc = dalloc(m, &v.kz, (size_t)B * v.sdual))) return rc;
   if ((rc = dalloc(m, &v.kza, (size_t)B * v.sdual))) return rc;
   if ((rc = dalloc(m, &v.kty, (size_t)B * v.skty))) return rc;
-  if ((rc = dalloc(m, &v.part, (size_t)B * v.spart))) return rc;
   if ((rc = dalloc(m, &v.tpart, (size_t)B * v.stpart))) return rc;
   if ((rc = dalloc(m, &v.bpart, (size_t)B * v.sbpart))) return rc;
   if ((rc = dalloc(m, &v.npart, (size_t)B * v.snpart))) return rc;
   if ((rc = dalloc(m, &v.ctrl, (size_t)B))) return rc;
   if ((rc = dalloc(m, &m.d_slots, (size_t)B))) return rc;
+  if ((rc = dalloc(m, &m.d_new, (size_t)B))) return rc;
   HIPCHK(hipMemsetAsync(v.ctrl, 0, sizeof(Ctrl) * B, m.stream));
   HIPCHK(hipMemsetAsync(v.x, 0, sizeof(float) * B * v.sx, m.stream));
   HIPCHK(hipMemsetAsync(v.xa, 0, sizeof(float) * B * v.sx, m.stream));
@@ -649,11 +637,7 @@ bool presolve(const Model &m, const double *lbi, const double *ubi, std::vector<
   return true;
 }
 
-int solve_batch(Model &m, int B, const int32_t *slots, const double *lbi, const double *ubi, const nep_lp_opts *opts,
-                double *obj, double *pobj, int32_t *status, int64_t *iters) {
-  auto t0 = std::chrono::steady_clock::now();
-  if (B <= 0) return NEP_OK;
-  if (B > m.max_batch) return fail(NEP_ERR_ARG, "B > max_batch");
+nep_lp_opts resolve_opts(const nep_lp_opts *opts) {
   nep_lp_opts o{};
   o.tol = 1e-7;
   o.cutoff = INF;
@@ -667,64 +651,87 @@ int solve_batch(Model &m, int B, const int32_t *slots, const double *lbi, const 
     if (opts->check_every > 0) o.check_every = opts->check_every;
     o.warm_start = opts->warm_start;
   }
+  return o;
+}
+
+// Start n node LPs: presolve each on the host, upload its bounds and destination mask, initialise
+// the slot (cold or warm) and add it to the iterating set.  status[b] = NEP_LP_INFEASIBLE for a
+// node presolve proves infeasible (it does not iterate), else NEP_LP_ITERATION_LIMIT.
+int submit(Model &m, int n, const int32_t *slots, const double *lbi, const double *ubi, const nep_lp_opts *opts,
+           int32_t *status) {
+  if (n <= 0) return NEP_OK;
+  const nep_lp_opts o = resolve_opts(opts);
+  if (!m.act.empty() && o.check_every != m.run.check_every)
+    return fail(NEP_ERR_STATE, "check_every cannot change while LPs are iterating");
+  for (int b = 0; b < n; ++b) {
+    const int s = slots[b];
+    if (s < 0 || s >= m.max_batch) return fail(NEP_ERR_ARG, "slot out of range");
+    if (m.busy[s]) return fail(NEP_ERR_STATE, "slot " + std::to_string(s) + " is still iterating");
+  }
+  m.run = o;
   DeviceView &v = m.v;
   v.tol = o.tol;
   v.cutoff = o.cutoff;
   v.max_iters = o.max_iters;
-  const int n = m.il.n_int;
-  std::vector<int32_t> act;
+  const int ni = m.il.n_int;
+  std::vector<int32_t> fresh;
   std::vector<double> lb, ub;
   std::vector<uint8_t> mask;
-  for (int b = 0; b < B; ++b) {
+  for (int b = 0; b < n; ++b) {
     const int s = slots[b];
-    if (s < 0 || s >= m.max_batch) return fail(NEP_ERR_ARG, "slot out of range");
-    const bool ok = presolve(m, lbi ? lbi + (size_t)b * n : nullptr, ubi ? ubi + (size_t)b * n : nullptr, lb, ub, mask);
+    const bool ok = presolve(m, lbi ? lbi + (size_t)b * ni : nullptr, ubi ? ubi + (size_t)b * ni : nullptr, lb, ub, mask);
     status[b] = ok ? NEP_LP_ITERATION_LIMIT : NEP_LP_INFEASIBLE;
-    obj[b] = ok ? -INF : INF;
-    pobj[b] = NAN;
-    iters[b] = 0;
     if (!ok) continue;
-    HIPCHK(hipMemcpyAsync(v.lb + (size_t)s * v.sint, lb.data(), n * sizeof(double), hipMemcpyHostToDevice, m.stream));
-    HIPCHK(hipMemcpyAsync(v.ub + (size_t)s * v.sint, ub.data(), n * sizeof(double), hipMemcpyHostToDevice, m.stream));
+    HIPCHK(hipMemcpyAsync(v.lb + (size_t)s * v.sint, lb.data(), ni * sizeof(double), hipMemcpyHostToDevice, m.stream));
+    HIPCHK(hipMemcpyAsync(v.ub + (size_t)s * v.sint, ub.data(), ni * sizeof(double), hipMemcpyHostToDevice, m.stream));
     HIPCHK(hipMemcpyAsync(v.mask + (size_t)s * v.smask, mask.data(), mask.size(), hipMemcpyHostToDevice, m.stream));
-    // synchronous copies above read host vectors that are reused: wait before the next slot
+    // the host vectors are reused for the next node: wait for the copies
     HIPCHK(hipStreamSynchronize(m.stream));
-    act.push_back(s);
+    m.busy[s] = 1;
+    fresh.push_back(s);
   }
-  if (!act.empty()) {
-    HIPCHK(hipMemcpyAsync(m.d_slots, act.data(), act.size() * sizeof(int32_t), hipMemcpyHostToDevice, m.stream));
-    const int na = (int)act.size();
-    HIPCHK(launch_init_slot(v, m.d_slots, na, o.warm_start != 0, m.eta, m.omega0, m.stream));
-    HIPCHK(launch_x_pass(v, m.d_slots, na, false, true, true, true, 0, m.stream));
-    HIPCHK(launch_small_passes(v, m.d_slots, na, false, true, true, true, 0, m.stream));
-    HIPCHK(launch_scalar_pass(v, m.d_slots, na, false, true, true, true, 0, 0, o.check_every, m.stream));
-  }
+  if (fresh.empty()) return NEP_OK;
+  const int nf = (int)fresh.size();
+  HIPCHK(hipMemcpyAsync(m.d_new, fresh.data(), nf * sizeof(int32_t), hipMemcpyHostToDevice, m.stream));
+  HIPCHK(launch_init_slot(v, m.d_new, nf, o.warm_start != 0, m.eta, m.omega0, m.stream));
+  HIPCHK(launch_x_pass(v, m.d_new, nf, false, true, true, true, 0, m.stream));
+  HIPCHK(launch_node_pass(v, m.d_new, nf, false, true, true, true, 0, m.stream));
+  HIPCHK(launch_scalar_pass(v, m.d_new, nf, false, true, true, true, 0, o.check_every, m.stream));
+  m.act.insert(m.act.end(), fresh.begin(), fresh.end());
+  HIPCHK(hipMemcpyAsync(m.d_slots, m.act.data(), m.act.size() * sizeof(int32_t), hipMemcpyHostToDevice, m.stream));
+  HIPCHK(hipStreamSynchronize(m.stream));
+  return NEP_OK;
+}
+
+// Run blocks of `check_every` PDHG iterations on every iterating slot until at least `min_done`
+// of them have finished (min_done <= 0: exactly one block).  Finished slots are reported in
+// done[0 .. *n_done) with their results.
+int advance(Model &m, int min_done, int32_t *n_done, int32_t *done, double *obj, double *pobj, int32_t *status,
+            int64_t *iters) {
+  *n_done = 0;
+  DeviceView &v = m.v;
+  const int ce = m.run.check_every;
   std::vector<Ctrl> ctrl(m.max_batch);
-  // Block of `ce` iterations: it == 0 is the certificate iteration (a plain PDHG step whose input
-  // dual is the previous block's plain output, so it satisfies the row sign constraints and its
-  // Lagrangian is a valid bound); restarts decided there take effect at it == 1; it == ce - 1 is
-  // plain again; the others are reflected Halpern steps.
-  int64_t block_no = 0;
-  while (!act.empty()) {
-    const int na = (int)act.size();
-    const int ce = o.check_every;
-    // one steady-state x-pass launch per block is bracketed by HIP events on the model's stream;
-    // the events are read after the block's own stream sync, so sampling adds no synchronisation
+  while (!m.act.empty()) {
+    const int na = (int)m.act.size();
+    // Block of `ce` iterations: it == 0 is the certificate iteration (a plain PDHG step whose
+    // input dual is the previous block's plain output, so it satisfies the row sign constraints
+    // and its Lagrangian is a valid bound); restarts decided there take effect at it == 1;
+    // it == ce - 1 is plain again; the others are reflected Halpern steps.  One steady-state
+    // x-pass launch per block is bracketed by HIP events on the model's stream; the events are
+    // read after the block's own stream sync, so sampling adds no synchronisation.
     const int sample_it = ce >= 4 ? 2 : -1;
     for (int it = 0; it < ce; ++it) {
       const bool check = it == 0, first = it == 1;
       const bool plain = ce < 4 || it == 0 || it == ce - 1;
       const bool sample = it == sample_it;
-      const int done = check ? (block_no == 0 ? 1 : ce) : 0;
       if (sample) HIPCHK(hipEventRecord(m.ev0, m.stream));
       HIPCHK(launch_x_pass(v, m.d_slots, na, check, false, first, plain, it, m.stream));
       if (sample) HIPCHK(hipEventRecord(m.ev1, m.stream));
-      HIPCHK(launch_small_passes(v, m.d_slots, na, check, false, first, plain, it, m.stream));
-      if (m.step2 || check)
-        HIPCHK(launch_scalar_pass(v, m.d_slots, na, check, false, first, plain, it, done, ce, m.stream));
+      HIPCHK(launch_node_pass(v, m.d_slots, na, check, false, first, plain, it, m.stream));
+      if (m.step2 || check) HIPCHK(launch_scalar_pass(v, m.d_slots, na, check, false, first, plain, it, ce, m.stream));
       m.stats.x_pass_launches += 1;
     }
-    ++block_no;
     HIPCHK(hipMemcpyAsync(ctrl.data(), v.ctrl, sizeof(Ctrl) * m.max_batch, hipMemcpyDeviceToHost, m.stream));
     HIPCHK(hipStreamSynchronize(m.stream));
     if (sample_it >= 0) {
@@ -736,22 +743,65 @@ int solve_batch(Model &m, int B, const int32_t *slots, const double *lbi, const 
     }
     m.stats.lp_iterations += (int64_t)na * ce;
     std::vector<int32_t> still;
-    for (int s : act)
-      if (ctrl[s].active) still.push_back(s);
-    if (still.size() != act.size() && !still.empty())
-      HIPCHK(hipMemcpyAsync(m.d_slots, still.data(), still.size() * sizeof(int32_t), hipMemcpyHostToDevice, m.stream));
-    act.swap(still);
+    for (int s : m.act) {
+      if (ctrl[s].active) {
+        still.push_back(s);
+        continue;
+      }
+      const Ctrl &c = ctrl[s];
+      const int k = (*n_done)++;
+      done[k] = s;
+      status[k] = c.status;
+      iters[k] = c.k;
+      pobj[k] = c.pobj;
+      obj[k] = c.status == NEP_LP_INFEASIBLE ? INF : (c.status == NEP_LP_OPTIMAL ? c.lagr : c.best_lagr);
+      m.busy[s] = 0;
+    }
+    if (still.size() != m.act.size()) {
+      m.act.swap(still);
+      if (!m.act.empty())
+        HIPCHK(hipMemcpyAsync(m.d_slots, m.act.data(), m.act.size() * sizeof(int32_t), hipMemcpyHostToDevice,
+                              m.stream));
+    }
+    if (min_done <= 0 || *n_done >= min_done) break;
   }
-  HIPCHK(hipMemcpyAsync(ctrl.data(), v.ctrl, sizeof(Ctrl) * m.max_batch, hipMemcpyDeviceToHost, m.stream));
   HIPCHK(hipStreamSynchronize(m.stream));
+  return NEP_OK;
+}
+
+int solve_batch(Model &m, int B, const int32_t *slots, const double *lbi, const double *ubi, const nep_lp_opts *opts,
+                double *obj, double *pobj, int32_t *status, int64_t *iters) {
+  auto t0 = std::chrono::steady_clock::now();
+  if (B <= 0) return NEP_OK;
+  if (B > m.max_batch) return fail(NEP_ERR_ARG, "B > max_batch");
+  if (!m.act.empty()) return fail(NEP_ERR_STATE, "streamed LPs are still iterating (nep_lp_advance them first)");
+  std::vector<int> where(m.max_batch, -1);
   for (int b = 0; b < B; ++b) {
-    if (status[b] == NEP_LP_INFEASIBLE) continue;
-    const Ctrl &c = ctrl[slots[b]];
-    status[b] = c.status;
-    iters[b] = c.k;
-    pobj[b] = c.pobj;
-    obj[b] = c.status == NEP_LP_OPTIMAL ? c.lagr : c.best_lagr;
-    if (c.status == NEP_LP_INFEASIBLE) obj[b] = INF;
+    if (slots[b] < 0 || slots[b] >= m.max_batch) return fail(NEP_ERR_ARG, "slot out of range");
+    if (where[slots[b]] >= 0) return fail(NEP_ERR_ARG, "duplicate slot");
+    where[slots[b]] = b;
+  }
+  int rc = submit(m, B, slots, lbi, ubi, opts, status);
+  if (rc) return rc;
+  for (int b = 0; b < B; ++b) {
+    obj[b] = status[b] == NEP_LP_INFEASIBLE ? INF : -INF;
+    pobj[b] = NAN;
+    iters[b] = 0;
+  }
+  std::vector<int32_t> dn(m.max_batch), ds(m.max_batch);
+  std::vector<double> dobj(m.max_batch), dpobj(m.max_batch);
+  std::vector<int64_t> dit(m.max_batch);
+  while (!m.act.empty()) {
+    int32_t nd = 0;
+    rc = advance(m, INT_MAX, &nd, dn.data(), dobj.data(), dpobj.data(), ds.data(), dit.data());
+    if (rc) return rc;
+    for (int k = 0; k < nd; ++k) {
+      const int b = where[dn[k]];
+      status[b] = ds[k];
+      obj[b] = dobj[k];
+      pobj[b] = dpobj[k];
+      iters[b] = dit[k];
+    }
   }
   m.stats.solve_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   return NEP_OK;
@@ -788,7 +838,7 @@ int nep_model_get_info(void *model, nep_model_info *info) {
   const Model &m = *static_cast<Model *>(model);
   info->n_int = m.il.n_int;
   info->n_rows = m.R;
-  info->n_tiles = m.T;
+  info->n_tiles = m.F;
   info->max_batch = m.max_batch;
   info->x_entries = (int64_t)m.R * m.N;
   // B_iter = 4 (2P + 2FN + 2N + 2m), P = x entries iterated, m = dual rows
@@ -801,6 +851,28 @@ int nep_lp_solve_batch(void *model, int32_t B, const int32_t *slots, const doubl
                        const nep_lp_opts *opts, double *obj, double *primal_obj, int32_t *status, int64_t *iters) {
   if (!model || !slots || !obj || !primal_obj || !status || !iters) return fail(NEP_ERR_ARG, "null argument");
   return solve_batch(*static_cast<Model *>(model), B, slots, lb_int, ub_int, opts, obj, primal_obj, status, iters);
+}
+
+int nep_lp_submit(void *model, int32_t n, const int32_t *slots, const double *lb_int, const double *ub_int,
+                  const nep_lp_opts *opts, int32_t *status) {
+  if (!model || (n > 0 && (!slots || !status))) return fail(NEP_ERR_ARG, "null argument");
+  return submit(*static_cast<Model *>(model), n, slots, lb_int, ub_int, opts, status);
+}
+
+int nep_lp_advance(void *model, int32_t min_done, int32_t *n_done, int32_t *done_slots, double *obj,
+                   double *primal_obj, int32_t *status, int64_t *iters) {
+  if (!model || !n_done || !done_slots || !obj || !primal_obj || !status || !iters)
+    return fail(NEP_ERR_ARG, "null argument");
+  auto t0 = std::chrono::steady_clock::now();
+  Model &m = *static_cast<Model *>(model);
+  const int rc = advance(m, min_done, n_done, done_slots, obj, primal_obj, status, iters);
+  m.stats.solve_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  return rc;
+}
+
+int nep_lp_active(void *model) {
+  if (!model) return fail(NEP_ERR_ARG, "null model");
+  return (int)static_cast<Model *>(model)->act.size();
 }
 
 int nep_lp_get_solution(void *model, int32_t slot, double *z_int, float *x_dense) {
@@ -848,6 +920,7 @@ int nep_lp_copy_state(void *model, int32_t src, int32_t dst) {
   if (!model) return fail(NEP_ERR_ARG, "null model");
   Model &m = *static_cast<Model *>(model);
   if (src < 0 || dst < 0 || src >= m.max_batch || dst >= m.max_batch) return fail(NEP_ERR_ARG, "slot out of range");
+  if (m.busy[dst]) return fail(NEP_ERR_STATE, "destination slot is still iterating");
   if (src == dst) return NEP_OK;
   const DeviceView &v = m.v;
   HIPCHK(hipMemcpyAsync(v.x + dst * v.sx, v.x + src * v.sx, v.sx * sizeof(float), hipMemcpyDeviceToDevice, m.stream));
@@ -878,6 +951,7 @@ int nep_lp_get_diag(void *model, int32_t slot, double *out16) {
 int nep_debug_state(void *model, int32_t slot, double *y, double *kz, float *kty, double *lb, double *ub) {
   if (!model) return fail(NEP_ERR_ARG, "null model");
   Model &m = *static_cast<Model *>(model);
+  if (slot < 0 || slot >= m.max_batch) return fail(NEP_ERR_ARG, "slot out of range");
   const DeviceView &v = m.v;
   if (y) HIPCHK(hipMemcpy(y, v.y + slot * v.sdual, v.sdual * sizeof(double), hipMemcpyDeviceToHost));
   if (kz) HIPCHK(hipMemcpy(kz, v.kz + slot * v.sdual, v.sdual * sizeof(double), hipMemcpyDeviceToHost));
@@ -897,7 +971,7 @@ int nep_debug_build(const nep_model_desc *desc, double *eta, double *rho, double
   if (gam) std::memcpy(gam, m.gam.data(), m.gam.size() * sizeof(double));
   if (rownorm) std::memcpy(rownorm, m.rownorm.data(), m.rownorm.size() * sizeof(double));
   if (dims) {
-    dims[0] = m.R; dims[1] = m.T; dims[2] = m.il.n_int; dims[3] = m.dl.n_dual;
+    dims[0] = m.R; dims[1] = m.F; dims[2] = m.il.n_int; dims[3] = m.dl.n_dual;
   }
   return NEP_OK;
 }

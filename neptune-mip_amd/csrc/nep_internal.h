@@ -4,18 +4,18 @@
 // and `max_batch` LP slots (B&B nodes).  Layout in HBM (per slot unless noted):
 //
 //   x     [R][NP] f32   routing rows x̄[r, j]; row r = (function f, source i) or the pooled
-//                       zero-workload sources of f (exact aggregation)
+//                       zero-workload sources of f (exact aggregation); the rows of
+//                       one function are consecutive (frow[f] .. frow[f+1])
 //   xa    [R][NP] f32   restart anchor of x
 //   mask  [F][NP] u8    destination j allowed for function f at this node (c_ub[f,j] > 0)
 //   zi    [n_int] f64   small primal: c, (mf, mt, a, d), n        + anchor zia, bounds lb/ub
 //   y     [n_dual] f64  duals of the dualised rows   + anchor ya, activity kz (iterate) / kza (anchor)
 //   kty   [F*NP + NP + 4] f32  packed duals the x pass needs: y1+y2 per (f,j), y5 per j, yS
-//   part  [T][2][NP] f32  per-tile partial column sums (C1/C2 activity) and CPU sums (C5)
-//   tpart [T][NTS] f64  per-tile scalars (score row, objective, Lagrangian, movement, distance)
-//   npart [FB][3][NP] f64 per-(function block, node) partial sums: memory, Σ_f c, CPU
-//   bpart [FB*JB+JB][NBS] f64 per-block scalars of the small-variable kernels
+//   tpart [F][NTS] f64  per-function scalars of the rows (score row, objective, Lagrangian, movement)
+//   npart [F][3][NP] f64 per-(function, node) shares of the node rows: memory, c, CPU
+//   bpart [F+JB][NBS] f64 per-block scalars of the small variables
 //   ctrl  Ctrl          step sizes, primal weight, restart state, status
-// Static (shared by all slots): row_f/src/m/w/wobj/wsc [R], tiles, D [N][NP] f32, cpr [F][NP] f32,
+// Static (shared by all slots): rows [R] (RowInfo), frow [F+1], D [N][NP] f32, cpr [F][NP] f32,
 // gamma [n_int], rho / lo / hi / rownorm [n_dual], cost_int [n_int].
 #pragma once
 #include <cstdint>
@@ -25,10 +25,20 @@ namespace nep {
 constexpr int kWave = 64;
 constexpr int kTileWaves = 4;            // waves per x-pass workgroup
 constexpr int kTileThreads = kWave * kTileWaves;
+constexpr int kNodeWaves = 4;            // waves per node-pass workgroup
+constexpr int kNodeThreads = kWave * kNodeWaves;
 
-// per-tile scalar partials
+// one routing row (32 B, one scalar load): pooled-row weight m (1 for a single source), workload
+// w = W[f, src], objective weight wobj (cost of x[r, j] = wobj * D[src, j]), score-row weight wsc
+// (step 2), source node (-1 = the pooled zero-workload sources of f), function f
+struct RowInfo {
+  float m, w, wobj, wsc;
+  int32_t src, f, pad0, pad1;
+};
+
+// per-function scalar partials
 enum { TS_SCORE = 0, TS_POBJ, TS_LAGR, TS_MOVE, TS_DIST, TS_EMPTY, NTS };
-// per-j-block scalar partials
+// per-block scalar partials of the small variables
 enum {
   BS_SUMC_NEW = 0,   // sum over (f,j) of c'            (step-2 rows D3/D4)
   BS_SCORE_N,        // score-row n part of the new n   (step-2 MU/MDU)
@@ -61,15 +71,14 @@ struct IntLayout {
 
 struct DeviceView {
   // sizes
-  int N, NP, F, R, T, JB, FB, FPB, CPL;
+  int N, NP, F, R, JB, CPL;
   int has_n, step2, variant;
   double M, eps, sigma4, cost_n, score_n_coef, w_dis;
   DualLayout dl;
   IntLayout il;
   // static
-  const int32_t *row_f, *row_src;
-  const float *row_m, *row_w, *row_wobj, *row_wsc;
-  const int32_t *tile_row0, *tile_nrows, *tile_f, *ftile_ptr;
+  const RowInfo *rows;
+  const int32_t *frow;
   const float *D, *cpr;
   const double *gam, *rho, *lo, *hi, *rownorm, *cost_int, *mem_f;
   // per slot (base pointers; slot stride below)
@@ -78,10 +87,9 @@ struct DeviceView {
   double *zi, *zia, *lb, *ub;
   double *y, *ya, *kz, *kza;             // duals, anchor, activity K z of the iterate and of the anchor
   float *kty;
-  float *part;
   double *tpart, *bpart, *npart;
   Ctrl *ctrl;
-  int64_t sx, smask, sint, sdual, skty, spart, stpart, sbpart, snpart;   // per-slot strides (elements)
+  int64_t sx, smask, sint, sdual, skty, stpart, sbpart, snpart;   // per-slot strides (elements)
   // check/solve parameters
   double tol, cutoff;
   int64_t max_iters;

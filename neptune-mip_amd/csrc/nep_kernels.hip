@@ -3,14 +3,19 @@
 // Iteration = one PDHG operator T (diagonally preconditioned; the primal set keeps every routing
 // row on its simplex), wrapped in reflected restarted Halpern iterations (r2HPDHG):
 //   x̂  = Π_simplex( x̄ − τ (cost_x − Kᵀ_x y) )           x_pass      (HBM-bound)
-//   ẑ  = clip( z − τ γ² (cost_z − Kᵀ_z y) )              fj_pass / node_pass / scalar_pass
-//   ŷ  = prox( y − σ ρ² K(2·[x̂,ẑ] − [x̄,z]) )             fj_pass / node_pass / scalar_pass
+//   ẑ  = clip( z − τ γ² (cost_z − Kᵀ_z y) )              x_pass (c, moved) / node_pass (n) / scalar_pass
+//   ŷ  = prox( y − σ ρ² K(2·[x̂,ẑ] − [x̄,z]) )             same split
 //   w' = λ_k (2·T(w) − w) + (1 − λ_k) w_anchor,  λ_k = (k+1)/(k+2), k = iterations since restart
 // ("plain" iterations take w' = T(w): the certificate iteration and the one before it, so the
 // certificate's dual is a T output and satisfies the row sign constraints).
 // K·[x̂, ẑ] is produced in the same passes that write the iterate (column sums, CPU sums, score
 // row); the iterate's activity K w is kept in `kz` (and the anchor's in `kza`, K is linear), so
 // K(2ẑ − z) = 2·Kẑ − Kz costs no extra pass.
+//
+// Launches per iteration: x_pass (one workgroup per (function f, LP slot): all routing rows of f,
+// then the per-(f,j) variables c / moved_from / moved_to and rows C1/C2/D1/D2 of that f) and
+// node_pass (per-node rows C3/C5/C6/C7 and n); scalar_pass on certificate iterations and on every
+// step-2 iteration.  Every reduction has a fixed order: results are bitwise reproducible.
 //
 // Reference rows (core/solvers/neptune/utils): C1/C2 constraints_step1.py:5-15 (column sums),
 // C3 :18-23, C4 :27-34 (the simplex), C5 :57-65 (CPU), C6/C7 :69-78; step 2 D1-D4
@@ -23,15 +28,26 @@
 
 namespace nep {
 
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+// ---------------------------------------------------------------------------------------------
+// wave reductions
+// ---------------------------------------------------------------------------------------------
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, false));
 }
-__device__ __forceinline__ int wave_sum_i(int v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+__device__ __forceinline__ float readlane_f(float v, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+// Wave-uniform f32 sum: DPP butterfly inside each 16-lane row (quad_perm [1,0,3,2], quad_perm
+// [2,3,0,1], row_ror:4, row_ror:8 — every lane of a row then holds the row sum), then the four
+// row sums read as scalars.  No LDS-crossbar (ds_bpermute) round trips; every lane gets the same
+// value in the same summation order.
+__device__ __forceinline__ float wave_sum_u(float v) {
+  v += dpp_f<0xB1>(v);
+  v += dpp_f<0x4E>(v);
+  v += dpp_f<0x124>(v);
+  v += dpp_f<0x128>(v);
+  return (readlane_f(v, 0) + readlane_f(v, 16)) + (readlane_f(v, 32) + readlane_f(v, 48));
 }
 __device__ __forceinline__ double wave_sum_d(double v) {
 #pragma unroll
@@ -68,235 +84,9 @@ __device__ __forceinline__ double row_viol(double a, double lo, double hi) {
   return fmax(fmax(lo - a, a - hi), 0.0);
 }
 
-// ---------------------------------------------------------------------------------------------
-// x_pass: one workgroup = one tile (consecutive routing rows of ONE function f) of one LP slot.
-// Each wave owns whole rows (N destinations = CPL float4 chunks per lane, 1 KiB per
-// wave-instruction), projects each row on its simplex with Michelot's algorithm (wave
-// reductions), writes x̄' and accumulates the tile's column sums for the C1/C2/C5 rows.
-// ---------------------------------------------------------------------------------------------
-template <int CPL, bool CHECK, bool INIT>
-__global__ __launch_bounds__(kTileThreads) void x_pass(DeviceView v, const int32_t *__restrict__ slots, int first,
-                                                       int plain, int it) {
-  constexpr int E = 4 * CPL;
-  extern __shared__ __attribute__((aligned(16))) float lds[];   // [2][kTileWaves][NP]
-  __shared__ double lds_s[kTileWaves][NTS];
-  const int tile = blockIdx.x;
-  const int slot = slots[blockIdx.y];
-  Ctrl *ctrl = v.ctrl + slot;
-  if (!ctrl->active) return;
-  const int NP = v.NP, F = v.F;
-  const float tau = INIT ? 0.f : (float)ctrl->tau;
-  const bool restart = INIT || (first && ctrl->restart_pending);
-  const bool halp = !INIT && !plain;
-  float lam = 1.f;
-  if (halp) {
-    const double ks = (double)(ctrl->ks_base + it);
-    lam = (float)((ks + 1.0) / (ks + 2.0));
-  }
-  const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x >> 6;
-  const int f = v.tile_f[tile], row0 = v.tile_row0[tile], nrows = v.tile_nrows[tile];
-  float *__restrict__ x = v.x + slot * v.sx;
-  float *__restrict__ xa = v.xa + slot * v.sx;
-  const uint8_t *__restrict__ mask = v.mask + slot * v.smask + (int64_t)f * NP;
-  const float *__restrict__ kty = v.kty + slot * v.skty;
-  const float ys = kty[(int64_t)F * NP + NP];
-
-  float kx[E], cy5[E], cp[E];
-  bool mk[E];
-#pragma unroll
-  for (int q = 0; q < CPL; ++q) {
-    const int j0 = 4 * (lane + kWave * q);
-    if (j0 < NP) {
-      const float4 a = *reinterpret_cast<const float4 *>(kty + (int64_t)f * NP + j0);
-      const float4 b = *reinterpret_cast<const float4 *>(kty + (int64_t)F * NP + j0);
-      const float4 c = *reinterpret_cast<const float4 *>(v.cpr + (int64_t)f * NP + j0);
-      const uchar4 m = *reinterpret_cast<const uchar4 *>(mask + j0);
-      kx[4 * q] = a.x; kx[4 * q + 1] = a.y; kx[4 * q + 2] = a.z; kx[4 * q + 3] = a.w;
-      cp[4 * q] = c.x; cp[4 * q + 1] = c.y; cp[4 * q + 2] = c.z; cp[4 * q + 3] = c.w;
-      cy5[4 * q] = c.x * b.x; cy5[4 * q + 1] = c.y * b.y; cy5[4 * q + 2] = c.z * b.z; cy5[4 * q + 3] = c.w * b.w;
-      mk[4 * q] = m.x; mk[4 * q + 1] = m.y; mk[4 * q + 2] = m.z; mk[4 * q + 3] = m.w;
-    } else {
-#pragma unroll
-      for (int e = 0; e < 4; ++e) { kx[4 * q + e] = 0.f; cy5[4 * q + e] = 0.f; cp[4 * q + e] = 0.f; mk[4 * q + e] = false; }
-    }
-  }
-  float colS[E], colW[E];
-#pragma unroll
-  for (int e = 0; e < E; ++e) { colS[e] = 0.f; colW[e] = 0.f; }
-  double s_score = 0.0, s_pobj = 0.0, s_lagr = 0.0, s_move = 0.0, s_dist = 0.0, s_empty = 0.0;
-
-  for (int rr = wave; rr < nrows; rr += kTileWaves) {
-    const int r = row0 + rr;
-    const float m = v.row_m[r], w = v.row_w[r], wobj = v.row_wobj[r], wsc = v.row_wsc[r];
-    const int src = v.row_src[r];
-    float xv[E], dv[E];
-    float *xrow = x + (int64_t)r * NP;
-    const bool need_d = src >= 0 && (wobj != 0.f || wsc != 0.f);
-#pragma unroll
-    for (int q = 0; q < CPL; ++q) {
-      const int j0 = 4 * (lane + kWave * q);
-      float4 a = make_float4(0.f, 0.f, 0.f, 0.f), d = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (j0 < NP) {
-        a = *reinterpret_cast<const float4 *>(xrow + j0);
-        if (need_d) d = *reinterpret_cast<const float4 *>(v.D + (int64_t)src * NP + j0);
-      }
-      xv[4 * q] = a.x; xv[4 * q + 1] = a.y; xv[4 * q + 2] = a.z; xv[4 * q + 3] = a.w;
-      dv[4 * q] = d.x; dv[4 * q + 1] = d.y; dv[4 * q + 2] = d.z; dv[4 * q + 3] = d.w;
-    }
-    // gradient step (reduced cost of x̄[r, j] = cost − Kᵀy)
-    float vv[E];
-    float s = 0.f;
-    int cnt = 0;
-    const float gs = wsc * ys;
-#pragma unroll
-    for (int e = 0; e < E; ++e) {
-      const float g = wobj * dv[e] - (m * kx[e] + w * cy5[e] + gs * dv[e]);
-      vv[e] = xv[e] - tau * g;
-      if (mk[e]) { s += vv[e]; cnt += 1; }
-    }
-    if (CHECK) {
-      // Lagrangian term of this row: min over the simplex of the reduced cost, in fp64
-      double gmin = INFINITY;
-#pragma unroll
-      for (int e = 0; e < E; ++e) {
-        if (mk[e]) {
-          const double g = (double)wobj * dv[e] -
-                           ((double)m * kx[e] + (double)w * cy5[e] + (double)wsc * (double)ys * dv[e]);
-          gmin = fmin(gmin, g);
-        }
-      }
-      gmin = wave_min_d(gmin);
-      if (lane == 0) s_lagr += gmin;
-    }
-    // Michelot projection onto {x >= 0, sum x = 1} over the allowed destinations
-    s = wave_sum(s);
-    cnt = wave_sum_i(cnt);
-    float theta = INFINITY;
-    if (cnt > 0) {
-      theta = (s - 1.f) / (float)cnt;
-      for (int it = 0; it < 4096; ++it) {
-        float s2 = 0.f;
-        int c2 = 0;
-#pragma unroll
-        for (int e = 0; e < E; ++e)
-          if (mk[e] && vv[e] > theta) { s2 += vv[e]; c2 += 1; }
-        s2 = wave_sum(s2);
-        c2 = wave_sum_i(c2);
-        if (c2 == cnt || c2 == 0) break;
-        cnt = c2;
-        theta = (s2 - 1.f) / (float)c2;
-      }
-    } else if (lane == 0) {
-      s_empty += 1.0;
-    }
-    float xn[E];
-#pragma unroll
-    for (int e = 0; e < E; ++e) xn[e] = mk[e] ? fmaxf(vv[e] - theta, 0.f) : 0.f;
-
-    float *arow = xa + (int64_t)r * NP;
-    // anchor row: needed by the Halpern combination and by the certificate's restart distance
-    float xav[E];
-    if ((halp || CHECK) && !restart) {
-#pragma unroll
-      for (int q = 0; q < CPL; ++q) {
-        const int j0 = 4 * (lane + kWave * q);
-        float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (j0 < NP) a = *reinterpret_cast<const float4 *>(arow + j0);
-        xav[4 * q] = a.x; xav[4 * q + 1] = a.y; xav[4 * q + 2] = a.z; xav[4 * q + 3] = a.w;
-      }
-    } else {
-#pragma unroll
-      for (int e = 0; e < E; ++e) xav[e] = INIT ? xn[e] : xv[e];
-    }
-    if (CHECK && !restart) {
-      double dd = 0.0;
-#pragma unroll
-      for (int e = 0; e < E; ++e) { const double t = (double)xn[e] - xav[e]; dd += t * t; }
-      s_dist += dd;
-    }
-    float xw[E];
-#pragma unroll
-    for (int e = 0; e < E; ++e) xw[e] = halp ? lam * (2.f * xn[e] - xv[e]) + (1.f - lam) * xav[e] : xn[e];
-#pragma unroll
-    for (int q = 0; q < CPL; ++q) {
-      const int j0 = 4 * (lane + kWave * q);
-      if (j0 < NP) {
-        *reinterpret_cast<float4 *>(xrow + j0) = make_float4(xw[4 * q], xw[4 * q + 1], xw[4 * q + 2], xw[4 * q + 3]);
-        if (restart)
-          *reinterpret_cast<float4 *>(arow + j0) =
-              make_float4(xav[4 * q], xav[4 * q + 1], xav[4 * q + 2], xav[4 * q + 3]);
-      }
-    }
-    float sc = 0.f;
-#pragma unroll
-    for (int e = 0; e < E; ++e) {
-      colS[e] += m * xn[e];
-      colW[e] += w * xn[e];
-      sc += dv[e] * xn[e];
-    }
-    s_score += (double)wsc * (double)sc;
-    if (CHECK) {
-      double po = 0.0, mv = 0.0;
-#pragma unroll
-      for (int e = 0; e < E; ++e) {
-        po += (double)dv[e] * xn[e];
-        const double t = (double)xn[e] - xv[e];
-        mv += t * t;
-      }
-      s_pobj += (double)wobj * po;
-      s_move += mv;
-    }
-  }
-
-  // cross-wave reduction of the tile's column partials
-  float *lS = lds, *lW = lds + kTileWaves * NP;
-#pragma unroll
-  for (int q = 0; q < CPL; ++q) {
-    const int j0 = 4 * (lane + kWave * q);
-    if (j0 < NP) {
-      *reinterpret_cast<float4 *>(lS + wave * NP + j0) = make_float4(colS[4 * q], colS[4 * q + 1], colS[4 * q + 2], colS[4 * q + 3]);
-      *reinterpret_cast<float4 *>(lW + wave * NP + j0) = make_float4(colW[4 * q], colW[4 * q + 1], colW[4 * q + 2], colW[4 * q + 3]);
-    }
-  }
-  double vals[NTS] = {s_score, s_pobj, s_lagr, s_move, s_dist, s_empty};
-#pragma unroll
-  for (int k = 0; k < NTS; ++k) {
-    const double t = wave_sum_d(vals[k]);
-    if (lane == 0) lds_s[wave][k] = t;
-  }
-  __syncthreads();
-  float *part = v.part + slot * v.spart + (int64_t)tile * 2 * NP;
-  for (int j = threadIdx.x; j < NP; j += kTileThreads) {
-    float a = 0.f, b = 0.f;
-#pragma unroll
-    for (int wv = 0; wv < kTileWaves; ++wv) { a += lS[wv * NP + j]; b += lW[wv * NP + j]; }
-    part[j] = a;
-    part[NP + j] = b * v.cpr[(int64_t)f * NP + j];
-  }
-  if (threadIdx.x < NTS) {
-    double t = 0.0;
-#pragma unroll
-    for (int wv = 0; wv < kTileWaves; ++wv) t += lds_s[wv][threadIdx.x];
-    v.tpart[slot * v.stpart + (int64_t)tile * NTS + threadIdx.x] = t;
-  }
-}
-
-// ---------------------------------------------------------------------------------------------
-// fj_pass: one wave per (slot, block of 64 destinations j, block of FPB functions).  Finishes the
-// column sums of the tiles of each f, updates c / moved_from / moved_to and the C1/C2/D1/D2 duals,
-// writes the packed f32 duals y1+y2 for the x pass, and the per-(f-block, j) partial sums the
-// node rows need (memory use, Σ_f c, CPU use).
-// ---------------------------------------------------------------------------------------------
 struct SmallAcc {
   double lagr = 0, pobj = 0, res = 0, mvz = 0, mvy = 0, dsz = 0, dsy = 0;
 };
-
-// Halpern weight of the current iteration for a slot (1 on plain iterations: w' = T(w))
-__device__ __forceinline__ double halpern_lambda(const Ctrl *ctrl, bool halp, int it) {
-  if (!halp) return 1.0;
-  const double ks = (double)(ctrl->ks_base + it);
-  return (ks + 1.0) / (ks + 2.0);
-}
 
 // Dual half-step of one row.  Returns the new *iterate* y'; `act` is the row activity at the T
 // output (K·[x̂, ẑ]).  On a Halpern iteration y' = λ(2ŷ − y) + (1 − λ)y_anchor and the iterate's
@@ -368,6 +158,326 @@ __device__ __forceinline__ double primal_step(const DeviceView &v, double *zi, d
   return nz;
 }
 
+// Halpern weight of the current iteration for a slot (1 on plain iterations: w' = T(w))
+__device__ __forceinline__ double halpern_lambda(const Ctrl *ctrl, bool halp, int it) {
+  if (!halp) return 1.0;
+  const double ks = (double)(ctrl->ks_base + it);
+  return (ks + 1.0) / (ks + 2.0);
+}
+
+__device__ __forceinline__ float4 ld4(const float *p) { return *reinterpret_cast<const float4 *>(p); }
+
+// one routing row's operands: x̄ row, delay row D[src, :] (if the row has delay-weighted
+// coefficients) and the anchor row (if needed)
+template <int CPL>
+__device__ __forceinline__ void load_row(const float *__restrict__ xrow, const float *__restrict__ drow,
+                                         const float *__restrict__ arow, bool nd, bool na, int lane, int NP,
+                                         float (&xo)[4 * CPL], float (&dout)[4 * CPL], float (&ao)[4 * CPL]) {
+#pragma unroll
+  for (int q = 0; q < CPL; ++q) {
+    const int j0 = 4 * (lane + kWave * q);
+    float4 a = make_float4(0.f, 0.f, 0.f, 0.f), d = a, an = a;
+    if (j0 < NP) {
+      a = ld4(xrow + j0);
+      if (nd) d = ld4(drow + j0);
+      if (na) an = ld4(arow + j0);
+    }
+    xo[4 * q] = a.x; xo[4 * q + 1] = a.y; xo[4 * q + 2] = a.z; xo[4 * q + 3] = a.w;
+    dout[4 * q] = d.x; dout[4 * q + 1] = d.y; dout[4 * q + 2] = d.z; dout[4 * q + 3] = d.w;
+    ao[4 * q] = an.x; ao[4 * q + 1] = an.y; ao[4 * q + 2] = an.z; ao[4 * q + 3] = an.w;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// x_pass: one workgroup = all routing rows of ONE function f of one LP slot, then the
+// per-(f, j) small variables of that f.
+//  1. rows: each wave owns whole rows (N destinations = CPL float4 chunks per lane, 1 KiB per
+//     wave-instruction; the next row's loads are issued before the current row is processed),
+//     projects each row on its simplex with Michelot's algorithm (DPP sums + ballot counts),
+//     writes x̄' and accumulates column sums (C1/C2) and W-weighted sums (C5);
+//  2. LDS reduction of the column sums across waves;
+//  3. per destination j: c[f,j] (+ moved_from/moved_to in step 2), the C1/C2 (D1/D2) duals,
+//     the packed dual y1+y2 the next iteration's rows read, and f's share of the node rows
+//     (memory, Σ_f c, CPU) for node_pass;
+//  4. (init / certificate / step-2 iterations) the workgroup's scalar partials.
+// ---------------------------------------------------------------------------------------------
+template <int CPL, bool CHECK, bool INIT>
+__global__ __launch_bounds__(kTileThreads) void x_pass(DeviceView v, const int32_t *__restrict__ slots, int first,
+                                                       int plain, int it) {
+  constexpr int E = 4 * CPL;
+  constexpr bool PF = CPL <= 2;   // software prefetch of the next row (register budget)
+  extern __shared__ __attribute__((aligned(16))) float lds[];   // [2][kTileWaves][NP]
+  __shared__ double lds_s[kTileWaves][NTS + NBS];
+  const int f = blockIdx.x;
+  const int slot = slots[blockIdx.y];
+  Ctrl *ctrl = v.ctrl + slot;
+  if (!ctrl->active) return;
+  const int NP = v.NP, F = v.F, N = v.N;
+  const float tau = INIT ? 0.f : (float)ctrl->tau;
+  const bool restart = INIT || (first && ctrl->restart_pending);
+  const bool halp = !INIT && !plain;
+  const double lamd = halpern_lambda(ctrl, halp, it);
+  const float lam = (float)lamd;
+  const bool need_anchor = (halp || CHECK) && !restart;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int r0 = v.frow[f], nrows = v.frow[f + 1] - r0;
+  float *__restrict__ x = v.x + slot * v.sx;
+  float *__restrict__ xa = v.xa + slot * v.sx;
+  const uint8_t *__restrict__ mask = v.mask + slot * v.smask + (int64_t)f * NP;
+  float *__restrict__ kty = v.kty + slot * v.skty;
+  const float ys = kty[(int64_t)F * NP + NP];
+
+  float kx[E], cy5[E];
+  uint32_t mbits = 0;
+#pragma unroll
+  for (int q = 0; q < CPL; ++q) {
+    const int j0 = 4 * (lane + kWave * q);
+    if (j0 < NP) {
+      const float4 a = ld4(kty + (int64_t)f * NP + j0);
+      const float4 b = ld4(kty + (int64_t)F * NP + j0);
+      const float4 c = ld4(v.cpr + (int64_t)f * NP + j0);
+      const uchar4 m = *reinterpret_cast<const uchar4 *>(mask + j0);
+      kx[4 * q] = a.x; kx[4 * q + 1] = a.y; kx[4 * q + 2] = a.z; kx[4 * q + 3] = a.w;
+      cy5[4 * q] = c.x * b.x; cy5[4 * q + 1] = c.y * b.y; cy5[4 * q + 2] = c.z * b.z; cy5[4 * q + 3] = c.w * b.w;
+      mbits |= (uint32_t)(m.x != 0) << (4 * q) | (uint32_t)(m.y != 0) << (4 * q + 1) |
+               (uint32_t)(m.z != 0) << (4 * q + 2) | (uint32_t)(m.w != 0) << (4 * q + 3);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { kx[4 * q + e] = 0.f; cy5[4 * q + e] = 0.f; }
+    }
+  }
+  // allowed destinations of f at this node: the same simplex support for every row of f
+  int cnt_f = 0;
+#pragma unroll
+  for (int e = 0; e < E; ++e) cnt_f += __popcll(__ballot((mbits >> e) & 1u));
+
+  float colS[E], colW[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) { colS[e] = 0.f; colW[e] = 0.f; }
+  double s_score = 0.0, s_pobj = 0.0, s_lagr = 0.0, s_move = 0.0, s_dist = 0.0;
+  const double s_empty = (cnt_f == 0 && threadIdx.x == 0) ? (double)nrows : 0.0;
+
+  float xv[E], dv[E], av[E];
+  for (int rr = wave; rr < nrows; rr += kTileWaves) {
+    const int r = r0 + rr;
+    const RowInfo ri = v.rows[r];
+    const bool nd = ri.src >= 0 && (ri.wobj != 0.f || ri.wsc != 0.f);
+    if (!PF || rr == wave)
+      load_row<CPL>(x + (int64_t)r * NP, v.D + (int64_t)(ri.src < 0 ? 0 : ri.src) * NP, xa + (int64_t)r * NP, nd,
+                    need_anchor, lane, NP, xv, dv, av);
+    float xc[E], dc[E], ac[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) { xc[e] = xv[e]; dc[e] = dv[e]; ac[e] = av[e]; }
+    if (PF && rr + kTileWaves < nrows) {
+      const RowInfo rn = v.rows[r + kTileWaves];
+      const bool ndn = rn.src >= 0 && (rn.wobj != 0.f || rn.wsc != 0.f);
+      load_row<CPL>(x + (int64_t)(r + kTileWaves) * NP, v.D + (int64_t)(rn.src < 0 ? 0 : rn.src) * NP,
+                    xa + (int64_t)(r + kTileWaves) * NP, ndn, need_anchor, lane, NP, xv, dv, av);
+    }
+    const float m = ri.m, w = ri.w, wobj = ri.wobj, wsc = ri.wsc;
+    // gradient step (reduced cost of x̄[r, j] = cost − Kᵀy)
+    float vv[E];
+    float s = 0.f;
+    const float gs = wsc * ys;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const float g = wobj * dc[e] - (m * kx[e] + w * cy5[e] + gs * dc[e]);
+      vv[e] = xc[e] - tau * g;
+      if ((mbits >> e) & 1u) s += vv[e];
+    }
+    if (CHECK) {
+      // Lagrangian term of this row: min over the simplex of the reduced cost, in fp64
+      double gmin = INFINITY;
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        if ((mbits >> e) & 1u) {
+          const double g = (double)wobj * dc[e] -
+                           ((double)m * kx[e] + (double)w * cy5[e] + (double)wsc * (double)ys * dc[e]);
+          gmin = fmin(gmin, g);
+        }
+      }
+      gmin = wave_min_d(gmin);
+      if (lane == 0) s_lagr += gmin;
+    }
+    // Michelot projection onto {x >= 0, sum x = 1} over the allowed destinations
+    float theta = INFINITY;
+    if (cnt_f > 0) {
+      s = wave_sum_u(s);
+      int cnt = cnt_f;
+      theta = (s - 1.f) / (float)cnt;
+      for (int k = 0; k < 4096; ++k) {
+        float s2 = 0.f;
+        int c2 = 0;
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          const bool in = ((mbits >> e) & 1u) && vv[e] > theta;
+          if (in) s2 += vv[e];
+          c2 += __popcll(__ballot(in));
+        }
+        s2 = wave_sum_u(s2);
+        if (c2 == cnt || c2 == 0) break;
+        cnt = c2;
+        theta = (s2 - 1.f) / (float)c2;
+      }
+    }
+    float xn[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) xn[e] = ((mbits >> e) & 1u) ? fmaxf(vv[e] - theta, 0.f) : 0.f;
+
+    // anchor row: needed by the Halpern combination and by the certificate's restart distance
+    float xav[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) xav[e] = need_anchor ? ac[e] : (INIT ? xn[e] : xc[e]);
+    if (CHECK && !restart) {
+      double dd = 0.0;
+#pragma unroll
+      for (int e = 0; e < E; ++e) { const double t = (double)xn[e] - xav[e]; dd += t * t; }
+      s_dist += dd;
+    }
+    float *xrow = x + (int64_t)r * NP;
+    float *arow = xa + (int64_t)r * NP;
+#pragma unroll
+    for (int q = 0; q < CPL; ++q) {
+      const int j0 = 4 * (lane + kWave * q);
+      if (j0 < NP) {
+        float o[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const int e = 4 * q + t;
+          o[t] = halp ? lam * (2.f * xn[e] - xc[e]) + (1.f - lam) * xav[e] : xn[e];
+        }
+        *reinterpret_cast<float4 *>(xrow + j0) = make_float4(o[0], o[1], o[2], o[3]);
+        if (restart)
+          *reinterpret_cast<float4 *>(arow + j0) =
+              make_float4(xav[4 * q], xav[4 * q + 1], xav[4 * q + 2], xav[4 * q + 3]);
+      }
+    }
+    float sc = 0.f;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      colS[e] += m * xn[e];
+      colW[e] += w * xn[e];
+      sc += dc[e] * xn[e];
+    }
+    s_score += (double)wsc * (double)sc;
+    if (CHECK) {
+      double po = 0.0, mv = 0.0;
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        po += (double)dc[e] * xn[e];
+        const double t = (double)xn[e] - xc[e];
+        mv += t * t;
+      }
+      s_pobj += (double)wobj * po;
+      s_move += mv;
+    }
+  }
+
+  // cross-wave reduction of the column partials
+  float *lS = lds, *lW = lds + kTileWaves * NP;
+#pragma unroll
+  for (int q = 0; q < CPL; ++q) {
+    const int j0 = 4 * (lane + kWave * q);
+    if (j0 < NP) {
+      *reinterpret_cast<float4 *>(lS + wave * NP + j0) =
+          make_float4(colS[4 * q], colS[4 * q + 1], colS[4 * q + 2], colS[4 * q + 3]);
+      *reinterpret_cast<float4 *>(lW + wave * NP + j0) =
+          make_float4(colW[4 * q], colW[4 * q + 1], colW[4 * q + 2], colW[4 * q + 3]);
+    }
+  }
+  __syncthreads();
+
+  // per-(f, j) small variables and rows
+  const DualLayout &dl = v.dl;
+  const IntLayout &il = v.il;
+  const double taud = INIT ? 0.0 : ctrl->tau, sigma = ctrl->sigma;
+  const bool copy_anchor = restart;
+  double *zi = v.zi + slot * v.sint, *zia = v.zia + slot * v.sint;
+  const double *lb = v.lb + slot * v.sint, *ub = v.ub + slot * v.sint;
+  double *y = v.y + slot * v.sdual, *ya = v.ya + slot * v.sdual, *kz = v.kz + slot * v.sdual;
+  double *kza = v.kza + slot * v.sdual;
+  double *np_ = v.npart + slot * v.snpart + (int64_t)f * 3 * NP;
+  const double memf = v.mem_f[f];
+  const double yD3a = v.step2 ? y[dl.oD3a] : 0.0, yD3b = v.step2 ? y[dl.oD3b] : 0.0;
+  const double yD4 = v.step2 ? y[dl.oD4] : 0.0;
+  SmallAcc a;
+  double sumc = 0.0;
+  for (int j = threadIdx.x; j < N; j += kTileThreads) {
+    float Sf = 0.f, Uf = 0.f;
+#pragma unroll
+    for (int wv = 0; wv < kTileWaves; ++wv) { Sf += lS[wv * NP + j]; Uf += lW[wv * NP + j]; }
+    const double S = Sf;
+    const double U = (double)(Uf * v.cpr[(int64_t)f * NP + j]);
+    const int idx = f * N + j;
+    const double y1 = y[dl.o1 + idx], y2 = y[dl.o2 + idx];
+    const double y3 = y[dl.o3 + j];
+    const double y6 = v.has_n ? y[dl.o6 + j] : 0.0;
+    const double y7 = v.has_n ? y[dl.o7 + j] : 0.0;
+    double kty_c = -v.M * y1 - y2 + memf * y3 + y6 + y7;
+    double yd1 = 0.0, yd2 = 0.0;
+    if (v.step2) {
+      yd1 = y[dl.oD1 + idx];
+      yd2 = y[dl.oD2 + idx];
+      kty_c += -yd1 + yd2 - yD3a + yD3b + v.sigma4 * yD4;
+    }
+    const double cn = primal_step<CHECK>(v, zi, zia, lb, ub, il.oc + idx, v.cost_int[il.oc + idx] - kty_c, taud,
+                                         copy_anchor, halp, lamd, a);
+    const double y1n = dual_step<CHECK, INIT>(v, y, ya, kz, kza, dl.o1 + idx, S - v.M * cn, y1, sigma, copy_anchor,
+                                              halp, lamd, a);
+    const double y2n = dual_step<CHECK, INIT>(v, y, ya, kz, kza, dl.o2 + idx, S - cn, y2, sigma, copy_anchor, halp,
+                                              lamd, a);
+    if (v.step2) {
+      const double mfn = primal_step<CHECK>(v, zi, zia, lb, ub, il.omf + idx, v.cost_int[il.omf + idx] - yd1, taud,
+                                            copy_anchor, halp, lamd, a);
+      const double mtn = primal_step<CHECK>(v, zi, zia, lb, ub, il.omt + idx, v.cost_int[il.omt + idx] - yd2, taud,
+                                            copy_anchor, halp, lamd, a);
+      dual_step<CHECK, INIT>(v, y, ya, kz, kza, dl.oD1 + idx, mfn - cn, yd1, sigma, copy_anchor, halp, lamd, a);
+      dual_step<CHECK, INIT>(v, y, ya, kz, kza, dl.oD2 + idx, mtn + cn, yd2, sigma, copy_anchor, halp, lamd, a);
+    }
+    kty[(int64_t)f * NP + j] = (float)(y1n + y2n);
+    np_[j] = memf * cn;
+    np_[NP + j] = cn;
+    np_[2 * NP + j] = U;
+    sumc += cn;
+  }
+
+  // scalar partials of this (f, slot): read by scalar_pass on init / certificate / step-2 iterations
+  if (!(INIT || CHECK || v.step2)) return;
+  double vals[NTS + NBS];
+  vals[TS_SCORE] = s_score;
+  vals[TS_POBJ] = s_pobj;
+  vals[TS_LAGR] = s_lagr;
+  vals[TS_MOVE] = s_move;
+  vals[TS_DIST] = s_dist;
+  vals[TS_EMPTY] = s_empty;
+  vals[NTS + BS_SUMC_NEW] = sumc;
+  vals[NTS + BS_SCORE_N] = 0.0;
+  vals[NTS + BS_LAGR] = a.lagr;
+  vals[NTS + BS_POBJ] = a.pobj;
+  vals[NTS + BS_RES] = a.res;
+  vals[NTS + BS_MOVE_Z] = a.mvz;
+  vals[NTS + BS_MOVE_Y] = a.mvy;
+  vals[NTS + BS_DIST_Z] = a.dsz;
+  vals[NTS + BS_DIST_Y] = a.dsy;
+#pragma unroll
+  for (int k = 0; k < NTS + NBS; ++k) {
+    const bool needed = INIT || CHECK || k == TS_SCORE || k == NTS + BS_SUMC_NEW;
+    double t = 0.0;
+    if (needed) t = (k == NTS + BS_RES) ? wave_max_d(vals[k]) : wave_sum_d(vals[k]);
+    if (lane == 0) lds_s[wave][k] = t;
+  }
+  __syncthreads();
+  const int k = threadIdx.x;
+  if (k < NTS + NBS) {
+    double t = 0.0;
+#pragma unroll
+    for (int wv = 0; wv < kTileWaves; ++wv) t = (k == NTS + BS_RES) ? fmax(t, lds_s[wv][k]) : t + lds_s[wv][k];
+    if (k < NTS) v.tpart[slot * v.stpart + (int64_t)f * NTS + k] = t;
+    else v.bpart[slot * v.sbpart + (int64_t)f * NBS + (k - NTS)] = t;
+  }
+}
+
 __device__ __forceinline__ void write_bpart(double *bp, const SmallAcc &a, double sumc, double score_n, int lane) {
   double vals[NBS];
   vals[BS_SUMC_NEW] = sumc;
@@ -386,91 +496,50 @@ __device__ __forceinline__ void write_bpart(double *bp, const SmallAcc &a, doubl
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// node_pass: one workgroup per (slot, block of 64 nodes j): the waves sum the per-function
+// shares of the node rows (fixed order), then wave 0 updates rows C3 (memory), C5 (CPU), n and
+// C6/C7.
+// ---------------------------------------------------------------------------------------------
 template <bool CHECK, bool INIT>
-__global__ __launch_bounds__(kWave) void fj_pass(DeviceView v, const int32_t *__restrict__ slots, int first, int plain,
-                                                 int it) {
-  const int jb = blockIdx.x, fb = blockIdx.y;
-  const int slot = slots[blockIdx.z];
-  Ctrl *ctrl = v.ctrl + slot;
-  if (!ctrl->active) return;
-  const int lane = threadIdx.x;
-  const int j = jb * kWave + lane;
-  const bool valid = j < v.N;
-  const int N = v.N, NP = v.NP, F = v.F;
-  const DualLayout &dl = v.dl;
-  const IntLayout &il = v.il;
-  const double tau = INIT ? 0.0 : ctrl->tau, sigma = ctrl->sigma;
-  const bool copy_anchor = INIT || (first && ctrl->restart_pending);
-  const bool halp = !INIT && !plain;
-  const double lam = halpern_lambda(ctrl, halp, it);
-  double *zi = v.zi + slot * v.sint, *zia = v.zia + slot * v.sint;
-  const double *lb = v.lb + slot * v.sint, *ub = v.ub + slot * v.sint;
-  double *y = v.y + slot * v.sdual, *ya = v.ya + slot * v.sdual, *kz = v.kz + slot * v.sdual;
-  double *kza = v.kza + slot * v.sdual;
-  float *kty = v.kty + slot * v.skty;
-  const float *part = v.part + slot * v.spart;
-  SmallAcc a;
-  double U = 0.0, memc = 0.0, sumc = 0.0;
-  const int f0 = fb * v.FPB, f1 = min(F, f0 + v.FPB);
-  if (valid) {
-    const double y3 = y[dl.o3 + j];
-    const double y6 = v.has_n ? y[dl.o6 + j] : 0.0;
-    const double y7 = v.has_n ? y[dl.o7 + j] : 0.0;
-    const double yD3a = v.step2 ? y[dl.oD3a] : 0.0, yD3b = v.step2 ? y[dl.oD3b] : 0.0;
-    const double yD4 = v.step2 ? y[dl.oD4] : 0.0;
-    for (int f = f0; f < f1; ++f) {
-      double S = 0.0;
-      for (int t = v.ftile_ptr[f]; t < v.ftile_ptr[f + 1]; ++t) {
-        S += part[(int64_t)t * 2 * NP + j];
-        U += part[(int64_t)t * 2 * NP + NP + j];
-      }
-      const int idx = f * N + j;
-      const double y1 = y[dl.o1 + idx], y2 = y[dl.o2 + idx];
-      double kty_c = -v.M * y1 - y2 + v.mem_f[f] * y3 + y6 + y7;
-      double yd1 = 0.0, yd2 = 0.0;
-      if (v.step2) {
-        yd1 = y[dl.oD1 + idx];
-        yd2 = y[dl.oD2 + idx];
-        kty_c += -yd1 + yd2 - yD3a + yD3b + v.sigma4 * yD4;
-      }
-      const double cn = primal_step<CHECK>(v, zi, zia, lb, ub, il.oc + idx, v.cost_int[il.oc + idx] - kty_c, tau,
-                                           copy_anchor, halp, lam, a);
-      const double y1n = dual_step<CHECK, INIT>(v, y, ya, kz, kza, dl.o1 + idx, S - v.M * cn, y1, sigma, copy_anchor,
-                                                halp, lam, a);
-      const double y2n = dual_step<CHECK, INIT>(v, y, ya, kz, kza, dl.o2 + idx, S - cn, y2, sigma, copy_anchor, halp,
-                                                lam, a);
-      if (v.step2) {
-        const double mfn = primal_step<CHECK>(v, zi, zia, lb, ub, il.omf + idx, v.cost_int[il.omf + idx] - yd1, tau,
-                                              copy_anchor, halp, lam, a);
-        const double mtn = primal_step<CHECK>(v, zi, zia, lb, ub, il.omt + idx, v.cost_int[il.omt + idx] - yd2, tau,
-                                              copy_anchor, halp, lam, a);
-        dual_step<CHECK, INIT>(v, y, ya, kz, kza, dl.oD1 + idx, mfn - cn, yd1, sigma, copy_anchor, halp, lam, a);
-        dual_step<CHECK, INIT>(v, y, ya, kz, kza, dl.oD2 + idx, mtn + cn, yd2, sigma, copy_anchor, halp, lam, a);
-      }
-      memc += v.mem_f[f] * cn;
-      sumc += cn;
-      kty[(int64_t)f * NP + j] = (float)(y1n + y2n);
-    }
-    double *np_ = v.npart + slot * v.snpart + (int64_t)fb * 3 * NP;
-    np_[j] = memc;
-    np_[NP + j] = sumc;
-    np_[2 * NP + j] = U;
-  }
-  write_bpart(v.bpart + slot * v.sbpart + ((int64_t)fb * v.JB + jb) * NBS, a, valid ? sumc : 0.0, 0.0, lane);
-}
-
-// node_pass: one wave per (slot, block of 64 nodes j): rows C3 (memory), C5 (CPU), n, C6/C7.
-template <bool CHECK, bool INIT>
-__global__ __launch_bounds__(kWave) void node_pass(DeviceView v, const int32_t *__restrict__ slots, int first,
-                                                   int plain, int it) {
+__global__ __launch_bounds__(kNodeThreads) void node_pass(DeviceView v, const int32_t *__restrict__ slots, int first,
+                                                          int plain, int it) {
+  __shared__ double red[kNodeWaves][3][kWave];
   const int jb = blockIdx.x;
   const int slot = slots[blockIdx.y];
   Ctrl *ctrl = v.ctrl + slot;
   if (!ctrl->active) return;
-  const int lane = threadIdx.x;
+  const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x >> 6;
   const int j = jb * kWave + lane;
   const bool valid = j < v.N;
   const int NP = v.NP, F = v.F;
+  {
+    const int per = (F + kNodeWaves - 1) / kNodeWaves;
+    const int f0 = wave * per, f1 = min(F, f0 + per);
+    double memc = 0.0, sumc = 0.0, U = 0.0;
+    if (valid) {
+      const double *np_ = v.npart + slot * v.snpart;
+#pragma unroll 4
+      for (int f = f0; f < f1; ++f) {
+        const double *p = np_ + (int64_t)f * 3 * NP;
+        memc += p[j];
+        sumc += p[NP + j];
+        U += p[2 * NP + j];
+      }
+    }
+    red[wave][0][lane] = memc;
+    red[wave][1][lane] = sumc;
+    red[wave][2][lane] = U;
+  }
+  __syncthreads();
+  if (wave != 0) return;
+  double memc = 0.0, sumc = 0.0, U = 0.0;
+#pragma unroll
+  for (int wv = 0; wv < kNodeWaves; ++wv) {
+    memc += red[wv][0][lane];
+    sumc += red[wv][1][lane];
+    U += red[wv][2][lane];
+  }
   const DualLayout &dl = v.dl;
   const IntLayout &il = v.il;
   const double tau = INIT ? 0.0 : ctrl->tau, sigma = ctrl->sigma;
@@ -485,13 +554,6 @@ __global__ __launch_bounds__(kWave) void node_pass(DeviceView v, const int32_t *
   SmallAcc a;
   double score_n = 0.0;
   if (valid) {
-    double memc = 0.0, sumc = 0.0, U = 0.0;
-    const double *np_ = v.npart + slot * v.snpart;
-    for (int fb = 0; fb < v.FB; ++fb) {
-      memc += np_[(int64_t)fb * 3 * NP + j];
-      sumc += np_[(int64_t)fb * 3 * NP + NP + j];
-      U += np_[(int64_t)fb * 3 * NP + 2 * NP + j];
-    }
     dual_step<CHECK, INIT>(v, y, ya, kz, kza, dl.o3 + j, memc, y[dl.o3 + j], sigma, copy_anchor, halp, lam, a);
     const double y5n = dual_step<CHECK, INIT>(v, y, ya, kz, kza, dl.o5 + j, U, y[dl.o5 + j], sigma, copy_anchor, halp,
                                               lam, a);
@@ -507,7 +569,7 @@ __global__ __launch_bounds__(kWave) void node_pass(DeviceView v, const int32_t *
       score_n = v.score_n_coef * nn;
     }
   }
-  write_bpart(v.bpart + slot * v.sbpart + ((int64_t)v.FB * v.JB + jb) * NBS, a, 0.0, score_n, lane);
+  write_bpart(v.bpart + slot * v.sbpart + ((int64_t)F + jb) * NBS, a, 0.0, score_n, lane);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -517,7 +579,7 @@ __global__ __launch_bounds__(kWave) void node_pass(DeviceView v, const int32_t *
 // ---------------------------------------------------------------------------------------------
 template <bool CHECK, bool INIT>
 __global__ __launch_bounds__(256) void scalar_pass(DeviceView v, const int32_t *__restrict__ slots, int first,
-                                                   int plain, int it, int iters_done, int block_len) {
+                                                   int plain, int it, int block_len) {
   __shared__ double red[256];
   __shared__ double tot[NTS + NBS];
   const int slot = slots[blockIdx.x];
@@ -526,13 +588,13 @@ __global__ __launch_bounds__(256) void scalar_pass(DeviceView v, const int32_t *
   const int tid = threadIdx.x;
   const double *tp = v.tpart + slot * v.stpart;
   const double *bp = v.bpart + slot * v.sbpart;
-  const int nb = v.FB * v.JB + v.JB;
+  const int nb = v.F + v.JB;
   // deterministic block reductions (fixed order per thread, fixed tree)
   for (int k = 0; k < NTS + NBS; ++k) {
     const bool is_max = (k == NTS + BS_RES);
     double acc = 0.0;
     if (k < NTS) {
-      for (int t = tid; t < v.T; t += 256) acc += tp[(int64_t)t * NTS + k];
+      for (int t = tid; t < v.F; t += 256) acc += tp[(int64_t)t * NTS + k];
     } else {
       for (int t = tid; t < nb; t += 256) {
         const double u = bp[(int64_t)t * NBS + (k - NTS)];
@@ -597,8 +659,11 @@ __global__ __launch_bounds__(256) void scalar_pass(DeviceView v, const int32_t *
   }
   if (!CHECK) return;
 
-  ctrl->k += iters_done;
-  ctrl->k_since_restart += iters_done;
+  // iterations since the last certificate: 1 at the slot's first certificate (its first
+  // iteration), a whole block afterwards — per slot, so slots may join between blocks
+  const int64_t done = ctrl->k == 0 ? 1 : block_len;
+  ctrl->k += done;
+  ctrl->k_since_restart += done;
   ctrl->restart_pending = 0;
   if (tot[TS_EMPTY] > 0) { ctrl->status = 2; ctrl->active = 0; return; }
   const double lagr = a.lagr, pobj = a.pobj, res = a.res;
@@ -683,7 +748,7 @@ __global__ void init_slot(DeviceView v, const int32_t *__restrict__ slots, int w
 template <int CPL>
 static hipError_t launch_x_cpl(const DeviceView &v, const int32_t *slots, int nslots, bool check, bool init,
                                bool first, bool plain, int it, hipStream_t s) {
-  dim3 grid(v.T, nslots), block(kTileThreads);
+  dim3 grid(v.F, nslots), block(kTileThreads);
   const size_t lds = (size_t)2 * kTileWaves * v.NP * sizeof(float);
   const int fi = first ? 1 : 0, pl = plain ? 1 : 0;
   if (init) hipLaunchKernelGGL((x_pass<CPL, false, true>), grid, block, lds, s, v, slots, fi, pl, it);
@@ -703,33 +768,26 @@ hipError_t launch_x_pass(const DeviceView &v, const int32_t *slots, int nslots, 
   }
 }
 
-hipError_t launch_small_passes(const DeviceView &v, const int32_t *slots, int nslots, bool check, bool init,
-                               bool first, bool plain, int it, hipStream_t s) {
+hipError_t launch_node_pass(const DeviceView &v, const int32_t *slots, int nslots, bool check, bool init, bool first,
+                            bool plain, int it, hipStream_t s) {
   const int fi = first ? 1 : 0, pl = plain ? 1 : 0;
-  dim3 g1(v.JB, v.FB, nslots), g2(v.JB, nslots), block(kWave);
-  if (init) {
-    hipLaunchKernelGGL((fj_pass<false, true>), g1, block, 0, s, v, slots, fi, pl, it);
-    hipLaunchKernelGGL((node_pass<false, true>), g2, block, 0, s, v, slots, fi, pl, it);
-  } else if (check) {
-    hipLaunchKernelGGL((fj_pass<true, false>), g1, block, 0, s, v, slots, fi, pl, it);
-    hipLaunchKernelGGL((node_pass<true, false>), g2, block, 0, s, v, slots, fi, pl, it);
-  } else {
-    hipLaunchKernelGGL((fj_pass<false, false>), g1, block, 0, s, v, slots, fi, pl, it);
-    hipLaunchKernelGGL((node_pass<false, false>), g2, block, 0, s, v, slots, fi, pl, it);
-  }
+  dim3 grid(v.JB, nslots), block(kNodeThreads);
+  if (init) hipLaunchKernelGGL((node_pass<false, true>), grid, block, 0, s, v, slots, fi, pl, it);
+  else if (check) hipLaunchKernelGGL((node_pass<true, false>), grid, block, 0, s, v, slots, fi, pl, it);
+  else hipLaunchKernelGGL((node_pass<false, false>), grid, block, 0, s, v, slots, fi, pl, it);
   return hipGetLastError();
 }
 
 hipError_t launch_scalar_pass(const DeviceView &v, const int32_t *slots, int nslots, bool check, bool init,
-                              bool first, bool plain, int it, int iters_done, int block_len, hipStream_t s) {
+                              bool first, bool plain, int it, int block_len, hipStream_t s) {
   dim3 grid(nslots), block(256);
   const int fi = first ? 1 : 0, pl = plain ? 1 : 0;
   if (init)
-    hipLaunchKernelGGL((scalar_pass<false, true>), grid, block, 0, s, v, slots, fi, pl, it, iters_done, block_len);
+    hipLaunchKernelGGL((scalar_pass<false, true>), grid, block, 0, s, v, slots, fi, pl, it, block_len);
   else if (check)
-    hipLaunchKernelGGL((scalar_pass<true, false>), grid, block, 0, s, v, slots, fi, pl, it, iters_done, block_len);
+    hipLaunchKernelGGL((scalar_pass<true, false>), grid, block, 0, s, v, slots, fi, pl, it, block_len);
   else
-    hipLaunchKernelGGL((scalar_pass<false, false>), grid, block, 0, s, v, slots, fi, pl, it, iters_done, block_len);
+    hipLaunchKernelGGL((scalar_pass<false, false>), grid, block, 0, s, v, slots, fi, pl, it, block_len);
   return hipGetLastError();
 }
 
