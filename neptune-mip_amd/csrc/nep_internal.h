@@ -25,7 +25,7 @@ namespace nep {
 constexpr int kWave = 64;
 constexpr int kTileWaves = 4;            // waves per x-pass workgroup
 constexpr int kTileThreads = kWave * kTileWaves;
-constexpr int kNodeWaves = 4;            // waves per node-pass workgroup
+constexpr int kNodeWaves = 16;           // waves per node-pass workgroup (each sums F/16 functions)
 constexpr int kNodeThreads = kWave * kNodeWaves;
 
 // one routing row (32 B, one scalar load): pooled-row weight m (1 for a single source), workload

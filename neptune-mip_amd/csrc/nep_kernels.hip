@@ -49,6 +49,13 @@ __device__ __forceinline__ float wave_sum_u(float v) {
   v += dpp_f<0x128>(v);
   return (readlane_f(v, 0) + readlane_f(v, 16)) + (readlane_f(v, 32) + readlane_f(v, 48));
 }
+__device__ __forceinline__ float wave_max_u(float v) {
+  v = fmaxf(v, dpp_f<0xB1>(v));
+  v = fmaxf(v, dpp_f<0x4E>(v));
+  v = fmaxf(v, dpp_f<0x124>(v));
+  v = fmaxf(v, dpp_f<0x128>(v));
+  return fmaxf(fmaxf(readlane_f(v, 0), readlane_f(v, 16)), fmaxf(readlane_f(v, 32), readlane_f(v, 48)));
+}
 __device__ __forceinline__ double wave_sum_d(double v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
@@ -300,25 +307,45 @@ __global__ __launch_bounds__(kTileThreads) void x_pass(DeviceView v, const int32
       gmin = wave_min_d(gmin);
       if (lane == 0) s_lagr += gmin;
     }
-    // Michelot projection onto {x >= 0, sum x = 1} over the allowed destinations
+    // Projection onto {x >= 0, sum x = 1} over the allowed destinations: the threshold theta is
+    // the root of f(t) = sum_j max(v_j - t, 0) - 1 (convex, decreasing).  Michelot's iteration is
+    // Newton's method on f from the left (t <- (S(t) - 1) / c(t), S/c = sum/count of v > t) and is
+    // exact once the count stops changing, but it can take O(N) steps when many values sit just
+    // above the root.  Safeguard: after 4 Newton steps, alternate bisection steps on the bracket
+    // [lo, hi] (f(lo) >= 0 > f(hi), width <= 1 from [vmax - 1, vmax]) with Newton steps.  Every step
+    // costs one DPP sum and E ballots; the converged theta is the same (S* - 1) / |S*| Michelot
+    // returns, summed in the same order.
     float theta = INFINITY;
     if (cnt_f > 0) {
-      s = wave_sum_u(s);
-      int cnt = cnt_f;
-      theta = (s - 1.f) / (float)cnt;
-      for (int k = 0; k < 4096; ++k) {
+      float vm = -INFINITY;
+#pragma unroll
+      for (int e = 0; e < E; ++e)
+        if ((mbits >> e) & 1u) vm = fmaxf(vm, vv[e]);
+      float hi = wave_max_u(vm);
+      float lo_s = wave_sum_u(s);   // S(-inf), c(-inf) = cnt_f
+      int lo_c = cnt_f;
+      float lo = -INFINITY;
+      for (int k = 0; k < 96; ++k) {
+        const bool bisect = k >= 4 && (k & 1) && lo > -INFINITY;
+        const float t = bisect ? 0.5f * (lo + hi) : (lo_s - 1.f) / (float)lo_c;
         float s2 = 0.f;
         int c2 = 0;
 #pragma unroll
         for (int e = 0; e < E; ++e) {
-          const bool in = ((mbits >> e) & 1u) && vv[e] > theta;
+          const bool in = ((mbits >> e) & 1u) && vv[e] > t;
           if (in) s2 += vv[e];
           c2 += __popcll(__ballot(in));
         }
         s2 = wave_sum_u(s2);
-        if (c2 == cnt || c2 == 0) break;
-        cnt = c2;
-        theta = (s2 - 1.f) / (float)c2;
+        if (!bisect) {
+          theta = t;
+          if (c2 == lo_c || c2 == 0) break;   // support unchanged: t is the exact threshold
+          lo = t; lo_s = s2; lo_c = c2;
+        } else if (s2 - t * (float)c2 - 1.f >= 0.f && c2 > 0) {
+          lo = t; lo_s = s2; lo_c = c2;
+        } else {
+          hi = t;
+        }
       }
     }
     float xn[E];

@@ -1,0 +1,84 @@
+#!/usr/bin/env python3
+"""HBM traffic of the bench's dominant kernel (x_pass) from rocprofv3 PMC counters.
+
+On the GPU box, one counter per pass (FETCH_SIZE and WRITE_SIZE do not fit one TCC pass):
+  rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run -- python3 tools/traffic.py run
+  rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run -- python3 tools/traffic.py run
+Then (anywhere):
+  python3 tools/traffic.py summarize gpurun_out/pmc_fetch gpurun_out/pmc_write > profiles/traffic.json
+
+`run` builds bench.py's default model (same generator, seed, batch), starts the batch's node LPs
+cold and runs 4 blocks of PDHG iterations: a few hundred dispatches, x_pass steady-state launches
+with all `batch` LPs active, as in the bench's timed region.  `summarize` averages the counters
+over the steady-state x_pass launches (x_pass<CPL, false, false>, full grid) and converts them:
+FETCH_SIZE and WRITE_SIZE are KiB (rocprofiler-sdk derived_counters.xml); FETCH_SIZE is doubled for
+wide streaming reads on gfx950 (MI355X_MICROARCH.md, HBM).
+"""
+import json
+import os
+import sqlite3
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(REPO, "neptune-mip_amd"), REPO]
+
+
+def run():
+    import numpy as np
+    import bench
+    from core.engine.lp import LPModel
+    from core.utils import data_to_solver_input
+    from core.utils.synthetic import synthetic_payload
+    a = bench.parse([])
+    p = synthetic_payload(a.nodes, a.functions, seed=a.seed)
+    d = data_to_solver_input(p, with_db=False)
+    m = LPModel(d, "MinDelayAndUtilization", step=1, alpha=p["solver"]["args"]["alpha"], max_batch=a.batch)
+    lb, ub = bench.node_bounds(m.n_int, a.functions, a.nodes, a.batch, a.fix, seed=a.seed)
+    m.submit(np.arange(a.batch), lb, ub, tol=a.tol, max_iters=a.max_iters, check_every=a.check_every)
+    for _ in range(4):
+        m.advance(0)
+    print(json.dumps({"workload": bench.workload_name(a), "active": m.active(), "P": m.info.x_entries}))
+    m.close()
+
+
+def _counters(d):
+    dbs = [os.path.join(r, f) for r, _, fs in os.walk(d) for f in fs if f.endswith(".db")]
+    vals = {}
+    for db in dbs:
+        c = sqlite3.connect(db)
+        q = ("select k.name, k.grid_y, p.counter_name, p.value from counters_collection p "
+             "join kernels k on k.dispatch_id = p.dispatch_id")
+        try:
+            rows = list(c.execute(q))
+        except sqlite3.Error:
+            rows = [(r[0], r[1], r[2], r[3]) for r in c.execute(
+                "select kernel_name, grid_y, counter_name, counter_value from counters_collection")]
+        for name, gy, cname, v in rows:
+            if "x_pass" in name and "false, false" in name:
+                vals.setdefault((cname, gy), []).append(float(v))
+    return vals
+
+
+def summarize(fetch_dir, write_dir):
+    import bench
+    a = bench.parse([])
+    f = _counters(fetch_dir)
+    w = _counters(write_dir)
+    fk = max(f, key=lambda k: (k[1], len(f[k])))
+    wk = max(w, key=lambda k: (k[1], len(w[k])))
+    fetch_kib = sum(f[fk]) / len(f[fk])
+    write_kib = sum(w[wk]) / len(w[wk])
+    fetch_b = 2.0 * fetch_kib * 1024.0
+    write_b = write_kib * 1024.0
+    out = {"workload": bench.workload_name(a), "kernel": "x_pass<CPL,false,false>", "lps_per_launch": fk[1],
+           "fetch_kib_raw": fetch_kib, "write_kib_raw": write_kib, "fetch_bytes": fetch_b, "write_bytes": write_b,
+           "bytes_per_launch": fetch_b + write_b, "launches": [len(f[fk]), len(w[wk])],
+           "note": "FETCH_SIZE x2 (gfx950 wide-read tally), KiB -> bytes; per steady-state x_pass launch"}
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    if sys.argv[1] == "run":
+        run()
+    else:
+        summarize(sys.argv[2], sys.argv[3])
