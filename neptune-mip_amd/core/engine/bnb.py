@@ -9,6 +9,13 @@ Branching variables: the placement binaries c[f,j] and the node binaries n[j] of
 integer vector (include/neptune_lp.h).  moved_from / moved_to / allocated / deallocated follow
 from c — with c integral their LP optimum is integral — and are never branched on.
 
+Multi-GPU: with a communicator (`core/engine/comm.py`, one rank per GPU) every
+rank runs the same search redundantly until the open-node frontier holds `world * batch` nodes,
+then keeps the frontier nodes whose canonical position is its rank modulo `world` and searches
+those subtrees alone.  Per batch the ranks exchange the incumbent value (all-reduce MIN, 8 B) and
+their open-node counts (all-reduce SUM, termination); at the end the owner of the best incumbent
+(lowest rank on ties) broadcasts its placement.  No collective runs inside an LP.
+
 Exactness:
   * a node's value is the engine's certified Lagrangian bound, a valid lower bound even when PDHG
     stopped at its iteration limit, so pruning never discards the optimum;
@@ -23,6 +30,7 @@ import time
 
 import numpy as np
 
+from .comm import LocalComm
 from .lp import LP_CUTOFF, LP_INFEASIBLE, LP_OPTIMAL
 
 OPTIMAL, INFEASIBLE, LIMIT = "OPTIMAL", "INFEASIBLE", "LIMIT"
@@ -60,7 +68,7 @@ class BranchAndBound:
     """
 
     def __init__(self, lp, workload, fn_mem, node_mem, batch=16, tol=1e-7, gap=1e-6, max_iters=100000,
-                 node_limit=20000, time_limit=None, upper_bound=math.inf, flow_tol=1e-4, log=None):
+                 node_limit=20000, time_limit=None, upper_bound=math.inf, flow_tol=1e-4, log=None, comm=None):
         self.lp = lp
         self.N, self.F = lp.N, lp.F
         L = lp.layout()
@@ -76,6 +84,7 @@ class BranchAndBound:
         self.ub0 = upper_bound
         self.flow_tol = flow_tol
         self.log = log or (lambda *_: None)
+        self.comm = comm or LocalComm()
         self.branch_vars = list(range(self.c0, self.c1))
         if self.n_range is not None:
             self.branch_vars += list(range(*self.n_range))
@@ -152,9 +161,27 @@ class BranchAndBound:
         pending_leaves = []
         seen_leaves = set()
         limit_hit = False
-        while heap or pending_leaves:
+        comm = self.comm
+        sharded = comm.world == 1
+        while True:
+            if not sharded and len(heap) >= comm.world * self.batch:
+                # deal the (identical on every rank) frontier: canonical order, round robin
+                heap.sort()
+                heap = [h for i, h in enumerate(heap) if i % comm.world == comm.rank]
+                heapq.heapify(heap)
+                pending_leaves = [lf for i, lf in enumerate(pending_leaves) if i % comm.world == comm.rank]
+                sharded = True
+            if comm.world > 1 and sharded:
+                inc = comm.min(inc)
+                if comm.sum(len(heap) + len(pending_leaves)) == 0:
+                    break
+            elif not (heap or pending_leaves):
+                break
             if res.nodes >= self.node_limit or (self.time_limit and time.time() - t0 > self.time_limit):
                 limit_hit = True
+                if comm.world > 1 and sharded:
+                    heap, pending_leaves = [], []
+                    continue
                 break
             batch = []
             while pending_leaves and len(batch) < self.batch:
@@ -219,6 +246,21 @@ class BranchAndBound:
             res.bound = min(min(h[0] for h in heap), inc)
         else:
             res.bound = inc
+        if comm.world > 1:
+            res.bound = comm.min(res.bound)
+            limit_hit = comm.sum(int(limit_hit)) > 0
+            # the owner of the best incumbent (lowest rank on ties) broadcasts the placement
+            mine = res.objective is not None and res.objective <= inc
+            owner = int(comm.min(comm.rank if mine else comm.world))
+            if owner < comm.world:
+                nz = self.lp.n_int
+                z = res.z if mine and comm.rank == owner else np.zeros(nz)
+                x = res.x if mine and comm.rank == owner else np.zeros((self.N, self.F, self.N), np.float32)
+                res.z = comm.bcast(np.asarray(z, np.float64), owner)
+                res.x = comm.bcast(np.asarray(x, np.float32), owner)
+                res.objective = inc
+            res.nodes = comm.sum(res.nodes)
+            res.lps = comm.sum(res.lps)
         if res.objective is None:
             res.status = LIMIT if limit_hit else INFEASIBLE
         else:
