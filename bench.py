@@ -9,11 +9,14 @@ objective `neptune/utils/objectives.py:30-52`).  Every node is a child of the ro
 the root's primal/dual state, as a B&B child is from its parent (`--cold`: from zero).  The engine
 keeps `--batch` node LPs in flight per GPU (nep_lp_submit / nep_lp_advance): a slot whose LP
 finishes takes the next node at once, as a B&B with an open-node queue does.  One *step* =
-`--batch` completed node LPs.  A node counts as an LP relaxation only if the engine certifies it:
-primal objective - Lagrangian bound <= tol*max(1,|bound|) and every row residual <= tol
-(DESIGN.md §4); nodes that stop at `--max-iters` are reported, not counted.  The root LP is solved
-before the timed region; the instance tensors live on the device before the timer starts; node
-bounds are uploaded inside the step, as the B&B host does per node.
+`--batch` node LPs; the timed region streams `--steps` x `--batch` nodes through the slots and
+drains them, so every node of the timed region finishes inside it (the hard ones included: no node
+is left iterating outside the clock).  A node counts as an LP relaxation only if the engine
+certifies it: primal objective - Lagrangian bound <= tol*max(1,|bound|) and every row residual <=
+tol; nodes that stop at the node-LP iteration limit `--max-iters` keep a valid
+Lagrangian bound (usable for pruning) and are reported, not counted.  The root LP is solved before
+the timed region; the instance tensors live on the device before the timer starts; node bounds are
+uploaded inside the timed region, as the B&B host does per node.
 
 Multi-GPU (`torch.distributed.run`, one rank per GPU): every rank holds the same instance and
 solves its own node stream (subtree sharding); the only exchange is the B&B
@@ -49,17 +52,22 @@ HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md "HBM")
 def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=8)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--nodes", type=int, default=512)
     ap.add_argument("--functions", type=int, default=256)
-    ap.add_argument("--batch", type=int, default=16, help="node LPs in flight per GPU (= completed LPs per step)")
+    ap.add_argument("--batch", type=int, default=32, help="node LPs in flight per GPU (= node LPs per step)")
     ap.add_argument("--fix", type=int, default=2, help="c[f,j] fixings per node LP")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--tol", type=float, default=1e-6)
-    ap.add_argument("--max-iters", type=int, default=100000, help="per node LP")
+    ap.add_argument("--max-iters", type=int, default=4096,
+                    help="per node LP (a B&B node-LP iteration limit; nodes that reach it keep a valid "
+                         "Lagrangian bound but are not counted as LP relaxations)")
+    ap.add_argument("--warm-omega-floor", type=float, default=0.0,
+                    help="warm-start primal-weight floor x the parent's (0: engine default)")
     ap.add_argument("--root-max-iters", type=int, default=400000)
-    ap.add_argument("--check-every", type=int, default=64)
+    ap.add_argument("--check-every", type=int, default=32, help="PDHG iterations per certificate check (node LPs)")
+    ap.add_argument("--root-check-every", type=int, default=64)
     ap.add_argument("--cold", action="store_true", help="cold-start every node LP")
     ap.add_argument("--cpu-budget", type=float, default=25.0, help="seconds for the CPU baseline (0 = skip)")
     ap.add_argument("--traffic", default=os.path.join(REPO, "profiles", "traffic.json"))
@@ -143,7 +151,7 @@ def cpu_baseline(N, F, seed, fix, budget):
 
 class NodeStream:
     """B&B child LPs of the root, `batch` of them in flight on the engine (nep_lp_submit/advance):
-    a slot whose LP finishes takes the next node at once."""
+    a slot whose LP finishes takes the next node at once, as a B&B with an open-node queue does."""
 
     def __init__(self, m, root, a, rank):
         self.m, self.root, self.a, self.rank = m, root, a, rank
@@ -151,28 +159,29 @@ class NodeStream:
         self.done = []          # (status, obj, primal_obj, iters) per completed node
 
     def _start(self, slot):
+        """Submit the next node into `slot`; False once `limit` nodes were submitted."""
         from core.engine.lp import LP_INFEASIBLE
         a = self.a
-        while True:
+        while self.counter < self.limit:
             seed = (a.seed * 1000003 + self.rank) * 7919 + self.counter
             self.counter += 1
             lb, ub = node_bounds(self.m.n_int, a.functions, a.nodes, 1, a.fix, seed)
             if not a.cold:
                 self.m.copy_state(self.root, slot)
             st = self.m.submit([slot], lb, ub, tol=a.tol, max_iters=a.max_iters, check_every=a.check_every,
-                               warm_start=not a.cold)
+                               warm_start=not a.cold, warm_omega_floor=a.warm_omega_floor)
             if int(st[0]) != LP_INFEASIBLE:
-                return
+                return True
             self.done.append((LP_INFEASIBLE, float("inf"), float("nan"), 0))
+        return False
 
-    def fill(self):
+    def drain(self, n):
+        """Stream the next n nodes through the `batch` slots until every one of them finished."""
+        self.limit = self.counter + n
         for s in range(self.a.batch):
-            self._start(s)
-
-    def run(self, n):
-        """Advance until n more node LPs completed; finished slots are refilled immediately."""
-        target = len(self.done) + n
-        while len(self.done) < target:
+            if not self._start(s):
+                break
+        while self.m.active() > 0:
             r = self.m.advance(1)
             for i, s in enumerate(r["slots"]):
                 self.done.append((int(r["status"][i]), float(r["obj"][i]), float(r["primal_obj"][i]),
@@ -210,7 +219,7 @@ def main():
         f"built in {time.perf_counter() - t_build:.1f}s")
     P = m.info.x_entries
     t_root = time.perf_counter()
-    rr = m.solve([root], tol=a.tol, max_iters=a.root_max_iters, check_every=a.check_every)
+    rr = m.solve([root], tol=a.tol, max_iters=a.root_max_iters, check_every=a.root_check_every)
     root_obj, root_status, root_iters = float(rr["obj"][0]), int(rr["status"][0]), int(rr["iters"][0])
     log(f"rank {rank}: root LP status {root_status} obj {root_obj:.10g} after {root_iters} iterations "
         f"({time.perf_counter() - t_root:.2f}s)")
@@ -218,27 +227,28 @@ def main():
         raise RuntimeError(f"root LP not certified: status {root_status} after {root_iters} iterations")
 
     stream = NodeStream(m, root, a, rank)
-    stream.fill()
 
-    def step():
-        stream.run(B)
+    def bound_exchange():
         ok = [o for st, o, _, _ in stream.done if st == LP_OPTIMAL]
         best = torch.tensor([min(ok) if ok else float("inf")], dtype=torch.float64, device=dev)
         if dist:
             td.all_reduce(best, op=td.ReduceOp.MIN)     # B&B bound exchange (8 B)
 
-    for s in range(a.warmup):
-        step()
-        log(f"rank {rank}: warmup step {s}: {len(stream.done)} node LPs completed")
+    if a.warmup > 0:
+        stream.drain(a.warmup * B)
+        bound_exchange()
+        log(f"rank {rank}: warmup: {len(stream.done)} node LPs completed")
     m.reset_stats()
     i0 = len(stream.done)
     if dist:
         td.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for s in range(a.steps):
-        step()
-        log(f"rank {rank}: step {s}: {len(stream.done) - i0} node LPs completed, {time.perf_counter() - t0:.2f}s")
+    # the timed K steps: K*B nodes streamed through the B slots and drained (every node finished,
+    # hard ones included — no node is left iterating outside the timed region)
+    stream.drain(a.steps * B)
+    bound_exchange()
+    log(f"rank {rank}: {len(stream.done) - i0} node LPs completed in {time.perf_counter() - t0:.2f}s")
     torch.cuda.synchronize()
     if dist:
         td.barrier()
@@ -249,6 +259,8 @@ def main():
     n_it = sum(r[3] for r in res)
     gmax = max([abs(p - o) / max(1.0, abs(o)) for s_, o, p, _ in res if s_ == LP_OPTIMAL] or [0.0])
     n_done = len(res)
+    util = n_it / max(1, st["lp_iterations"])           # this rank's LP iterations / slot-iterations run
+    iq = [int(v) for v in np.percentile([r[3] for r in res], [50, 90, 100])] if res else [0, 0, 0]
 
     tot = torch.tensor([wall, n_ok, n_it, gmax, n_done], dtype=torch.float64, device=dev)
     if dist:
@@ -298,7 +310,9 @@ def main():
                           "note": "(primal obj - Lagrangian bound)/max(1,|bound|) per certified LP; "
                                   "HiGHS parity on the reference's own models: tests/test_gpu_lp.py"},
         "lp": {"certified": n_ok, "completed": n_done, "iterations": n_it,
-               "mean_iters": n_it / max(1, n_done), "root_obj": root_obj, "root_iters": root_iters},
+               "mean_iters": n_it / max(1, n_done), "iters_p50_p90_max": iq,
+               "slot_utilisation_rank0": util,
+               "root_obj": root_obj, "root_iters": root_iters},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": "x_pass", "algorithmic_bytes_per_launch": per_lp * lps_per_launch,

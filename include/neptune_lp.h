@@ -79,6 +79,8 @@ typedef struct {
   int64_t max_iters;           /* default 200000 */
   int32_t check_every;         /* PDHG iterations between certificate checks (default 64) */
   int32_t warm_start;          /* 1: continue from the slot's current state (after nep_lp_copy_state) */
+  double warm_omega_floor;     /* warm starts: the primal weight stays >= this x the parent's
+                                  (0: default 2; < 0: no floor) */
 } nep_lp_opts;
 
 typedef struct {

@@ -644,12 +644,14 @@ nep_lp_opts resolve_opts(const nep_lp_opts *opts) {
   o.max_iters = 200000;
   o.check_every = 64;
   o.warm_start = 0;
+  o.warm_omega_floor = 2.0;
   if (opts) {
     if (opts->tol > 0) o.tol = opts->tol;
     o.cutoff = opts->cutoff;
     if (opts->max_iters > 0) o.max_iters = opts->max_iters;
     if (opts->check_every > 0) o.check_every = opts->check_every;
     o.warm_start = opts->warm_start;
+    if (opts->warm_omega_floor != 0) o.warm_omega_floor = opts->warm_omega_floor < 0 ? 0.0 : opts->warm_omega_floor;
   }
   return o;
 }
@@ -671,6 +673,7 @@ int submit(Model &m, int n, const int32_t *slots, const double *lbi, const doubl
   m.run = o;
   DeviceView &v = m.v;
   v.tol = o.tol;
+  v.warm_omega_floor = o.warm_omega_floor;
   v.cutoff = o.cutoff;
   v.max_iters = o.max_iters;
   const int ni = m.il.n_int;

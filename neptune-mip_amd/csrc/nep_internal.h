@@ -92,6 +92,7 @@ struct DeviceView {
   int64_t sx, smask, sint, sdual, skty, stpart, sbpart, snpart;   // per-slot strides (elements)
   // check/solve parameters
   double tol, cutoff;
+  double warm_omega_floor;               // warm starts: primal weight kept >= this x the parent's (0: off)
   int64_t max_iters;
 };
 

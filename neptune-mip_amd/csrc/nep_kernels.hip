@@ -759,6 +759,12 @@ __global__ void init_slot(DeviceView v, const int32_t *__restrict__ slots, int w
     ctrl->eta = eta;
     ctrl->omega_lo = omega0 * 1e-5;
     ctrl->omega_hi = omega0 * 1e5;
+    // A warm-started child keeps its parent's primal weight as a floor (times warm_omega_floor):
+    // the PDLP update right after a warm start sees the large primal move of re-routing the fixed
+    // placements and would shrink omega by orders of magnitude, which stalls the dual (measured on
+    // the 512x256 bench children: 81/96 certified within 20k iterations without a floor, 95/96 with
+    // floor 2, 62k iterations in all instead of 304k; tools/floor_probe.py).
+    if (warm && v.warm_omega_floor > 0) ctrl->omega_lo = fmin(ctrl->omega * v.warm_omega_floor, ctrl->omega_hi);
     ctrl->tau = eta / ctrl->omega;
     ctrl->sigma = eta * ctrl->omega;
     ctrl->status = 1;
