@@ -158,35 +158,44 @@ class NodeStream:
         self.counter = 0
         self.done = []          # (status, obj, primal_obj, iters) per completed node
 
-    def _start(self, slot):
-        """Submit the next node into `slot`; False once `limit` nodes were submitted."""
+    def _refill(self, slots):
+        """Submit the next nodes into the free `slots` (one nep_lp_submit call); stops once `limit`
+        nodes were submitted.  Nodes presolve proves infeasible complete at once and their slot
+        takes the next node."""
+        import numpy as np
         from core.engine.lp import LP_INFEASIBLE
         a = self.a
-        while self.counter < self.limit:
-            seed = (a.seed * 1000003 + self.rank) * 7919 + self.counter
-            self.counter += 1
-            lb, ub = node_bounds(self.m.n_int, a.functions, a.nodes, 1, a.fix, seed)
-            if not a.cold:
-                self.m.copy_state(self.root, slot)
-            st = self.m.submit([slot], lb, ub, tol=a.tol, max_iters=a.max_iters, check_every=a.check_every,
-                               warm_start=not a.cold, warm_omega_floor=a.warm_omega_floor)
-            if int(st[0]) != LP_INFEASIBLE:
-                return True
-            self.done.append((LP_INFEASIBLE, float("inf"), float("nan"), 0))
-        return False
+        free = list(slots)
+        while free and self.counter < self.limit:
+            take = free[: self.limit - self.counter]
+            lbs, ubs = [], []
+            for slot in take:
+                seed = (a.seed * 1000003 + self.rank) * 7919 + self.counter
+                self.counter += 1
+                lb, ub = node_bounds(self.m.n_int, a.functions, a.nodes, 1, a.fix, seed)
+                lbs.append(lb[0])
+                ubs.append(ub[0])
+                if not a.cold:
+                    self.m.copy_state(self.root, slot)
+            st = self.m.submit(take, np.array(lbs), np.array(ubs), tol=a.tol, max_iters=a.max_iters,
+                               check_every=a.check_every, warm_start=not a.cold,
+                               warm_omega_floor=a.warm_omega_floor)
+            free = free[len(take):]
+            for slot, code in zip(take, st):
+                if int(code) == LP_INFEASIBLE:
+                    self.done.append((LP_INFEASIBLE, float("inf"), float("nan"), 0))
+                    free.append(slot)
 
     def drain(self, n):
         """Stream the next n nodes through the `batch` slots until every one of them finished."""
         self.limit = self.counter + n
-        for s in range(self.a.batch):
-            if not self._start(s):
-                break
+        self._refill(range(self.a.batch))
         while self.m.active() > 0:
             r = self.m.advance(1)
-            for i, s in enumerate(r["slots"]):
+            for i in range(len(r["slots"])):
                 self.done.append((int(r["status"][i]), float(r["obj"][i]), float(r["primal_obj"][i]),
                                   int(r["iters"][i])))
-                self._start(int(s))
+            self._refill(r["slots"].tolist())
 
 
 def main():

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define NEP_API_VERSION 2
+#define NEP_API_VERSION 3
 
 /* variants: neptune.py:41-66 (NeptuneMinDelay / MinUtilization / MinDelayAndUtilization) */
 enum { NEP_MIN_DELAY = 0, NEP_MIN_UTILIZATION = 1, NEP_MIN_DELAY_AND_UTILIZATION = 2 };
@@ -148,6 +148,11 @@ int nep_debug_state(void *model, int32_t slot, double *y, double *kz, float *kty
  * n_dual}.  Lets the CPU test-suite check the model build without a GPU. */
 int nep_debug_build(const nep_model_desc *desc, double *eta, double *rho, double *gam, double *rownorm,
                     int32_t *dims);
+/* host-only node presolve of n nodes (lb_int/ub_int as for nep_lp_submit), evaluated twice: from
+ * scratch and as the sparse change of the model's base box that nep_lp_submit uses.  ok_* [n]:
+ * 1 = feasible; box_* [n][2][n_int] (may be NULL): the resulting node bounds (lb then ub). */
+int nep_debug_presolve(const nep_model_desc *desc, int32_t n, const double *lb_int, const double *ub_int,
+                       int32_t *ok_full, int32_t *ok_node, double *box_full, double *box_node);
 void nep_reset_stats(void *model);
 
 const char *nep_last_error(void);

@@ -18,7 +18,7 @@ STEP1, STEP2_DELETE, STEP2_CREATE = 1, 2, 3
 LP_OPTIMAL, LP_ITERATION_LIMIT, LP_INFEASIBLE, LP_CUTOFF, LP_NUMERICAL = 0, 1, 2, 3, 4
 VARIANTS = {"MinDelay": MIN_DELAY, "MinUtilization": MIN_UTILIZATION,
             "MinDelayAndUtilization": MIN_DELAY_AND_UTILIZATION}
-API_VERSION = 2
+API_VERSION = 3
 
 _dp = ctypes.POINTER(ctypes.c_double)
 
@@ -59,7 +59,8 @@ class Stats(ctypes.Structure):
 EXPORTS = ("nep_model_create", "nep_model_destroy", "nep_model_get_info", "nep_lp_solve_batch",
            "nep_lp_submit", "nep_lp_advance", "nep_lp_active",
            "nep_lp_get_solution", "nep_lp_get_rows", "nep_lp_copy_state", "nep_get_stats", "nep_reset_stats",
-           "nep_last_error", "nep_api_version", "nep_lp_get_diag", "nep_debug_build", "nep_debug_state")
+           "nep_last_error", "nep_api_version", "nep_lp_get_diag", "nep_debug_build", "nep_debug_state",
+           "nep_debug_presolve")
 
 _lib = None
 
@@ -94,6 +95,7 @@ def load_library(path=None):
     lib.nep_lp_get_diag.argtypes = [vp, i32, _dp]
     lib.nep_debug_build.argtypes = [ctypes.POINTER(ModelDesc), _dp, _dp, _dp, _dp, ctypes.POINTER(i32)]
     lib.nep_debug_state.argtypes = [vp, i32, _dp, _dp, ctypes.POINTER(ctypes.c_float), _dp, _dp]
+    lib.nep_debug_presolve.argtypes = [ctypes.POINTER(ModelDesc), i32, _dp, _dp, pi32, pi32, _dp, _dp]
     lib.nep_last_error.restype = ctypes.c_char_p
     lib.nep_api_version.restype = ctypes.c_int
     if lib.nep_api_version() != API_VERSION:
@@ -150,6 +152,27 @@ def debug_build(data, variant, step=STEP1, alpha=0.5, soften_step1_sol=1.3, max_
            "nep_debug_build")
     return {"eta": float(eta[0]), "rho": rho, "gam": gam, "rownorm": rn, "R": R, "T": T, "n_int": n_int,
             "n_dual": n_dual}
+
+
+def debug_presolve(data, variant, lb, ub, step=STEP1, alpha=0.5, soften_step1_sol=1.3, max_score=0.0,
+                   prev_network_delay=0.0):
+    """Host-only node presolve of [n, n_int] node bounds, from scratch and as the sparse change of
+    the base box nep_lp_submit uses: returns (ok_full, ok_node, box_full, box_node)."""
+    lib = load_library()
+    N, F = len(data.nodes), len(data.functions)
+    v = VARIANTS[variant] if isinstance(variant, str) else int(variant)
+    k = _arrays(data, N, F)
+    d = _desc(k, N, F, v, int(step), alpha, soften_step1_sol, max_score, prev_network_delay, data.node_budget)
+    lb = np.ascontiguousarray(lb, np.float64)
+    ub = np.ascontiguousarray(ub, np.float64)
+    n, ni = lb.shape
+    okf = np.zeros(n, np.int32)
+    okn = np.zeros(n, np.int32)
+    bf = np.zeros((n, 2, ni))
+    bn = np.zeros((n, 2, ni))
+    _check(lib, lib.nep_debug_presolve(ctypes.byref(d), n, _ptr(lb), _ptr(ub), _ptr(okf, ctypes.c_int32),
+                                       _ptr(okn, ctypes.c_int32), _ptr(bf), _ptr(bn)), "nep_debug_presolve")
+    return okf.astype(bool), okn.astype(bool), bf, bn
 
 
 class LPModel:

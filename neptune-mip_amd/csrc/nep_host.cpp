@@ -26,6 +26,9 @@ hipError_t launch_node_pass(const DeviceView &v, const int32_t *slots, int nslot
                             bool plain, int it, hipStream_t s);
 hipError_t launch_scalar_pass(const DeviceView &v, const int32_t *slots, int nslots, bool check, bool init,
                               bool first, bool plain, int it, int block_len, hipStream_t s);
+hipError_t launch_node_bounds(const DeviceView &v, const int32_t *slots, int nslots, const double *base_lb,
+                              const double *base_ub, const uint8_t *base_mask, const int32_t *off, const int32_t *idx,
+                              const double *cl, const double *cu, int max_chg, hipStream_t s);
 hipError_t launch_init_slot(const DeviceView &v, const int32_t *slots, int nslots, bool warm, double eta,
                             double omega0, hipStream_t s);
 }  // namespace nep
@@ -76,6 +79,15 @@ struct Model {
   std::vector<int> Kr, Kc;
   std::vector<double> Kv, ftot;
   bool x_coef_nonneg = true;   // every x coefficient outside C1/C2 is >= 0 (W, cpr, D >= 0)
+  // node presolve as a sparse change of the base box (presolve_setup / presolve_node)
+  bool base_ok = false;
+  std::vector<double> base_lb, base_ub, base_amin, base_amax;
+  std::vector<uint8_t> base_mask;
+  std::vector<int> base_cnt, Kcp, Kcr;
+  std::vector<double> Kcv;
+  std::vector<int> pos, fdelta, touched, ftouched;   // scratch, reset after every node
+  std::vector<double> dmin, dmax;
+  std::vector<uint8_t> rowmark;
   double eta = 0, sigma_max = 0, omega0 = 1.0;
   // device
   hipStream_t stream = nullptr;
@@ -84,6 +96,10 @@ struct Model {
   std::vector<void *> allocs;
   int32_t *d_slots = nullptr;   // the slots currently iterating (mirror of `act`)
   int32_t *d_new = nullptr;     // slots being initialised by nep_lp_submit
+  double *d_base_lb = nullptr, *d_base_ub = nullptr;
+  uint8_t *d_base_mask = nullptr;
+  int32_t *d_chg_off = nullptr, *d_chg_idx = nullptr;   // packed bound changes of the nodes being submitted
+  double *d_chg_lb = nullptr, *d_chg_ub = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   nep_stats stats{};
   // streaming state
@@ -565,6 +581,20 @@ int setup_dense(Model &m, const nep_model_desc &d) {
   if ((rc = dalloc(m, &v.ctrl, (size_t)B))) return rc;
   if ((rc = dalloc(m, &m.d_slots, (size_t)B))) return rc;
   if ((rc = dalloc(m, &m.d_new, (size_t)B))) return rc;
+  {
+    const double *p = nullptr;
+    if ((rc = upload(m, &p, m.base_lb))) return rc;
+    m.d_base_lb = const_cast<double *>(p);
+    if ((rc = upload(m, &p, m.base_ub))) return rc;
+    m.d_base_ub = const_cast<double *>(p);
+    const uint8_t *q = nullptr;
+    if ((rc = upload(m, &q, m.base_mask))) return rc;
+    m.d_base_mask = const_cast<uint8_t *>(q);
+  }
+  if ((rc = dalloc(m, &m.d_chg_off, (size_t)B + 1))) return rc;
+  if ((rc = dalloc(m, &m.d_chg_idx, (size_t)B * v.sint))) return rc;
+  if ((rc = dalloc(m, &m.d_chg_lb, (size_t)B * v.sint))) return rc;
+  if ((rc = dalloc(m, &m.d_chg_ub, (size_t)B * v.sint))) return rc;
   HIPCHK(hipMemsetAsync(v.ctrl, 0, sizeof(Ctrl) * B, m.stream));
   HIPCHK(hipMemsetAsync(v.x, 0, sizeof(float) * B * v.sx, m.stream));
   HIPCHK(hipMemsetAsync(v.xa, 0, sizeof(float) * B * v.sx, m.stream));
@@ -574,10 +604,54 @@ int setup_dense(Model &m, const nep_model_desc &d) {
   return NEP_OK;
 }
 
-// per-node presolve: bounds, the C8 cap, n_ub = 0 => c_ub[:, j] = 0, destination masks.
-// Returns false if the node is infeasible.
-bool presolve(const Model &m, const double *lbi, const double *ubi, std::vector<double> &lb, std::vector<double> &ub,
-              std::vector<uint8_t> &mask) {
+// Node presolve: bounds, the C8 cap, n_ub = 0 => c_ub[:, j] = 0, destination masks, and a
+// row-activity test over the node's box: the activity range of each dualised row, from the small
+// variables' bounds and the x part's range (flow into (f, j) is in [0, ftot_f] when j is allowed for
+// f, else 0; the CPU and score rows have non-negative x coefficients).  A row whose range misses
+// [lo, hi] proves the node LP infeasible — e.g. step-2 delete mode with more fixed placements than
+// the old allocation (constraints_step2.py:36-44), memory over-committed by fixed placements
+// (constraints_step1.py:18-23), an open node with every placement closed (:69-78).
+//
+// presolve_full() evaluates all of it from scratch; it runs once per model on the natural bounds
+// (the "base" box).  presolve_node() evaluates a node as a sparse change of that base: node bounds
+// only tighten the base box, so a base-infeasible model makes every node infeasible, rows no
+// changed variable touches keep their (feasible) base range, and the rows a change touches are
+// re-tested from base range + delta (CSC of the non-x part of K).  Cost per node: one O(n_int) scan
+// of the caller's bounds + O(changes x column length), instead of O(n_int + nnz(K) + F*N).
+static void activity_ranges(const Model &m, const std::vector<double> &lb, const std::vector<double> &ub,
+                            const std::vector<uint8_t> &mask, std::vector<double> &amin, std::vector<double> &amax) {
+  const int N = m.N, F = m.F, NP = m.NP, o = m.dl.n_dual;
+  amin.assign(o, 0.0);
+  amax.assign(o, 0.0);
+  for (int f = 0; f < F; ++f)
+    for (int j = 0; j < N; ++j) {
+      const double fx = mask[(size_t)f * NP + j] ? m.ftot[f] : 0.0;
+      amax[m.dl.o1 + f * N + j] += fx;
+      amax[m.dl.o2 + f * N + j] += fx;
+    }
+  for (int j = 0; j < N; ++j) {
+    amax[m.dl.o5 + j] = INF;
+    if (!m.x_coef_nonneg) amin[m.dl.o5 + j] = -INF;
+  }
+  if (m.step2) {
+    amax[m.dl.oS] = INF;
+    if (!m.x_coef_nonneg) amin[m.dl.oS] = -INF;
+  }
+  for (size_t e = 0; e < m.Kv.size(); ++e) {
+    const double a = m.Kv[e] * lb[m.Kc[e]], b = m.Kv[e] * ub[m.Kc[e]];
+    amin[m.Kr[e]] += std::min(a, b);
+    amax[m.Kr[e]] += std::max(a, b);
+  }
+}
+
+static inline bool row_range_ok(const Model &m, int k, double amin, double amax) {
+  if (amin > m.hi[k] + 1e-9 * std::max(1.0, std::fabs(m.hi[k]))) return false;
+  if (amax < m.lo[k] - 1e-9 * std::max(1.0, std::fabs(m.lo[k]))) return false;
+  return true;
+}
+
+bool presolve_full(const Model &m, const double *lbi, const double *ubi, std::vector<double> &lb,
+                   std::vector<double> &ub, std::vector<uint8_t> &mask) {
   const int n = m.il.n_int, N = m.N, F = m.F, NP = m.NP;
   lb = m.nat_lb;
   ub = m.nat_ub;
@@ -603,38 +677,124 @@ bool presolve(const Model &m, const double *lbi, const double *ubi, std::vector<
     if (cnt == 0) ok = false;   // every routing row of f would be empty (C4 infeasible)
   }
   if (!ok) return false;
-  // row-activity test over the node's box: the activity range of each dualised row, from the
-  // small variables' bounds and the x part's range (flow into (f, j) is in [0, N] when j is
-  // allowed for f, else 0; the CPU and score rows have non-negative x coefficients).  A row whose
-  // range misses [lo, hi] proves the node LP infeasible — e.g. step-2 delete mode with more fixed
-  // placements than the old allocation (constraints_step2.py:36-44), memory over-committed by
-  // fixed placements (constraints_step1.py:18-23), an open node with every placement closed (:69-78).
-  const int o = m.dl.n_dual;
-  std::vector<double> amin(o, 0.0), amax(o, 0.0);
-  for (int f = 0; f < F; ++f)
-    for (int j = 0; j < N; ++j) {
-      const double fx = mask[(size_t)f * NP + j] ? m.ftot[f] : 0.0;
-      amax[m.dl.o1 + f * N + j] += fx;
-      amax[m.dl.o2 + f * N + j] += fx;
-    }
-  for (int j = 0; j < N; ++j) {
-    amax[m.dl.o5 + j] = INF;
-    if (!m.x_coef_nonneg) amin[m.dl.o5 + j] = -INF;
-  }
-  if (m.step2) {
-    amax[m.dl.oS] = INF;
-    if (!m.x_coef_nonneg) amin[m.dl.oS] = -INF;
-  }
-  for (size_t e = 0; e < m.Kv.size(); ++e) {
-    const double a = m.Kv[e] * lb[m.Kc[e]], b = m.Kv[e] * ub[m.Kc[e]];
-    amin[m.Kr[e]] += std::min(a, b);
-    amax[m.Kr[e]] += std::max(a, b);
-  }
-  for (int k = 0; k < o; ++k) {
-    if (amin[k] > m.hi[k] + 1e-9 * std::max(1.0, std::fabs(m.hi[k]))) return false;
-    if (amax[k] < m.lo[k] - 1e-9 * std::max(1.0, std::fabs(m.lo[k]))) return false;
-  }
+  std::vector<double> amin, amax;
+  activity_ranges(m, lb, ub, mask, amin, amax);
+  for (int k = 0; k < m.dl.n_dual; ++k)
+    if (!row_range_ok(m, k, amin[k], amax[k])) return false;
   return true;
+}
+
+// once per model: the base box (natural bounds) and what presolve_node() needs
+void presolve_setup(Model &m) {
+  const int n = m.il.n_int, F = m.F, NP = m.NP;
+  m.base_ok = presolve_full(m, nullptr, nullptr, m.base_lb, m.base_ub, m.base_mask);
+  activity_ranges(m, m.base_lb, m.base_ub, m.base_mask, m.base_amin, m.base_amax);
+  m.base_cnt.assign(F, 0);
+  for (int f = 0; f < F; ++f)
+    for (int j = 0; j < m.N; ++j) m.base_cnt[f] += m.base_mask[(size_t)f * NP + j];
+  m.Kcp.assign(n + 1, 0);
+  for (int c : m.Kc) m.Kcp[c + 1]++;
+  for (int k = 0; k < n; ++k) m.Kcp[k + 1] += m.Kcp[k];
+  m.Kcr.resize(m.Kc.size());
+  m.Kcv.resize(m.Kc.size());
+  std::vector<int> fill(m.Kcp.begin(), m.Kcp.end() - 1);
+  for (size_t e = 0; e < m.Kc.size(); ++e) {
+    const int at = fill[m.Kc[e]]++;
+    m.Kcr[at] = m.Kr[e];
+    m.Kcv[at] = m.Kv[e];
+  }
+  m.pos.assign(n, -1);
+  m.dmin.assign(m.dl.n_dual, 0.0);
+  m.dmax.assign(m.dl.n_dual, 0.0);
+  m.rowmark.assign(m.dl.n_dual, 0);
+  m.fdelta.assign(F, 0);
+}
+
+// One node as changes (index, lb, ub) of the base box, appended to ci/cl/cu.  Returns false (and
+// appends nothing) if the node is infeasible.
+bool presolve_node(Model &m, const double *lbi, const double *ubi, std::vector<int32_t> &ci,
+                   std::vector<double> &cl, std::vector<double> &cu) {
+  const int n = m.il.n_int, N = m.N, F = m.F, NP = m.NP, oc = m.il.oc;
+  if (!m.base_ok) return false;
+  const size_t c0 = ci.size();
+  for (int k = 0; k < n; ++k) {
+    const double l = lbi ? std::max(m.base_lb[k], lbi[k]) : m.base_lb[k];
+    const double u = ubi ? std::min(m.base_ub[k], ubi[k]) : m.base_ub[k];
+    if (l != m.base_lb[k] || u != m.base_ub[k]) {
+      m.pos[k] = (int)(ci.size() - c0);
+      ci.push_back(k);
+      cl.push_back(l);
+      cu.push_back(u);
+    }
+  }
+  if (m.has_n) {
+    const size_t nc = ci.size();
+    for (size_t t = c0; t < nc; ++t) {
+      const int k = ci[t];
+      if (k < m.il.on || k >= m.il.on + N || cu[t] > 0.0) continue;
+      const int j = k - m.il.on;
+      for (int f = 0; f < F; ++f) {
+        const int kc = oc + f * N + j;
+        if (m.pos[kc] >= 0) {
+          double &u = cu[c0 + m.pos[kc]];
+          u = std::min(u, 0.0);
+        } else if (m.base_ub[kc] > 0.0) {
+          m.pos[kc] = (int)(ci.size() - c0);
+          ci.push_back(kc);
+          cl.push_back(m.base_lb[kc]);
+          cu.push_back(0.0);
+        }
+      }
+    }
+  }
+  bool ok = true;
+  std::vector<int> &touched = m.touched, &ftouched = m.ftouched;
+  touched.clear();
+  ftouched.clear();
+  auto touch = [&](int r) {
+    if (!m.rowmark[r]) { m.rowmark[r] = 1; touched.push_back(r); }
+  };
+  for (size_t t = c0; t < ci.size(); ++t) {
+    const int k = ci[t];
+    const double l = cl[t], u = cu[t], bl = m.base_lb[k], bu = m.base_ub[k];
+    if (l > u + 1e-12) ok = false;
+    if (k >= oc && k < oc + F * N) {
+      const int f = (k - oc) / N, j = (k - oc) % N;
+      const int now = u > 0.0, was = m.base_mask[(size_t)f * NP + j];
+      if (now != was) {
+        if (m.fdelta[f] == 0) ftouched.push_back(f);
+        m.fdelta[f] += now - was;
+        const double dfx = (now - was) * m.ftot[f];
+        for (int r : {m.dl.o1 + f * N + j, m.dl.o2 + f * N + j}) {
+          touch(r);
+          m.dmax[r] += dfx;
+        }
+      }
+    }
+    for (int e = m.Kcp[k]; e < m.Kcp[k + 1]; ++e) {
+      const int r = m.Kcr[e];
+      const double a = m.Kcv[e];
+      touch(r);
+      m.dmin[r] += std::min(a * l, a * u) - std::min(a * bl, a * bu);
+      m.dmax[r] += std::max(a * l, a * u) - std::max(a * bl, a * bu);
+    }
+  }
+  for (int f : ftouched) {
+    if (m.base_cnt[f] + m.fdelta[f] == 0) ok = false;   // every routing row of f empty
+    m.fdelta[f] = 0;
+  }
+  for (int r : touched) {
+    if (ok && !row_range_ok(m, r, m.base_amin[r] + m.dmin[r], m.base_amax[r] + m.dmax[r])) ok = false;
+    m.dmin[r] = m.dmax[r] = 0.0;
+    m.rowmark[r] = 0;
+  }
+  for (size_t t = c0; t < ci.size(); ++t) m.pos[ci[t]] = -1;
+  if (!ok) {
+    ci.resize(c0);
+    cl.resize(c0);
+    cu.resize(c0);
+  }
+  return ok;
 }
 
 nep_lp_opts resolve_opts(const nep_lp_opts *opts) {
@@ -676,26 +836,34 @@ int submit(Model &m, int n, const int32_t *slots, const double *lbi, const doubl
   v.warm_omega_floor = o.warm_omega_floor;
   v.cutoff = o.cutoff;
   v.max_iters = o.max_iters;
-  const int ni = m.il.n_int;
-  std::vector<int32_t> fresh;
-  std::vector<double> lb, ub;
-  std::vector<uint8_t> mask;
+  std::vector<int32_t> fresh, off(1, 0), ci;
+  std::vector<double> cl, cu;
+  const size_t ni = (size_t)m.il.n_int;
+  int max_chg = 0;
   for (int b = 0; b < n; ++b) {
     const int s = slots[b];
-    const bool ok = presolve(m, lbi ? lbi + (size_t)b * ni : nullptr, ubi ? ubi + (size_t)b * ni : nullptr, lb, ub, mask);
+    const size_t c0 = ci.size();
+    const bool ok = presolve_node(m, lbi ? lbi + (size_t)b * ni : nullptr, ubi ? ubi + (size_t)b * ni : nullptr, ci, cl, cu);
     status[b] = ok ? NEP_LP_ITERATION_LIMIT : NEP_LP_INFEASIBLE;
     if (!ok) continue;
-    HIPCHK(hipMemcpyAsync(v.lb + (size_t)s * v.sint, lb.data(), ni * sizeof(double), hipMemcpyHostToDevice, m.stream));
-    HIPCHK(hipMemcpyAsync(v.ub + (size_t)s * v.sint, ub.data(), ni * sizeof(double), hipMemcpyHostToDevice, m.stream));
-    HIPCHK(hipMemcpyAsync(v.mask + (size_t)s * v.smask, mask.data(), mask.size(), hipMemcpyHostToDevice, m.stream));
-    // the host vectors are reused for the next node: wait for the copies
-    HIPCHK(hipStreamSynchronize(m.stream));
     m.busy[s] = 1;
     fresh.push_back(s);
+    off.push_back((int32_t)ci.size());
+    max_chg = std::max(max_chg, (int)(ci.size() - c0));
   }
   if (fresh.empty()) return NEP_OK;
   const int nf = (int)fresh.size();
+  // the node boxes on the device: base box copy + the packed changes scattered over it (a few
+  // KB per node instead of the 2 x 8 x n_int bytes of bounds and the F x NP mask)
   HIPCHK(hipMemcpyAsync(m.d_new, fresh.data(), nf * sizeof(int32_t), hipMemcpyHostToDevice, m.stream));
+  HIPCHK(hipMemcpyAsync(m.d_chg_off, off.data(), off.size() * sizeof(int32_t), hipMemcpyHostToDevice, m.stream));
+  if (!ci.empty()) {
+    HIPCHK(hipMemcpyAsync(m.d_chg_idx, ci.data(), ci.size() * sizeof(int32_t), hipMemcpyHostToDevice, m.stream));
+    HIPCHK(hipMemcpyAsync(m.d_chg_lb, cl.data(), cl.size() * sizeof(double), hipMemcpyHostToDevice, m.stream));
+    HIPCHK(hipMemcpyAsync(m.d_chg_ub, cu.data(), cu.size() * sizeof(double), hipMemcpyHostToDevice, m.stream));
+  }
+  HIPCHK(launch_node_bounds(v, m.d_new, nf, m.d_base_lb, m.d_base_ub, m.d_base_mask, m.d_chg_off, m.d_chg_idx,
+                            m.d_chg_lb, m.d_chg_ub, max_chg, m.stream));
   HIPCHK(launch_init_slot(v, m.d_new, nf, o.warm_start != 0, m.eta, m.omega0, m.stream));
   HIPCHK(launch_x_pass(v, m.d_new, nf, false, true, true, true, 0, m.stream));
   HIPCHK(launch_node_pass(v, m.d_new, nf, false, true, true, true, 0, m.stream));
@@ -825,6 +993,7 @@ int nep_model_create(const nep_model_desc *desc, int32_t max_batch, void *hip_st
   if (max_batch <= 0) return fail(NEP_ERR_ARG, "max_batch must be positive");
   std::unique_ptr<Model> m(new Model());
   int rc = build(*m, *desc);
+  if (rc == NEP_OK) presolve_setup(*m);
   if (rc) return rc;
   rc = setup_device(*m, max_batch, hip_stream);
   if (rc) return rc;
@@ -990,3 +1159,39 @@ void nep_reset_stats(void *model) {
 }
 
 }  // extern "C"
+
+int nep_debug_presolve(const nep_model_desc *desc, int32_t n, const double *lbi, const double *ubi, int32_t *ok_full,
+                       int32_t *ok_node, double *box_full, double *box_node) {
+  if (!desc || n < 0 || !ok_full || !ok_node) return fail(NEP_ERR_ARG, "null argument");
+  Model m;
+  int rc = build(m, *desc);
+  if (rc) return rc;
+  presolve_setup(m);
+  const size_t ni = (size_t)m.il.n_int;
+  std::vector<double> lb, ub;
+  std::vector<uint8_t> mask;
+  std::vector<int32_t> ci;
+  std::vector<double> cl, cu;
+  for (int b = 0; b < n; ++b) {
+    const double *l = lbi ? lbi + b * ni : nullptr, *u = ubi ? ubi + b * ni : nullptr;
+    ok_full[b] = presolve_full(m, l, u, lb, ub, mask) ? 1 : 0;
+    if (box_full) {
+      std::memcpy(box_full + 2 * b * ni, lb.data(), ni * sizeof(double));
+      std::memcpy(box_full + (2 * b + 1) * ni, ub.data(), ni * sizeof(double));
+    }
+    ci.clear();
+    cl.clear();
+    cu.clear();
+    ok_node[b] = presolve_node(m, l, u, ci, cl, cu) ? 1 : 0;
+    if (box_node) {
+      double *bl = box_node + 2 * b * ni, *bu = box_node + (2 * b + 1) * ni;
+      std::memcpy(bl, m.base_lb.data(), ni * sizeof(double));
+      std::memcpy(bu, m.base_ub.data(), ni * sizeof(double));
+      for (size_t t = 0; t < ci.size(); ++t) {
+        bl[ci[t]] = cl[t];
+        bu[ci[t]] = cu[t];
+      }
+    }
+  }
+  return NEP_OK;
+}

@@ -22,6 +22,7 @@
 // constraints_step2.py:5-55, score rows :57-88.  Objectives objectives.py:4-63.
 #include <hip/hip_runtime.h>
 #include <cfloat>
+#include <algorithm>
 #include <cmath>
 
 #include "nep_internal.h"
@@ -775,6 +776,41 @@ __global__ void init_slot(DeviceView v, const int32_t *__restrict__ slots, int w
   }
 }
 
+// a node's box on the device: the model's base box (natural bounds, all allowed destinations) ...
+__global__ void node_bounds_base(DeviceView v, const int32_t *__restrict__ slots, const double *__restrict__ blb,
+                                 const double *__restrict__ bub, const uint8_t *__restrict__ bmask) {
+  const int slot = slots[blockIdx.y];
+  const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  double *lb = v.lb + slot * v.sint, *ub = v.ub + slot * v.sint;
+  for (int64_t i = tid; i < v.sint; i += stride) {
+    lb[i] = blb[i];
+    ub[i] = bub[i];
+  }
+  uint8_t *mask = v.mask + slot * v.smask;
+  for (int64_t i = tid; i < v.smask; i += stride) mask[i] = bmask[i];
+}
+// ... then the node's packed bound changes (presolve_node, nep_host.cpp), with the destination
+// masks of the changed c[f, j]
+__global__ void node_bounds_scatter(DeviceView v, const int32_t *__restrict__ slots, const int32_t *__restrict__ off,
+                                    const int32_t *__restrict__ idx, const double *__restrict__ cl,
+                                    const double *__restrict__ cu) {
+  const int b = blockIdx.y;
+  const int slot = slots[b];
+  double *lb = v.lb + slot * v.sint, *ub = v.ub + slot * v.sint;
+  uint8_t *mask = v.mask + slot * v.smask;
+  const int oc = v.il.oc, FN = v.F * v.N;
+  for (int t = off[b] + blockIdx.x * blockDim.x + threadIdx.x; t < off[b + 1]; t += gridDim.x * blockDim.x) {
+    const int k = idx[t];
+    lb[k] = cl[t];
+    ub[k] = cu[t];
+    if (k >= oc && k < oc + FN) {
+      const int f = (k - oc) / v.N, j = (k - oc) - f * v.N;
+      mask[(int64_t)f * v.NP + j] = cu[t] > 0.0 ? 1 : 0;
+    }
+  }
+}
+
 // ------------------------------------------------------------------------------------------
 // launchers
 // ------------------------------------------------------------------------------------------
@@ -821,6 +857,17 @@ hipError_t launch_scalar_pass(const DeviceView &v, const int32_t *slots, int nsl
     hipLaunchKernelGGL((scalar_pass<true, false>), grid, block, 0, s, v, slots, fi, pl, it, block_len);
   else
     hipLaunchKernelGGL((scalar_pass<false, false>), grid, block, 0, s, v, slots, fi, pl, it, block_len);
+  return hipGetLastError();
+}
+
+hipError_t launch_node_bounds(const DeviceView &v, const int32_t *slots, int nslots, const double *base_lb,
+                              const double *base_ub, const uint8_t *base_mask, const int32_t *off, const int32_t *idx,
+                              const double *cl, const double *cu, int max_chg, hipStream_t s) {
+  hipLaunchKernelGGL(node_bounds_base, dim3(128, nslots), dim3(256), 0, s, v, slots, base_lb, base_ub, base_mask);
+  if (max_chg > 0) {
+    const int gx = std::min(64, (max_chg + 255) / 256);
+    hipLaunchKernelGGL(node_bounds_scatter, dim3(gx, nslots), dim3(256), 0, s, v, slots, off, idx, cl, cu);
+  }
   return hipGetLastError();
 }
 

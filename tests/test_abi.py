@@ -58,3 +58,40 @@ def test_host_build_matches_mirror(name, k):
     np.testing.assert_allclose(got["rownorm"], ref.rownorm, rtol=1e-12)
     # power iteration from different random starts: same operator norm to a few 1e-3
     assert abs(got["eta"] / ref.eta - 1.0) < 5e-3
+
+
+@pytest.mark.parametrize("name,k", CASES)
+def test_node_presolve_incremental_equals_full(name, k):
+    """nep_lp_submit presolves a node as a sparse change of the model's base box (presolve_node);
+    it must decide feasibility and produce the node box exactly as the from-scratch presolve does."""
+    from core.engine.lp import debug_build, debug_presolve
+    data, variant, step, kw = build_args(name, k)
+    n_int = debug_build(data, variant, step=step, **kw)["n_int"]
+    N, F = len(data.nodes), len(data.functions)
+    rng = np.random.default_rng(k + 17)
+    nodes = 24
+    lb = np.full((nodes, n_int), -np.inf)
+    ub = np.full((nodes, n_int), np.inf)
+    for b in range(nodes):
+        kind = b % 4
+        if kind == 0:                      # a few 0/1 fixings anywhere (crossed bounds included)
+            idx = rng.choice(n_int, size=min(n_int, 3), replace=False)
+            val = rng.integers(0, 2, size=idx.size).astype(float)
+            lb[b, idx] = val
+            ub[b, idx] = val
+        elif kind == 1:                    # placements of one function closed but one
+            f = int(rng.integers(F))
+            ub[b, f * N:(f + 1) * N] = 0.0
+            ub[b, f * N + int(rng.integers(N))] = np.inf
+        elif kind == 2:                    # every placement of one function closed: infeasible (C4)
+            f = int(rng.integers(F))
+            ub[b, f * N:(f + 1) * N] = 0.0
+        else:                              # a node closed (n_j = 0 when the model has n) + a placement forced there
+            j = int(rng.integers(N))
+            ub[b, n_int - N + j] = 0.0
+            lb[b, int(rng.integers(F)) * N + j] = 1.0
+    ok_f, ok_n, box_f, box_n = debug_presolve(data, variant, lb, ub, step=step, **kw)
+    np.testing.assert_array_equal(ok_f, ok_n)
+    assert not ok_f[2::4].any()
+    for b in np.nonzero(ok_f)[0]:
+        np.testing.assert_array_equal(box_f[b], box_n[b])
