@@ -23,8 +23,6 @@
 namespace nep {
 
 constexpr int kWave = 64;
-constexpr int kTileWaves = 4;            // waves per x-pass workgroup
-constexpr int kTileThreads = kWave * kTileWaves;
 constexpr int kNodeWaves = 16;           // waves per node-pass workgroup (each sums F/16 functions)
 constexpr int kNodeThreads = kWave * kNodeWaves;
 

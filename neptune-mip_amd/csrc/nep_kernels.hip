@@ -199,23 +199,26 @@ __device__ __forceinline__ void load_row(const float *__restrict__ xrow, const f
 // ---------------------------------------------------------------------------------------------
 // x_pass: one workgroup = all routing rows of ONE function f of one LP slot, then the
 // per-(f, j) small variables of that f.
-//  1. rows: each wave owns whole rows (N destinations = CPL float4 chunks per lane, 1 KiB per
-//     wave-instruction; the next row's loads are issued before the current row is processed),
-//     projects each row on its simplex with Michelot's algorithm (DPP sums + ballot counts),
-//     writes x̄' and accumulates column sums (C1/C2) and W-weighted sums (C5);
-//  2. LDS reduction of the column sums across waves;
+//  1. rows: each of the TW waves owns whole rows (N destinations = CPL float4 chunks per lane,
+//     1 KiB per wave-instruction), projects each row on its simplex with Michelot's algorithm
+//     (DPP sums + ballot counts), writes x̄' and accumulates the column sums (C1/C2) and
+//     W-weighted sums (C5) into its own LDS row;
+//  2. LDS reduction of the column sums across waves (fixed wave order);
 //  3. per destination j: c[f,j] (+ moved_from/moved_to in step 2), the C1/C2 (D1/D2) duals,
 //     the packed dual y1+y2 the next iteration's rows read, and f's share of the node rows
 //     (memory, Σ_f c, CPU) for node_pass;
 //  4. (init / certificate / step-2 iterations) the workgroup's scalar partials.
 // ---------------------------------------------------------------------------------------------
-template <int CPL, bool CHECK, bool INIT>
-__global__ __launch_bounds__(kTileThreads) void x_pass(DeviceView v, const int32_t *__restrict__ slots, int first,
-                                                       int plain, int it) {
+template <int CPL, bool CHECK, bool INIT, int TW>
+// Occupancy: the plain iterations are held to <= 85 VGPRs (6 waves per SIMD, no spills at TW 4/8);
+// measured at 512x256 / ~14 LPs per launch: 0.382 ms per launch vs 0.402 at the compiler's own 86
+// VGPRs (5 waves) and 0.428 when forced to 8 waves (64 VGPRs + 68 B/lane of spills).  The
+// certificate iterations (fp64 Lagrangian terms, 143 VGPRs) run at 3 waves per SIMD.
+__global__ __launch_bounds__(kWave * TW) __attribute__((amdgpu_waves_per_eu(CHECK ? 2 : (TW == 16 ? 4 : 6), 8))) void x_pass(DeviceView v, const int32_t *__restrict__ slots, int first,
+                                                     int plain, int it) {
   constexpr int E = 4 * CPL;
-  constexpr bool PF = CPL <= 2;   // software prefetch of the next row (register budget)
-  extern __shared__ __attribute__((aligned(16))) float lds[];   // [2][kTileWaves][NP]
-  __shared__ double lds_s[kTileWaves][NTS + NBS];
+  extern __shared__ __attribute__((aligned(16))) float lds[];   // [2][TW][NP] accumulators + [2][NP] constants
+  __shared__ double lds_s[TW][NTS + NBS];
   const int f = blockIdx.x;
   const int slot = slots[blockIdx.y];
   Ctrl *ctrl = v.ctrl + slot;
@@ -236,54 +239,57 @@ __global__ __launch_bounds__(kTileThreads) void x_pass(DeviceView v, const int32
   float *__restrict__ kty = v.kty + slot * v.skty;
   const float ys = kty[(int64_t)F * NP + NP];
 
-  float kx[E], cy5[E];
+  // Per-function column constants (packed duals kx = y1 + y2 and cy5 = cpr * y5) and the per-wave
+  // column accumulators (C1/C2 column sums, C5 W-weighted sums) live in LDS, not in registers:
+  // 32 fewer VGPRs per lane at CPL = 2, i.e. more waves per SIMD to keep HBM reads in flight.
+  float *lS = lds, *lW = lds + TW * NP, *lK = lds + 2 * TW * NP, *lC = lK + NP;
+  for (int j = threadIdx.x; j < NP; j += kWave * TW) {
+    lK[j] = kty[(int64_t)f * NP + j];
+    lC[j] = v.cpr[(int64_t)f * NP + j] * kty[(int64_t)F * NP + j];
+  }
   uint32_t mbits = 0;
 #pragma unroll
   for (int q = 0; q < CPL; ++q) {
     const int j0 = 4 * (lane + kWave * q);
     if (j0 < NP) {
-      const float4 a = ld4(kty + (int64_t)f * NP + j0);
-      const float4 b = ld4(kty + (int64_t)F * NP + j0);
-      const float4 c = ld4(v.cpr + (int64_t)f * NP + j0);
       const uchar4 m = *reinterpret_cast<const uchar4 *>(mask + j0);
-      kx[4 * q] = a.x; kx[4 * q + 1] = a.y; kx[4 * q + 2] = a.z; kx[4 * q + 3] = a.w;
-      cy5[4 * q] = c.x * b.x; cy5[4 * q + 1] = c.y * b.y; cy5[4 * q + 2] = c.z * b.z; cy5[4 * q + 3] = c.w * b.w;
       mbits |= (uint32_t)(m.x != 0) << (4 * q) | (uint32_t)(m.y != 0) << (4 * q + 1) |
                (uint32_t)(m.z != 0) << (4 * q + 2) | (uint32_t)(m.w != 0) << (4 * q + 3);
-    } else {
-#pragma unroll
-      for (int e = 0; e < 4; ++e) { kx[4 * q + e] = 0.f; cy5[4 * q + e] = 0.f; }
+      *reinterpret_cast<float4 *>(lS + wave * NP + j0) = make_float4(0.f, 0.f, 0.f, 0.f);
+      *reinterpret_cast<float4 *>(lW + wave * NP + j0) = make_float4(0.f, 0.f, 0.f, 0.f);
     }
   }
+  __syncthreads();
   // allowed destinations of f at this node: the same simplex support for every row of f
   int cnt_f = 0;
 #pragma unroll
   for (int e = 0; e < E; ++e) cnt_f += __popcll(__ballot((mbits >> e) & 1u));
 
-  float colS[E], colW[E];
-#pragma unroll
-  for (int e = 0; e < E; ++e) { colS[e] = 0.f; colW[e] = 0.f; }
   double s_score = 0.0, s_pobj = 0.0, s_lagr = 0.0, s_move = 0.0, s_dist = 0.0;
   const double s_empty = (cnt_f == 0 && threadIdx.x == 0) ? (double)nrows : 0.0;
 
-  float xv[E], dv[E], av[E];
-  for (int rr = wave; rr < nrows; rr += kTileWaves) {
+  for (int rr = wave; rr < nrows; rr += TW) {
     const int r = r0 + rr;
     const RowInfo ri = v.rows[r];
     const bool nd = ri.src >= 0 && (ri.wobj != 0.f || ri.wsc != 0.f);
-    if (!PF || rr == wave)
-      load_row<CPL>(x + (int64_t)r * NP, v.D + (int64_t)(ri.src < 0 ? 0 : ri.src) * NP, xa + (int64_t)r * NP, nd,
-                    need_anchor, lane, NP, xv, dv, av);
+    // no software prefetch of the next row: the registers it costs are worth more as occupancy
+    // (0.575 vs 0.591 ms per launch before the LDS accumulators; other waves hide the latency)
     float xc[E], dc[E], ac[E];
-#pragma unroll
-    for (int e = 0; e < E; ++e) { xc[e] = xv[e]; dc[e] = dv[e]; ac[e] = av[e]; }
-    if (PF && rr + kTileWaves < nrows) {
-      const RowInfo rn = v.rows[r + kTileWaves];
-      const bool ndn = rn.src >= 0 && (rn.wobj != 0.f || rn.wsc != 0.f);
-      load_row<CPL>(x + (int64_t)(r + kTileWaves) * NP, v.D + (int64_t)(rn.src < 0 ? 0 : rn.src) * NP,
-                    xa + (int64_t)(r + kTileWaves) * NP, ndn, need_anchor, lane, NP, xv, dv, av);
-    }
+    load_row<CPL>(x + (int64_t)r * NP, v.D + (int64_t)(ri.src < 0 ? 0 : ri.src) * NP, xa + (int64_t)r * NP, nd,
+                  need_anchor, lane, NP, xc, dc, ac);
     const float m = ri.m, w = ri.w, wobj = ri.wobj, wsc = ri.wsc;
+    float kx[E], cy5[E];
+#pragma unroll
+    for (int q = 0; q < CPL; ++q) {
+      const int j0 = 4 * (lane + kWave * q);
+      float4 a = make_float4(0.f, 0.f, 0.f, 0.f), c = a;
+      if (j0 < NP) {
+        a = *reinterpret_cast<const float4 *>(lK + j0);
+        c = *reinterpret_cast<const float4 *>(lC + j0);
+      }
+      kx[4 * q] = a.x; kx[4 * q + 1] = a.y; kx[4 * q + 2] = a.z; kx[4 * q + 3] = a.w;
+      cy5[4 * q] = c.x; cy5[4 * q + 1] = c.y; cy5[4 * q + 2] = c.z; cy5[4 * q + 3] = c.w;
+    }
     // gradient step (reduced cost of x̄[r, j] = cost − Kᵀy)
     float vv[E];
     float s = 0.f;
@@ -383,11 +389,21 @@ __global__ __launch_bounds__(kTileThreads) void x_pass(DeviceView v, const int32
     }
     float sc = 0.f;
 #pragma unroll
-    for (int e = 0; e < E; ++e) {
-      colS[e] += m * xn[e];
-      colW[e] += w * xn[e];
-      sc += dc[e] * xn[e];
+    for (int q = 0; q < CPL; ++q) {
+      const int j0 = 4 * (lane + kWave * q);
+      if (j0 < NP) {
+        float4 *ps = reinterpret_cast<float4 *>(lS + wave * NP + j0);
+        float4 *pw = reinterpret_cast<float4 *>(lW + wave * NP + j0);
+        float4 a = *ps, b = *pw;
+        const float *xq = xn + 4 * q;
+        a.x += m * xq[0]; a.y += m * xq[1]; a.z += m * xq[2]; a.w += m * xq[3];
+        b.x += w * xq[0]; b.y += w * xq[1]; b.z += w * xq[2]; b.w += w * xq[3];
+        *ps = a;
+        *pw = b;
+      }
     }
+#pragma unroll
+    for (int e = 0; e < E; ++e) sc += dc[e] * xn[e];
     s_score += (double)wsc * (double)sc;
     if (CHECK) {
       double po = 0.0, mv = 0.0;
@@ -402,18 +418,7 @@ __global__ __launch_bounds__(kTileThreads) void x_pass(DeviceView v, const int32
     }
   }
 
-  // cross-wave reduction of the column partials
-  float *lS = lds, *lW = lds + kTileWaves * NP;
-#pragma unroll
-  for (int q = 0; q < CPL; ++q) {
-    const int j0 = 4 * (lane + kWave * q);
-    if (j0 < NP) {
-      *reinterpret_cast<float4 *>(lS + wave * NP + j0) =
-          make_float4(colS[4 * q], colS[4 * q + 1], colS[4 * q + 2], colS[4 * q + 3]);
-      *reinterpret_cast<float4 *>(lW + wave * NP + j0) =
-          make_float4(colW[4 * q], colW[4 * q + 1], colW[4 * q + 2], colW[4 * q + 3]);
-    }
-  }
+  // cross-wave reduction of the column partials (each wave's accumulators are in LDS)
   __syncthreads();
 
   // per-(f, j) small variables and rows
@@ -431,10 +436,10 @@ __global__ __launch_bounds__(kTileThreads) void x_pass(DeviceView v, const int32
   const double yD4 = v.step2 ? y[dl.oD4] : 0.0;
   SmallAcc a;
   double sumc = 0.0;
-  for (int j = threadIdx.x; j < N; j += kTileThreads) {
+  for (int j = threadIdx.x; j < N; j += kWave * TW) {
     float Sf = 0.f, Uf = 0.f;
 #pragma unroll
-    for (int wv = 0; wv < kTileWaves; ++wv) { Sf += lS[wv * NP + j]; Uf += lW[wv * NP + j]; }
+    for (int wv = 0; wv < TW; ++wv) { Sf += lS[wv * NP + j]; Uf += lW[wv * NP + j]; }
     const double S = Sf;
     const double U = (double)(Uf * v.cpr[(int64_t)f * NP + j]);
     const int idx = f * N + j;
@@ -500,7 +505,7 @@ __global__ __launch_bounds__(kTileThreads) void x_pass(DeviceView v, const int32
   if (k < NTS + NBS) {
     double t = 0.0;
 #pragma unroll
-    for (int wv = 0; wv < kTileWaves; ++wv) t = (k == NTS + BS_RES) ? fmax(t, lds_s[wv][k]) : t + lds_s[wv][k];
+    for (int wv = 0; wv < TW; ++wv) t = (k == NTS + BS_RES) ? fmax(t, lds_s[wv][k]) : t + lds_s[wv][k];
     if (k < NTS) v.tpart[slot * v.stpart + (int64_t)f * NTS + k] = t;
     else v.bpart[slot * v.sbpart + (int64_t)f * NBS + (k - NTS)] = t;
   }
@@ -814,16 +819,39 @@ __global__ void node_bounds_scatter(DeviceView v, const int32_t *__restrict__ sl
 // ------------------------------------------------------------------------------------------
 // launchers
 // ------------------------------------------------------------------------------------------
+template <int CPL, int TW>
+static hipError_t launch_x_tw(const DeviceView &v, const int32_t *slots, int nslots, bool check, bool init,
+                              bool first, bool plain, int it, hipStream_t s) {
+  dim3 grid(v.F, nslots), block(kWave * TW);
+  const size_t lds = (size_t)(2 * TW + 2) * v.NP * sizeof(float);
+  const int fi = first ? 1 : 0, pl = plain ? 1 : 0;
+  if (init) hipLaunchKernelGGL((x_pass<CPL, false, true, TW>), grid, block, lds, s, v, slots, fi, pl, it);
+  else if (check) hipLaunchKernelGGL((x_pass<CPL, true, false, TW>), grid, block, lds, s, v, slots, fi, pl, it);
+  else hipLaunchKernelGGL((x_pass<CPL, false, false, TW>), grid, block, lds, s, v, slots, fi, pl, it);
+  return hipGetLastError();
+}
+
+// Waves per workgroup: 4 when the LP slots alone fill the chip, more when few slots iterate (the
+// root LP, the tail of a B&B batch), so every CU still holds >= 16 waves: one LP at 512x256 runs
+// its x pass 1.9x faster with 16 waves (root LP 7.3 s -> 3.9 s) while 4 waves stay fastest from
+// ~4 slots on (0.47 vs 0.57 ms per launch at ~15 slots).  The column sums are then added in another
+// (still fixed) order, so an LP's last bits depend on how many slots iterated beside it.
+static int tile_waves(const DeviceView &v, int nslots) {
+  int tw = 4;
+  while (tw < 16 && (int64_t)nslots * v.F * tw < 4096) tw *= 2;
+  while (tw > 4 && (size_t)(2 * tw + 2) * v.NP * sizeof(float) > 128 * 1024) tw /= 2;
+  return tw;
+}
+
 template <int CPL>
 static hipError_t launch_x_cpl(const DeviceView &v, const int32_t *slots, int nslots, bool check, bool init,
                                bool first, bool plain, int it, hipStream_t s) {
-  dim3 grid(v.F, nslots), block(kTileThreads);
-  const size_t lds = (size_t)2 * kTileWaves * v.NP * sizeof(float);
-  const int fi = first ? 1 : 0, pl = plain ? 1 : 0;
-  if (init) hipLaunchKernelGGL((x_pass<CPL, false, true>), grid, block, lds, s, v, slots, fi, pl, it);
-  else if (check) hipLaunchKernelGGL((x_pass<CPL, true, false>), grid, block, lds, s, v, slots, fi, pl, it);
-  else hipLaunchKernelGGL((x_pass<CPL, false, false>), grid, block, lds, s, v, slots, fi, pl, it);
-  return hipGetLastError();
+  switch (tile_waves(v, nslots)) {
+    case 4: return launch_x_tw<CPL, 4>(v, slots, nslots, check, init, first, plain, it, s);
+    case 8: return launch_x_tw<CPL, 8>(v, slots, nslots, check, init, first, plain, it, s);
+    case 16: return launch_x_tw<CPL, 16>(v, slots, nslots, check, init, first, plain, it, s);
+    default: return hipErrorInvalidValue;
+  }
 }
 
 hipError_t launch_x_pass(const DeviceView &v, const int32_t *slots, int nslots, bool check, bool init, bool first,
