@@ -49,3 +49,48 @@ def test_root_and_node_lps(name, k):
         assert step >= 2 and st == LP_ITERATION_LIMIT, f"node {b}: status {st} iters {res['iters'][b]} obj {obj}"
         assert obj <= ref + TOL * max(1.0, abs(ref)), f"node {b}: bound {obj} above the LP optimum {ref}"
         assert _gap(obj, ref) <= LOOSE, f"node {b}: bound {obj} far from {ref}"
+
+
+@pytest.mark.parametrize("continuous", [False, True])
+def test_integer_and_continuous_delays(continuous):
+    """Integer delays (the generator's rounded distances) and continuous ones (496 distinct values):
+    the engine certifies the same LPs as HiGHS on the reference formulation."""
+    from core.engine.lp import LPModel, LP_OPTIMAL
+    from core.utils import data_to_solver_input
+    from core.utils.synthetic import synthetic_payload
+    from oracle.formulation import build_model
+    from oracle.inputs import data_to_solver_input as oracle_input
+    from oracle.solve import solve
+    N, F = 32, 12
+    p = synthetic_payload(N, F, seed=5, rho=0.3)
+    if continuous:
+        rng = np.random.default_rng(1)
+        D = rng.uniform(1.0, 100.0, size=(N, N))
+        D = np.minimum(D, D.T)
+        np.fill_diagonal(D, 0.0)
+        p["node_delay_matrix"] = D.tolist()
+        assert len(np.unique(D)) > 256
+    alpha = p["solver"]["args"]["alpha"]
+    data = data_to_solver_input(p, with_db=False)
+    ref_model = build_model(oracle_input(p, with_db=False), "MinDelayAndUtilization", step=1, alpha=alpha)
+    m = LPModel(data, "MinDelayAndUtilization", step=1, alpha=alpha, max_batch=4)
+    nx = N * N * F
+    rng = np.random.default_rng(2)
+    lb = np.full((4, m.n_int), -np.inf)
+    ub = np.full((4, m.n_int), np.inf)
+    for b in range(1, 4):
+        idx = rng.choice(F * N, size=2, replace=False)
+        lb[b, idx] = ub[b, idx] = rng.integers(0, 2, size=2)
+    res = m.solve(np.arange(4), lb, ub, tol=TOL, max_iters=100000)
+    for b in range(4):
+        rl, ru = ref_model["lb"].copy(), ref_model["ub"].copy()
+        fin = np.isfinite(lb[b])
+        rl[nx:][fin] = lb[b][fin]
+        ru[nx:][fin] = ub[b][fin]
+        _, ref, _ = solve(ref_model, relax=True, lb=rl, ub=ru)
+        if ref is None:
+            assert res["status"][b] != LP_OPTIMAL
+            continue
+        assert res["status"][b] == LP_OPTIMAL, f"node {b}: status {res['status'][b]}"
+        assert _gap(float(res["obj"][b]), ref) <= TOL, f"node {b}: {res['obj'][b]} vs {ref}"
+    m.close()
