@@ -66,7 +66,7 @@ def parse(argv=None):
     ap.add_argument("--warm-omega-floor", type=float, default=0.0,
                     help="warm-start primal-weight floor x the parent's (0: engine default)")
     ap.add_argument("--root-max-iters", type=int, default=400000)
-    ap.add_argument("--check-every", type=int, default=32, help="PDHG iterations per certificate check (node LPs)")
+    ap.add_argument("--check-every", type=int, default=16, help="PDHG iterations per certificate check (node LPs)")
     ap.add_argument("--root-check-every", type=int, default=64)
     ap.add_argument("--cold", action="store_true", help="cold-start every node LP")
     ap.add_argument("--cpu-budget", type=float, default=25.0, help="seconds for the CPU baseline (0 = skip)")

@@ -116,8 +116,9 @@ int nep_lp_solve_batch(void *model, int32_t B, const int32_t *slots, const doubl
 /* Streaming form, for a branch-and-bound that keeps every slot busy.
  * nep_lp_submit: start n node LPs in free slots (host presolve, then the slot's initialisation on
  *   the device).  status[b] = NEP_LP_INFEASIBLE when presolve proves node b infeasible (it does not
- *   iterate), NEP_LP_ITERATION_LIMIT when it starts iterating.  opts apply to every LP in flight;
- *   check_every cannot change while any slot iterates.
+ *   iterate), NEP_LP_ITERATION_LIMIT when it starts iterating.  max_iters, warm_start and
+ *   warm_omega_floor apply to the LPs of this call; tol and cutoff (the last submit's) to every LP
+ *   in flight; check_every cannot change while any slot iterates.
  * nep_lp_advance: run blocks of check_every PDHG iterations on every iterating slot until at least
  *   min_done of them finished (min_done <= 0: exactly one block).  The finished slots and their
  *   results go to the first *n_done entries of the outputs (each sized max_batch).

@@ -53,6 +53,7 @@ struct Ctrl {
   double pobj, lagr, best_lagr, pres, gap;
   double omega_lo, omega_hi;
   int64_t k, k_since_restart, ks_base;   // ks_base: Halpern counter at the block's first iteration
+  int64_t max_iters;                     // this LP's iteration limit (nep_lp_opts of its submit)
   int32_t status, active, restart_pending, pad;
 };
 

@@ -710,7 +710,7 @@ __global__ __launch_bounds__(256) void scalar_pass(DeviceView v, const int32_t *
     ctrl->status = 0; ctrl->active = 0; return;
   }
   if (ctrl->best_lagr > v.cutoff) { ctrl->status = 3; ctrl->active = 0; return; }
-  if (ctrl->k >= v.max_iters) { ctrl->status = 1; ctrl->active = 0; return; }
+  if (ctrl->k >= ctrl->max_iters) { ctrl->status = 1; ctrl->active = 0; return; }
   if (!isfinite(pobj) || !isfinite(a.mvz) || !isfinite(a.mvy)) { ctrl->status = 4; ctrl->active = 0; return; }
 
   // restart test on the fixed-point residual of the last iteration (ω-weighted norm)
@@ -775,6 +775,7 @@ __global__ void init_slot(DeviceView v, const int32_t *__restrict__ slots, int w
     ctrl->sigma = eta * ctrl->omega;
     ctrl->status = 1;
     ctrl->active = 1;
+    ctrl->max_iters = v.max_iters;
     ctrl->restart_pending = 1;
     ctrl->best_lagr = -INFINITY;
     ctrl->pobj = ctrl->lagr = ctrl->pres = ctrl->gap = NAN;
