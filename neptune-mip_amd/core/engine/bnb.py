@@ -16,6 +16,13 @@ those subtrees alone.  Per batch the ranks exchange the incumbent value (all-red
 their open-node counts (all-reduce SUM, termination); at the end the owner of the best incumbent
 (lowest rank on ties) broadcasts its placement.  No collective runs inside an LP.
 
+Warm starts: with `lp.max_batch >= 2 * batch + 1` (and an engine with nep_lp_copy_state) every
+node LP after the root starts from its parent's final PDHG state when the parent is still resident
+— batches alternate between the two halves of the slots, so the previous batch's nodes (the
+parents of the children best-first pops next) stay on the device — else from the root's state,
+kept in the last slot (SCIP warm-starts its node LPs from the parent basis the same way).  The
+engine floors a warm-started LP's primal weight at 2x the parent's.
+
 Exactness:
   * a node's value is the engine's certified Lagrangian bound, a valid lower bound even when PDHG
     stopped at its iteration limit, so pruning never discards the optimum;
@@ -68,7 +75,8 @@ class BranchAndBound:
     """
 
     def __init__(self, lp, workload, fn_mem, node_mem, batch=16, tol=1e-7, gap=1e-6, max_iters=100000,
-                 node_limit=20000, time_limit=None, upper_bound=math.inf, flow_tol=1e-4, log=None, comm=None):
+                 node_limit=20000, time_limit=None, upper_bound=math.inf, flow_tol=1e-4, log=None, comm=None,
+                 warm=True):
         self.lp = lp
         self.N, self.F = lp.N, lp.F
         L = lp.layout()
@@ -79,6 +87,9 @@ class BranchAndBound:
         self.fn_mem = np.asarray(fn_mem, np.float64).reshape(self.F)
         self.node_mem = np.asarray(node_mem, np.float64).reshape(self.N)
         self.batch = min(int(batch), lp.max_batch)
+        self.warm = bool(warm) and hasattr(lp, "copy_state") and lp.max_batch >= 2 * self.batch + 1
+        self.root_slot = lp.max_batch - 1
+        self.slot_gen = [0] * lp.max_batch     # bumped whenever a slot takes a new LP
         self.tol, self.gap, self.max_iters = tol, gap, max_iters
         self.node_limit, self.time_limit = node_limit, time_limit
         self.ub0 = upper_bound
@@ -150,6 +161,29 @@ class BranchAndBound:
             return None
         return max(free, key=lambda v: (z[v], -v))
 
+    def _place(self, batch, half, root_ready):
+        """Slots of this batch's LPs and whether they start warm.  Cold: slots 0..B-1.  Warm: the
+        half of the slots the previous batch did not use; each LP starts from its parent's state if
+        that is still resident in the other half, else from the root's."""
+        B = len(batch)
+        if not (self.warm and root_ready):
+            slots = np.arange(B, dtype=np.int32)
+            for s in slots:
+                self.slot_gen[s] += 1
+            return slots, False
+        base = half * self.batch
+        slots = np.arange(base, base + B, dtype=np.int32)
+        for b, (_, _, _, pref) in enumerate(batch):
+            src = self.root_slot
+            if pref is not None:
+                ps, pg = pref
+                if self.slot_gen[ps] == pg and not (base <= ps < base + self.batch):
+                    src = ps
+            self.lp.copy_state(src, int(slots[b]))
+        for s in slots:
+            self.slot_gen[s] += 1
+        return slots, True
+
     # ---------------------------------------------------------------------------------------
     def solve(self):
         t0 = time.time()
@@ -157,8 +191,11 @@ class BranchAndBound:
         lp, n_int = self.lp, self.lp.n_int
         inc = math.inf
         seq = itertools.count()
-        heap = [(-math.inf, 0, next(seq), {}, False)]   # (bound, -depth, seq, fixings, is_leaf)
-        pending_leaves = []
+        # (bound, -depth, seq, fixings, is_leaf, parent) with parent = (slot, generation) or None
+        heap = [(-math.inf, 0, next(seq), {}, False, None)]
+        pending_leaves = []                              # (fixings, parent)
+        half = 0
+        root_ready = False
         seen_leaves = set()
         limit_hit = False
         comm = self.comm
@@ -185,30 +222,37 @@ class BranchAndBound:
                 break
             batch = []
             while pending_leaves and len(batch) < self.batch:
-                batch.append((-math.inf, pending_leaves.pop(), True))
+                leaf, pref = pending_leaves.pop()
+                batch.append((-math.inf, leaf, True, pref))
             while heap and len(batch) < self.batch:
-                bnd, _, _, fix, is_leaf = heapq.heappop(heap)
+                bnd, _, _, fix, is_leaf, pref = heapq.heappop(heap)
                 if bnd >= inc - self._gap_abs(inc):
                     continue
-                batch.append((bnd, fix, is_leaf))
+                batch.append((bnd, fix, is_leaf, pref))
             if not batch:
                 continue
             B = len(batch)
+            slots, warm = self._place(batch, half, root_ready)
+            half ^= 1
             lb = np.full((B, n_int), -np.inf)
             ub = np.full((B, n_int), np.inf)
-            for b, (_, fix, _) in enumerate(batch):
+            for b, (_, fix, _, _) in enumerate(batch):
                 if fix:
                     idx = np.fromiter(fix.keys(), np.int64, len(fix))
                     val = np.fromiter(fix.values(), np.float64, len(fix))
                     lb[b, idx] = val
                     ub[b, idx] = val
             cutoff = min(inc, self.ub0)
-            r = lp.solve(np.arange(B), lb, ub, tol=self.tol, max_iters=self.max_iters,
-                         cutoff=cutoff if math.isfinite(cutoff) else math.inf)
+            r = lp.solve(slots, lb, ub, tol=self.tol, max_iters=self.max_iters,
+                         cutoff=cutoff if math.isfinite(cutoff) else math.inf, warm_start=warm)
             res.lps += B
             res.lp_iterations += int(r["iters"].sum())
-            for b, (pbound, fix, is_leaf) in enumerate(batch):
+            for b, (pbound, fix, is_leaf, _) in enumerate(batch):
+                slot = int(slots[b])
                 st = int(r["status"][b])
+                if self.warm and not fix and not root_ready and st not in (LP_INFEASIBLE, LP_CUTOFF):
+                    lp.copy_state(slot, self.root_slot)   # every later node can start from the root
+                    root_ready = True
                 if st in (LP_INFEASIBLE, LP_CUTOFF):
                     continue
                 bound = max(pbound, float(r["obj"][b]))
@@ -221,27 +265,28 @@ class BranchAndBound:
                     if val < inc - self._gap_abs(inc):
                         inc = val
                         res.objective = val
-                        res.z, res.x = lp.solution(b, dense_x=True)
+                        res.z, res.x = lp.solution(slot, dense_x=True)
                         self.log(f"incumbent {val:.10g} (lps {res.lps}, nodes {res.nodes})")
                     continue
                 if bound >= inc - self._gap_abs(inc):
                     continue
                 res.nodes += 1
-                z, _ = lp.solution(b, dense_x=False)
-                flow = self._flows(b)
+                z, _ = lp.solution(slot, dense_x=False)
+                flow = self._flows(slot)
+                me = (slot, self.slot_gen[slot])
                 leaf = self._round(fix, flow)
                 if leaf is not None:
                     key = tuple(sorted(k for k, v in leaf.items() if v > 0.5))
                     if key not in seen_leaves:
                         seen_leaves.add(key)
-                        pending_leaves.append(leaf)
+                        pending_leaves.append((leaf, me))
                 var = self._branch_var(fix, z, flow)
                 if var is None:
                     continue
                 for v in (1.0, 0.0):
                     child = dict(fix)
                     child[var] = v
-                    heapq.heappush(heap, (bound, -len(child), next(seq), child, self._complete(child)))
+                    heapq.heappush(heap, (bound, -len(child), next(seq), child, self._complete(child), me))
         if heap:
             res.bound = min(min(h[0] for h in heap), inc)
         else:

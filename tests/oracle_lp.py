@@ -68,6 +68,12 @@ class OracleLP:
             self._sol[int(s)] = x
         return {"obj": obj, "primal_obj": obj.copy(), "status": status, "iters": np.zeros(B, np.int64)}
 
+    def copy_state(self, src, dst):
+        """Warm-start hand-off of the engine (nep_lp_copy_state); HiGHS solves from scratch, so this
+        only records the copy (tests check the B&B's slot bookkeeping with it)."""
+        self.copies = getattr(self, "copies", 0) + 1
+        self._sol[int(dst)] = self._sol.get(int(src))
+
     def rows(self, slot):
         x = self._sol[int(slot)]
         xb = x[:self.nx].reshape(self.F * self.N, self.N).astype(np.float32)

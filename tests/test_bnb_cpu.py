@@ -40,9 +40,11 @@ def test_bnb_matches_recorded_mip(name, k):
         data.prev_x = m1["mip_x"][:N * N * F].reshape(F, N, N).transpose(1, 0, 2)
         kw["max_score"] = float(m1["mip_objective"])
         step = 2 if rec["mode"] == "step2_delete" else 3
-    lp = OracleLP(data, variant, step=step, max_batch=8, **kw)
+    lp = OracleLP(data, variant, step=step, max_batch=17, **kw)    # 2 x batch + root: warm-start slots
     res = BranchAndBound(lp, data.workload_matrix, data.function_memory_matrix, data.node_memory_matrix,
                          batch=8, node_limit=20000).solve()
+    if res.lps > 1:
+        assert getattr(lp, "copies", 0) > 0, "warm-start slot hand-offs never ran"
     if rec["status"] == 0:
         assert res.status == OPTIMAL, res.as_dict()
         assert _close(res.objective, rec["mip_objective"]), (res.objective, rec["mip_objective"])
