@@ -102,6 +102,12 @@ struct Model {
   double *d_chg_lb = nullptr, *d_chg_ub = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   nep_stats stats{};
+  // one block of check_every PDHG iterations as a captured HIP graph, per iterating-slot count
+  // (the launch grids depend on it); rebuilt when check_every changes
+  std::vector<hipGraphExec_t> block_graph;   // [max_batch + 1], index = slots iterating
+  int graph_ce = 0;
+  int64_t blocks = 0;
+  bool graphs_ok = true;                     // false once capture failed on this stream: eager blocks
   // streaming state
   std::vector<int32_t> act;     // slots currently iterating
   std::vector<uint8_t> busy;    // per slot: iterating
@@ -109,6 +115,8 @@ struct Model {
   ~Model() {
     if (stream) (void)hipStreamSynchronize(stream);
     for (void *p : allocs) (void)hipFree(p);
+    for (hipGraphExec_t g : block_graph)
+      if (g) (void)hipGraphExecDestroy(g);
     if (ev0) (void)hipEventDestroy(ev0);
     if (ev1) (void)hipEventDestroy(ev1);
     if (own_stream && stream) (void)hipStreamDestroy(stream);
@@ -874,6 +882,43 @@ int submit(Model &m, int n, const int32_t *slots, const double *lbi, const doubl
   return NEP_OK;
 }
 
+// The launches of one block (iterations 0 .. ce-1 on `na` iterating slots, m.d_slots) captured
+// once as a HIP graph and cached per na; m.d_slots is read by the kernels at run time, so the
+// graph replays for any set of na slots.
+hipError_t block_graph(Model &m, int na, hipGraphExec_t *out) {
+  const int ce = m.run.check_every;
+  if (m.graph_ce != ce) {
+    for (hipGraphExec_t &g : m.block_graph)
+      if (g) { (void)hipGraphExecDestroy(g); g = nullptr; }
+    m.block_graph.assign(m.max_batch + 1, nullptr);
+    m.graph_ce = ce;
+  }
+  if (!m.block_graph[na]) {
+    hipError_t e = hipStreamBeginCapture(m.stream, hipStreamCaptureModeThreadLocal);
+    if (e != hipSuccess) return e;
+    hipError_t le = hipSuccess;
+    for (int it = 0; it < ce && le == hipSuccess; ++it) {
+      const bool check = it == 0, first = it == 1;
+      const bool plain = ce < 4 || it == 0 || it == ce - 1;
+      le = launch_x_pass(m.v, m.d_slots, na, check, false, first, plain, it, m.stream);
+      if (le == hipSuccess) le = launch_node_pass(m.v, m.d_slots, na, check, false, first, plain, it, m.stream);
+      if (le == hipSuccess && (m.step2 || check))
+        le = launch_scalar_pass(m.v, m.d_slots, na, check, false, first, plain, it, ce, m.stream);
+    }
+    hipGraph_t graph = nullptr;
+    e = hipStreamEndCapture(m.stream, &graph);
+    if (le != hipSuccess) { if (graph) (void)hipGraphDestroy(graph); return le; }
+    if (e != hipSuccess) return e;
+    hipGraphExec_t exec = nullptr;
+    e = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(graph);
+    if (e != hipSuccess) return e;
+    m.block_graph[na] = exec;
+  }
+  *out = m.block_graph[na];
+  return hipSuccess;
+}
+
 // Run blocks of `check_every` PDHG iterations on every iterating slot until at least `min_done`
 // of them have finished (min_done <= 0: exactly one block).  Finished slots are reported in
 // done[0 .. *n_done) with their results.
@@ -891,8 +936,24 @@ int advance(Model &m, int min_done, int32_t *n_done, int32_t *done, double *obj,
     // it == ce - 1 is plain again; the others are reflected Halpern steps.  One steady-state
     // x-pass launch per block is bracketed by HIP events on the model's stream; the events are
     // read after the block's own stream sync, so sampling adds no synchronisation.
-    const int sample_it = ce >= 4 ? 2 : -1;
-    for (int it = 0; it < ce; ++it) {
+    // Every 4th block runs eagerly with one steady-state x-pass launch bracketed by HIP events
+    // (nep_get_stats); the others replay the block's launches as one HIP graph (a block is 2-3
+    // launches per iteration: at small sizes the iteration is launch-latency bound).
+    const int sample_it = (ce >= 4 && m.blocks % 4 == 0) ? 2 : -1;
+    m.blocks += 1;
+    bool eager = sample_it >= 0 || !m.graphs_ok;
+    if (!eager) {
+      hipGraphExec_t g = nullptr;
+      if (block_graph(m, na, &g) != hipSuccess) {
+        (void)hipGetLastError();
+        m.graphs_ok = false;   // e.g. a caller's stream that cannot be captured
+        eager = true;
+      } else {
+        HIPCHK(hipGraphLaunch(g, m.stream));
+        m.stats.x_pass_launches += ce;
+      }
+    }
+    for (int it = 0; it < ce && eager; ++it) {
       const bool check = it == 0, first = it == 1;
       const bool plain = ce < 4 || it == 0 || it == ce - 1;
       const bool sample = it == sample_it;
