@@ -74,9 +74,9 @@ class BranchAndBound:
                   stopped early (infeasible nodes have an unbounded Lagrangian)
     """
 
-    def __init__(self, lp, workload, fn_mem, node_mem, batch=16, tol=1e-7, gap=1e-6, max_iters=100000,
+    def __init__(self, lp, workload, fn_mem, node_mem, batch=16, tol=1e-7, gap=1e-6, max_iters=5000,
                  node_limit=20000, time_limit=None, upper_bound=math.inf, flow_tol=1e-4, log=None, comm=None,
-                 warm=True):
+                 warm=True, root_max_iters=200000):
         self.lp = lp
         self.N, self.F = lp.N, lp.F
         L = lp.layout()
@@ -90,7 +90,10 @@ class BranchAndBound:
         self.warm = bool(warm) and hasattr(lp, "copy_state") and lp.max_batch >= 2 * self.batch + 1
         self.root_slot = lp.max_batch - 1
         self.slot_gen = [0] * lp.max_batch     # bumped whenever a slot takes a new LP
+        # node LPs stop at max_iters (their Lagrangian bound stays valid for pruning; a leaf only
+        # becomes an incumbent when certified); the root, solved cold, gets root_max_iters
         self.tol, self.gap, self.max_iters = tol, gap, max_iters
+        self.root_max_iters = max(max_iters, root_max_iters)
         self.node_limit, self.time_limit = node_limit, time_limit
         self.ub0 = upper_bound
         self.flow_tol = flow_tol
@@ -243,7 +246,8 @@ class BranchAndBound:
                     lb[b, idx] = val
                     ub[b, idx] = val
             cutoff = min(inc, self.ub0)
-            r = lp.solve(slots, lb, ub, tol=self.tol, max_iters=self.max_iters,
+            is_root = res.lps == 0
+            r = lp.solve(slots, lb, ub, tol=self.tol, max_iters=self.root_max_iters if is_root else self.max_iters,
                          cutoff=cutoff if math.isfinite(cutoff) else math.inf, warm_start=warm)
             res.lps += B
             res.lp_iterations += int(r["iters"].sum())

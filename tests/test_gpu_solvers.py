@@ -9,7 +9,10 @@ from golden_util import golden, payload
 pytestmark = pytest.mark.gpu
 G = golden()
 CASES = ["payload", "testpy", "syn_4x3_s0_r0.5_NeptuneMinDelayAndUtilization", "syn_4x3_s0_r0.5_NeptuneMinDelay",
-         "syn_4x3_s0_r0.5_NeptuneMinUtilization", "sim3_NeptuneMinDelayAndUtilization", "sim2_NeptuneMinUtilization"]
+         "syn_4x3_s0_r0.5_NeptuneMinUtilization", "syn_6x4_s1_r0.3_NeptuneMinDelayAndUtilization",
+         "syn_6x4_s1_r0.3_NeptuneMinDelay", "syn_6x4_s1_r0.3_NeptuneMinUtilization",
+         "syn_8x4_s2_r0.1_NeptuneMinDelayAndUtilization", "sim0_NeptuneMinDelay", "sim3_NeptuneMinDelayAndUtilization",
+         "sim2_NeptuneMinUtilization", "sim4_NeptuneMinUtilization"]
 
 
 def _close(a, b, tol=1e-6):
