@@ -209,18 +209,26 @@ __device__ __forceinline__ void load_row(const float *__restrict__ xrow, const f
 //     (memory, Σ_f c, CPU) for node_pass;
 //  4. (init / certificate / step-2 iterations) the workgroup's scalar partials.
 // ---------------------------------------------------------------------------------------------
-template <int CPL, bool CHECK, bool INIT, int TW>
 // Occupancy: the plain iterations are held to <= 85 VGPRs (6 waves per SIMD, no spills at TW 4/8);
 // measured at 512x256 / ~14 LPs per launch: 0.382 ms per launch vs 0.402 at the compiler's own 86
 // VGPRs (5 waves) and 0.428 when forced to 8 waves (64 VGPRs + 68 B/lane of spills).  The
 // certificate iterations (fp64 Lagrangian terms, 143 VGPRs) run at 3 waves per SIMD.
-__global__ __launch_bounds__(kWave * TW) __attribute__((amdgpu_waves_per_eu(CHECK ? 2 : (TW == 16 ? 4 : 6), 8))) void x_pass(DeviceView v, const int32_t *__restrict__ slots, int first,
-                                                     int plain, int it) {
+template <int CPL, bool CHECK, bool INIT, int TW>
+__global__ __launch_bounds__(kWave * TW) __attribute__((amdgpu_waves_per_eu(CHECK ? 2 : (TW == 16 ? 4 : 6), 8)))
+void x_pass(DeviceView v, const int32_t *__restrict__ slots, int first, int plain, int it, int nslots) {
   constexpr int E = 4 * CPL;
   extern __shared__ __attribute__((aligned(16))) float lds[];   // [2][TW][NP] accumulators + [2][NP] constants
   __shared__ double lds_s[TW][NTS + NBS];
-  const int f = blockIdx.x;
-  const int slot = slots[blockIdx.y];
+  // XCD-aware order (speed only; every (f, slot) pair is one workgroup either way): workgroup
+  // ids are dealt round-robin over the 8 XCDs, so id -> p = (id % 8) * Q + id / 8 gives each XCD
+  // a contiguous run of p = f * nslots + s, i.e. all the LP slots of the same functions back to
+  // back on one XCD: the delay rows D[src, :] of a function's routing rows are then fetched into
+  // that XCD's L2 once and re-read from it by the function's other slots.
+  const int total = v.F * nslots, Q = (total + 7) / 8;
+  const int p = (int)(blockIdx.x % 8) * Q + (int)(blockIdx.x / 8);
+  if (p >= total) return;
+  const int f = p / nslots;
+  const int slot = slots[p - f * nslots];
   Ctrl *ctrl = v.ctrl + slot;
   if (!ctrl->active) return;
   const int NP = v.NP, F = v.F, N = v.N;
@@ -823,12 +831,13 @@ __global__ void node_bounds_scatter(DeviceView v, const int32_t *__restrict__ sl
 template <int CPL, int TW>
 static hipError_t launch_x_tw(const DeviceView &v, const int32_t *slots, int nslots, bool check, bool init,
                               bool first, bool plain, int it, hipStream_t s) {
-  dim3 grid(v.F, nslots), block(kWave * TW);
+  dim3 grid(8 * ((v.F * nslots + 7) / 8)), block(kWave * TW);
   const size_t lds = (size_t)(2 * TW + 2) * v.NP * sizeof(float);
   const int fi = first ? 1 : 0, pl = plain ? 1 : 0;
-  if (init) hipLaunchKernelGGL((x_pass<CPL, false, true, TW>), grid, block, lds, s, v, slots, fi, pl, it);
-  else if (check) hipLaunchKernelGGL((x_pass<CPL, true, false, TW>), grid, block, lds, s, v, slots, fi, pl, it);
-  else hipLaunchKernelGGL((x_pass<CPL, false, false, TW>), grid, block, lds, s, v, slots, fi, pl, it);
+  if (init) hipLaunchKernelGGL((x_pass<CPL, false, true, TW>), grid, block, lds, s, v, slots, fi, pl, it, nslots);
+  else if (check)
+    hipLaunchKernelGGL((x_pass<CPL, true, false, TW>), grid, block, lds, s, v, slots, fi, pl, it, nslots);
+  else hipLaunchKernelGGL((x_pass<CPL, false, false, TW>), grid, block, lds, s, v, slots, fi, pl, it, nslots);
   return hipGetLastError();
 }
 

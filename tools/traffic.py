@@ -41,29 +41,27 @@ def run():
     m.close()
 
 
-def _counters(d):
+def _counters(d, F):
+    """Per-launch counter values of the steady-state x_pass launches, keyed by (counter, LP slots in
+    the launch); slots = workgroups / F (the x-pass grid is F x slots workgroups, padded to a
+    multiple of 8 for its XCD-aware order)."""
     dbs = [os.path.join(r, f) for r, _, fs in os.walk(d) for f in fs if f.endswith(".db")]
     vals = {}
     for db in dbs:
         c = sqlite3.connect(db)
-        q = ("select k.name, k.grid_y, p.counter_name, p.value from counters_collection p "
+        q = ("select k.name, k.grid_x * k.grid_y / k.workgroup_x, p.counter_name, p.value from counters_collection p "
              "join kernels k on k.dispatch_id = p.dispatch_id")
-        try:
-            rows = list(c.execute(q))
-        except sqlite3.Error:
-            rows = [(r[0], r[1], r[2], r[3]) for r in c.execute(
-                "select kernel_name, grid_y, counter_name, counter_value from counters_collection")]
-        for name, gy, cname, v in rows:
+        for name, wgs, cname, v in c.execute(q):
             if "x_pass" in name and "false, false" in name:
-                vals.setdefault((cname, gy), []).append(float(v))
+                vals.setdefault((cname, int(wgs) // F), []).append(float(v))
     return vals
 
 
 def summarize(fetch_dir, write_dir):
     import bench
     a = bench.parse([])
-    f = _counters(fetch_dir)
-    w = _counters(write_dir)
+    f = _counters(fetch_dir, a.functions)
+    w = _counters(write_dir, a.functions)
     fk = max(f, key=lambda k: (k[1], len(f[k])))
     wk = max(w, key=lambda k: (k[1], len(w[k])))
     fetch_kib = sum(f[fk]) / len(f[fk])
