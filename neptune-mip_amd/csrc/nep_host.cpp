@@ -573,6 +573,7 @@ int setup_dense(Model &m, const nep_model_desc &d) {
   v.snpart = (int64_t)F * 3 * NP;
   if ((rc = dalloc(m, &v.x, (size_t)B * v.sx))) return rc;
   if ((rc = dalloc(m, &v.xa, (size_t)B * v.sx))) return rc;
+  if ((rc = dalloc(m, &v.theta, (size_t)B * m.R))) return rc;
   if ((rc = dalloc(m, &v.mask, (size_t)B * v.smask))) return rc;
   if ((rc = dalloc(m, &v.zi, (size_t)B * v.sint))) return rc;
   if ((rc = dalloc(m, &v.zia, (size_t)B * v.sint))) return rc;
@@ -606,6 +607,7 @@ int setup_dense(Model &m, const nep_model_desc &d) {
   HIPCHK(hipMemsetAsync(v.ctrl, 0, sizeof(Ctrl) * B, m.stream));
   HIPCHK(hipMemsetAsync(v.x, 0, sizeof(float) * B * v.sx, m.stream));
   HIPCHK(hipMemsetAsync(v.xa, 0, sizeof(float) * B * v.sx, m.stream));
+  HIPCHK(hipMemsetAsync(v.theta, 0xFF, sizeof(float) * B * m.R, m.stream));   // NaN: no hint
   HIPCHK(hipMemsetAsync(v.zi, 0, sizeof(double) * B * v.sint, m.stream));
   HIPCHK(hipMemsetAsync(v.y, 0, sizeof(double) * B * v.sdual, m.stream));
   HIPCHK(hipStreamSynchronize(m.stream));
@@ -1157,6 +1159,8 @@ int nep_lp_copy_state(void *model, int32_t src, int32_t dst) {
   if (src == dst) return NEP_OK;
   const DeviceView &v = m.v;
   HIPCHK(hipMemcpyAsync(v.x + dst * v.sx, v.x + src * v.sx, v.sx * sizeof(float), hipMemcpyDeviceToDevice, m.stream));
+  HIPCHK(hipMemcpyAsync(v.theta + dst * m.R, v.theta + src * m.R, m.R * sizeof(float), hipMemcpyDeviceToDevice,
+                        m.stream));
   HIPCHK(hipMemcpyAsync(v.zi + dst * v.sint, v.zi + src * v.sint, v.sint * sizeof(double), hipMemcpyDeviceToDevice,
                         m.stream));
   HIPCHK(hipMemcpyAsync(v.y + dst * v.sdual, v.y + src * v.sdual, v.sdual * sizeof(double), hipMemcpyDeviceToDevice,

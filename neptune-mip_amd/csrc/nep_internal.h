@@ -82,6 +82,7 @@ struct DeviceView {
   const double *gam, *rho, *lo, *hi, *rownorm, *cost_int, *mem_f;
   // per slot (base pointers; slot stride below)
   float *x, *xa;
+  float *theta;                          // [R] last simplex threshold of each routing row (a start hint)
   uint8_t *mask;
   double *zi, *zia, *lb, *ub;
   double *y, *ya, *kz, *kza;             // duals, anchor, activity K z of the iterate and of the anchor

@@ -243,6 +243,7 @@ void x_pass(DeviceView v, const int32_t *__restrict__ slots, int first, int plai
   const int r0 = v.frow[f], nrows = v.frow[f + 1] - r0;
   float *__restrict__ x = v.x + slot * v.sx;
   float *__restrict__ xa = v.xa + slot * v.sx;
+  float *__restrict__ th_row = v.theta + (int64_t)slot * v.R;   // per-row simplex thresholds (hints)
   const uint8_t *__restrict__ mask = v.mask + slot * v.smask + (int64_t)f * NP;
   float *__restrict__ kty = v.kty + slot * v.skty;
   const float ys = kty[(int64_t)F * NP + NP];
@@ -337,8 +338,29 @@ void x_pass(DeviceView v, const int32_t *__restrict__ slots, int first, int plai
       for (int e = 0; e < E; ++e)
         if ((mbits >> e) & 1u) vm = fmaxf(vm, vv[e]);
       float hi = wave_max_u(vm);
-      float lo_s = wave_sum_u(s);   // S(-inf), c(-inf) = cnt_f
-      int lo_c = cnt_f;
+      // Start from this row's threshold of the previous iteration when it is usable: one pass gives
+      // S and c at theta_prev, the first Newton step from there is the tangent root (left of the
+      // root from either side, f being convex), and the support usually stops changing one pass
+      // later.  Cold rows start from -inf (S = sum of all allowed values, c = cnt_f).  Either way
+      // the loop ends on the same exact (S* - 1) / |S*|, so the start only changes the pass count.
+      const float th0 = th_row[r];
+      float lo_s;
+      int lo_c;
+      if (!INIT && th0 < hi && th0 > -INFINITY) {   // false for NaN (no hint yet)
+        float s0 = 0.f;
+        int c0 = 0;
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          const bool in = ((mbits >> e) & 1u) && vv[e] > th0;
+          if (in) s0 += vv[e];
+          c0 += __popcll(__ballot(in));
+        }
+        lo_s = wave_sum_u(s0);
+        lo_c = c0;                                  // >= 1: the maximum lies above th0
+      } else {
+        lo_s = wave_sum_u(s);
+        lo_c = cnt_f;
+      }
       float lo = -INFINITY;
       for (int k = 0; k < 96; ++k) {
         const bool bisect = k >= 4 && (k & 1) && lo > -INFINITY;
@@ -363,6 +385,7 @@ void x_pass(DeviceView v, const int32_t *__restrict__ slots, int first, int plai
         }
       }
     }
+    if (lane == 0) th_row[r] = theta;
     float xn[E];
 #pragma unroll
     for (int e = 0; e < E; ++e) xn[e] = ((mbits >> e) & 1u) ? fmaxf(vv[e] - theta, 0.f) : 0.f;
