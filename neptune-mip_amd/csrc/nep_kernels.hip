@@ -337,33 +337,33 @@ void x_pass(DeviceView v, const int32_t *__restrict__ slots, int first, int plai
 #pragma unroll
       for (int e = 0; e < E; ++e)
         if ((mbits >> e) & 1u) vm = fmaxf(vm, vv[e]);
-      float hi = wave_max_u(vm);
       // Start from this row's threshold of the previous iteration when it is usable: one pass gives
       // S and c at theta_prev, the first Newton step from there is the tangent root (left of the
       // root from either side, f being convex), and the support usually stops changing one pass
       // later.  Cold rows start from -inf (S = sum of all allowed values, c = cnt_f).  Either way
       // the loop ends on the same exact (S* - 1) / |S*|, so the start only changes the pass count.
       const float th0 = th_row[r];
-      float lo_s;
-      int lo_c;
-      if (!INIT && th0 < hi && th0 > -INFINITY) {   // false for NaN (no hint yet)
+      float lo_s = 0.f;
+      int lo_c = 0;
+      if (!INIT && th0 > -INFINITY && th0 < INFINITY) {   // false for NaN (no hint yet)
         float s0 = 0.f;
-        int c0 = 0;
 #pragma unroll
         for (int e = 0; e < E; ++e) {
           const bool in = ((mbits >> e) & 1u) && vv[e] > th0;
           if (in) s0 += vv[e];
-          c0 += __popcll(__ballot(in));
+          lo_c += __popcll(__ballot(in));
         }
         lo_s = wave_sum_u(s0);
-        lo_c = c0;                                  // >= 1: the maximum lies above th0
-      } else {
+      }
+      if (lo_c == 0) {                              // no hint, or every value at or below it
         lo_s = wave_sum_u(s);
         lo_c = cnt_f;
       }
+      float hi = INFINITY;                          // right bracket max(v): reduced only if bisection is needed
       float lo = -INFINITY;
       for (int k = 0; k < 96; ++k) {
         const bool bisect = k >= 4 && (k & 1) && lo > -INFINITY;
+        if (bisect && hi == INFINITY) hi = wave_max_u(vm);
         const float t = bisect ? 0.5f * (lo + hi) : (lo_s - 1.f) / (float)lo_c;
         float s2 = 0.f;
         int c2 = 0;
