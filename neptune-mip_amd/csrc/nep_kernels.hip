@@ -209,7 +209,9 @@ __device__ __forceinline__ void load_row(const float *__restrict__ xrow, const f
 //     (memory, Σ_f c, CPU) for node_pass;
 //  4. (init / certificate / step-2 iterations) the workgroup's scalar partials.
 // ---------------------------------------------------------------------------------------------
-// Occupancy: the plain iterations are held to <= 85 VGPRs (6 waves per SIMD, no spills at TW 4/8);
+// Occupancy: the plain iterations are held to <= 85 VGPRs (6 waves per SIMD; no spills at TW 4, 11
+// VGPRs / 32 B per lane spilled at TW 8, which only runs for 2-3 slots where 6 waves keep 3
+// workgroups per CU resident);
 // measured at 512x256 / ~14 LPs per launch: 0.382 ms per launch vs 0.402 at the compiler's own 86
 // VGPRs (5 waves) and 0.428 when forced to 8 waves (64 VGPRs + 68 B/lane of spills).  The
 // certificate iterations (fp64 Lagrangian terms, 143 VGPRs) run at 3 waves per SIMD.
