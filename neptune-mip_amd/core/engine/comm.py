@@ -45,7 +45,10 @@ class TorchComm:
         return int(self._reduce(int(v), self._d.ReduceOp.SUM, self._t.int64))
 
     def bcast(self, arr, src):
+        """Broadcast from the member of rank `src` WITHIN this communicator's group (torch's
+        broadcast takes a global rank: mapped with get_global_rank for non-default groups)."""
         a = np.ascontiguousarray(arr)
         t = self._t.from_numpy(a.copy()).to(self.device)
-        self._d.broadcast(t, src=src, group=self._g)
+        gsrc = src if self._g is None else self._d.get_global_rank(self._g, src)
+        self._d.broadcast(t, src=gsrc, group=self._g)
         return t.cpu().numpy().reshape(a.shape)

@@ -94,6 +94,8 @@ struct Model {
   bool own_stream = false;
   DeviceView v{};
   std::vector<void *> allocs;
+  double *d_prm = nullptr;      // {tol, cutoff} of the LPs in flight (DeviceView::prm)
+  double prm_host[2] = {0, 0};
   int32_t *d_slots = nullptr;   // the slots currently iterating (mirror of `act`)
   int32_t *d_new = nullptr;     // slots being initialised by nep_lp_submit
   double *d_base_lb = nullptr, *d_base_ub = nullptr;
@@ -588,6 +590,8 @@ int setup_dense(Model &m, const nep_model_desc &d) {
   if ((rc = dalloc(m, &v.bpart, (size_t)B * v.sbpart))) return rc;
   if ((rc = dalloc(m, &v.npart, (size_t)B * v.snpart))) return rc;
   if ((rc = dalloc(m, &v.ctrl, (size_t)B))) return rc;
+  if ((rc = dalloc(m, &m.d_prm, 2))) return rc;
+  v.prm = m.d_prm;
   if ((rc = dalloc(m, &m.d_slots, (size_t)B))) return rc;
   if ((rc = dalloc(m, &m.d_new, (size_t)B))) return rc;
   {
@@ -606,7 +610,7 @@ int setup_dense(Model &m, const nep_model_desc &d) {
   if ((rc = dalloc(m, &m.d_chg_ub, (size_t)B * v.sint))) return rc;
   HIPCHK(hipMemsetAsync(v.ctrl, 0, sizeof(Ctrl) * B, m.stream));
   HIPCHK(hipMemsetAsync(v.x, 0, sizeof(float) * B * v.sx, m.stream));
-  HIPCHK(hipMemsetAsync(v.xa, 0, sizeof(float) * B * v.sx, m.stream));
+  HIPCHK(hipMemsetAsync(v.xa, 0, sizeof(anchor_t) * B * v.sx, m.stream));
   HIPCHK(hipMemsetAsync(v.theta, 0xFF, sizeof(float) * B * m.R, m.stream));   // NaN: no hint
   HIPCHK(hipMemsetAsync(v.zi, 0, sizeof(double) * B * v.sint, m.stream));
   HIPCHK(hipMemsetAsync(v.y, 0, sizeof(double) * B * v.sdual, m.stream));
@@ -842,10 +846,12 @@ int submit(Model &m, int n, const int32_t *slots, const double *lbi, const doubl
   }
   m.run = o;
   DeviceView &v = m.v;
-  v.tol = o.tol;
   v.warm_omega_floor = o.warm_omega_floor;
-  v.cutoff = o.cutoff;
   v.max_iters = o.max_iters;
+  // tol / cutoff of every LP in flight: device memory, read by the (graph-replayed) blocks
+  m.prm_host[0] = o.tol;
+  m.prm_host[1] = o.cutoff;
+  HIPCHK(hipMemcpyAsync(m.d_prm, m.prm_host, sizeof(m.prm_host), hipMemcpyHostToDevice, m.stream));
   std::vector<int32_t> fresh, off(1, 0), ci;
   std::vector<double> cl, cu;
   const size_t ni = (size_t)m.il.n_int;

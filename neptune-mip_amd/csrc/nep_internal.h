@@ -6,7 +6,7 @@
 //   x     [R][NP] f32   routing rows x̄[r, j]; row r = (function f, source i) or the pooled
 //                       zero-workload sources of f (exact aggregation); the rows of
 //                       one function are consecutive (frow[f] .. frow[f+1])
-//   xa    [R][NP] f32   restart anchor of x
+//   xa    [R][NP] f32   restart anchor of x (anchor_t: f16 when NEP_ANCHOR_F16=1)
 //   mask  [F][NP] u8    destination j allowed for function f at this node (c_ub[f,j] > 0)
 //   zi    [n_int] f64   small primal: c, (mf, mt, a, d), n        + anchor zia, bounds lb/ub
 //   y     [n_dual] f64  duals of the dualised rows   + anchor ya, activity kz (iterate) / kza (anchor)
@@ -20,7 +20,27 @@
 #pragma once
 #include <cstdint>
 
+// Build-time variants (A/B-measured on the MI355X):
+//   NEP_NT          1: the routing-state streams (x, anchor) use non-temporal loads/stores, so the
+//                      once-per-iteration stream does not evict the delay matrix D from the XCD's L2
+//   NEP_ANCHOR_F16  1: the Halpern anchor rows are stored in fp16.  Measured (512x256 bench, r02a):
+//                      certified node LPs fell from 374/384 to 70/384 — the anchor's rounding (5e-4
+//                      relative) re-enters every restart cycle as an O(dist(anchor, fixed set)/k) term,
+//                      so the iterates stall far above the 1e-6 certificate.  Off by default.
+#ifndef NEP_NT
+#define NEP_NT 1
+#endif
+#ifndef NEP_ANCHOR_F16
+#define NEP_ANCHOR_F16 0
+#endif
+
 namespace nep {
+
+#if NEP_ANCHOR_F16
+using anchor_t = _Float16;
+#else
+using anchor_t = float;
+#endif
 
 constexpr int kWave = 64;
 constexpr int kNodeWaves = 16;           // waves per node-pass workgroup (each sums F/16 functions)
@@ -81,7 +101,8 @@ struct DeviceView {
   const float *D, *cpr;
   const double *gam, *rho, *lo, *hi, *rownorm, *cost_int, *mem_f;
   // per slot (base pointers; slot stride below)
-  float *x, *xa;
+  float *x;
+  anchor_t *xa;
   float *theta;                          // [R] last simplex threshold of each routing row (a start hint)
   uint8_t *mask;
   double *zi, *zia, *lb, *ub;
@@ -90,8 +111,10 @@ struct DeviceView {
   double *tpart, *bpart, *npart;
   Ctrl *ctrl;
   int64_t sx, smask, sint, sdual, skty, stpart, sbpart, snpart;   // per-slot strides (elements)
-  // check/solve parameters
-  double tol, cutoff;
+  // check/solve parameters.  tol / cutoff live in device memory (prm[0] / prm[1], written by every
+  // nep_lp_submit) because the iteration blocks are replayed from captured HIP graphs: a value
+  // passed by value would stay frozen at capture time.
+  const double *prm;
   double warm_omega_floor;               // warm starts: primal weight kept >= this x the parent's (0: off)
   int64_t max_iters;
 };

@@ -173,22 +173,60 @@ __device__ __forceinline__ double halpern_lambda(const Ctrl *ctrl, bool halp, in
   return (ks + 1.0) / (ks + 2.0);
 }
 
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef anchor_t anc4 __attribute__((ext_vector_type(4)));
+
 __device__ __forceinline__ float4 ld4(const float *p) { return *reinterpret_cast<const float4 *>(p); }
+// the routing-state streams (x, anchor): read and written once per iteration, so non-temporal
+// (NEP_NT): they then do not push the delay rows D[src, :] — re-read by every row of a function
+// and by every LP slot — out of the XCD's L2
+__device__ __forceinline__ f32x4 ld_x4(const float *p) {
+#if NEP_NT
+  return __builtin_nontemporal_load(reinterpret_cast<const f32x4 *>(p));
+#else
+  return *reinterpret_cast<const f32x4 *>(p);
+#endif
+}
+__device__ __forceinline__ void st_x4(float *p, f32x4 v) {
+#if NEP_NT
+  __builtin_nontemporal_store(v, reinterpret_cast<f32x4 *>(p));
+#else
+  *reinterpret_cast<f32x4 *>(p) = v;
+#endif
+}
+__device__ __forceinline__ anc4 ld_a4(const anchor_t *p) {
+#if NEP_NT
+  return __builtin_nontemporal_load(reinterpret_cast<const anc4 *>(p));
+#else
+  return *reinterpret_cast<const anc4 *>(p);
+#endif
+}
+__device__ __forceinline__ void st_a4(anchor_t *p, anc4 v) {
+#if NEP_NT
+  __builtin_nontemporal_store(v, reinterpret_cast<anc4 *>(p));
+#else
+  *reinterpret_cast<anc4 *>(p) = v;
+#endif
+}
 
 // one routing row's operands: x̄ row, delay row D[src, :] (if the row has delay-weighted
 // coefficients) and the anchor row (if needed)
 template <int CPL>
 __device__ __forceinline__ void load_row(const float *__restrict__ xrow, const float *__restrict__ drow,
-                                         const float *__restrict__ arow, bool nd, bool na, int lane, int NP,
+                                         const anchor_t *__restrict__ arow, bool nd, bool na, int lane, int NP,
                                          float (&xo)[4 * CPL], float (&dout)[4 * CPL], float (&ao)[4 * CPL]) {
 #pragma unroll
   for (int q = 0; q < CPL; ++q) {
     const int j0 = 4 * (lane + kWave * q);
-    float4 a = make_float4(0.f, 0.f, 0.f, 0.f), d = a, an = a;
+    f32x4 a = {0.f, 0.f, 0.f, 0.f}, an = a;
+    float4 d = make_float4(0.f, 0.f, 0.f, 0.f);
     if (j0 < NP) {
-      a = ld4(xrow + j0);
+      a = ld_x4(xrow + j0);
       if (nd) d = ld4(drow + j0);
-      if (na) an = ld4(arow + j0);
+      if (na) {
+        const anc4 h = ld_a4(arow + j0);
+        an = f32x4{(float)h.x, (float)h.y, (float)h.z, (float)h.w};
+      }
     }
     xo[4 * q] = a.x; xo[4 * q + 1] = a.y; xo[4 * q + 2] = a.z; xo[4 * q + 3] = a.w;
     dout[4 * q] = d.x; dout[4 * q + 1] = d.y; dout[4 * q + 2] = d.z; dout[4 * q + 3] = d.w;
@@ -244,7 +282,7 @@ void x_pass(DeviceView v, const int32_t *__restrict__ slots, int first, int plai
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int r0 = v.frow[f], nrows = v.frow[f + 1] - r0;
   float *__restrict__ x = v.x + slot * v.sx;
-  float *__restrict__ xa = v.xa + slot * v.sx;
+  anchor_t *__restrict__ xa = v.xa + slot * v.sx;
   float *__restrict__ th_row = v.theta + (int64_t)slot * v.R;   // per-row simplex thresholds (hints)
   const uint8_t *__restrict__ mask = v.mask + slot * v.smask + (int64_t)f * NP;
   float *__restrict__ kty = v.kty + slot * v.skty;
@@ -254,10 +292,20 @@ void x_pass(DeviceView v, const int32_t *__restrict__ slots, int first, int plai
   // column accumulators (C1/C2 column sums, C5 W-weighted sums) live in LDS, not in registers:
   // 32 fewer VGPRs per lane at CPL = 2, i.e. more waves per SIMD to keep HBM reads in flight.
   float *lS = lds, *lW = lds + TW * NP, *lK = lds + 2 * TW * NP, *lC = lK + NP;
+  // certificate iterations: the same constants in fp64 from the fp64 duals, so the Lagrangian bound
+  // carries no fp32 rounding of y (|y1| can be large against the big-M rows)
+  double *lKd = reinterpret_cast<double *>(lds + (2 * TW + 2) * NP), *lCd = lKd + NP;
   for (int j = threadIdx.x; j < NP; j += kWave * TW) {
     lK[j] = kty[(int64_t)f * NP + j];
     lC[j] = v.cpr[(int64_t)f * NP + j] * kty[(int64_t)F * NP + j];
+    if (CHECK) {
+      const double *yv = v.y + slot * v.sdual;
+      const bool in = j < N;
+      lKd[j] = in ? yv[v.dl.o1 + f * N + j] + yv[v.dl.o2 + f * N + j] : 0.0;
+      lCd[j] = in ? (double)v.cpr[(int64_t)f * NP + j] * yv[v.dl.o5 + j] : 0.0;
+    }
   }
+  const double ysd = (CHECK && v.step2) ? v.y[slot * v.sdual + v.dl.oS] : 0.0;
   uint32_t mbits = 0;
 #pragma unroll
   for (int q = 0; q < CPL; ++q) {
@@ -317,8 +365,8 @@ void x_pass(DeviceView v, const int32_t *__restrict__ slots, int first, int plai
 #pragma unroll
       for (int e = 0; e < E; ++e) {
         if ((mbits >> e) & 1u) {
-          const double g = (double)wobj * dc[e] -
-                           ((double)m * kx[e] + (double)w * cy5[e] + (double)wsc * (double)ys * dc[e]);
+          const int j = 4 * (lane + kWave * (e / 4)) + (e & 3);
+          const double g = (double)wobj * dc[e] - ((double)m * lKd[j] + (double)w * lCd[j] + (double)wsc * ysd * dc[e]);
           gmin = fmin(gmin, g);
         }
       }
@@ -403,7 +451,7 @@ void x_pass(DeviceView v, const int32_t *__restrict__ slots, int first, int plai
       s_dist += dd;
     }
     float *xrow = x + (int64_t)r * NP;
-    float *arow = xa + (int64_t)r * NP;
+    anchor_t *arow = xa + (int64_t)r * NP;
 #pragma unroll
     for (int q = 0; q < CPL; ++q) {
       const int j0 = 4 * (lane + kWave * q);
@@ -414,10 +462,10 @@ void x_pass(DeviceView v, const int32_t *__restrict__ slots, int first, int plai
           const int e = 4 * q + t;
           o[t] = halp ? lam * (2.f * xn[e] - xc[e]) + (1.f - lam) * xav[e] : xn[e];
         }
-        *reinterpret_cast<float4 *>(xrow + j0) = make_float4(o[0], o[1], o[2], o[3]);
+        st_x4(xrow + j0, f32x4{o[0], o[1], o[2], o[3]});
         if (restart)
-          *reinterpret_cast<float4 *>(arow + j0) =
-              make_float4(xav[4 * q], xav[4 * q + 1], xav[4 * q + 2], xav[4 * q + 3]);
+          st_a4(arow + j0, anc4{(anchor_t)xav[4 * q], (anchor_t)xav[4 * q + 1], (anchor_t)xav[4 * q + 2],
+                                (anchor_t)xav[4 * q + 3]});
       }
     }
     float sc = 0.f;
@@ -739,10 +787,11 @@ __global__ __launch_bounds__(256) void scalar_pass(DeviceView v, const int32_t *
   if (lagr > ctrl->best_lagr) ctrl->best_lagr = lagr;
   ctrl->pres = res;
   ctrl->gap = gap;
-  if (isfinite(lagr) && res <= v.tol && gap <= v.tol * fmax(1.0, fabs(lagr))) {
+  const double tol = v.prm[0], cutoff = v.prm[1];
+  if (isfinite(lagr) && res <= tol && gap <= tol * fmax(1.0, fabs(lagr))) {
     ctrl->status = 0; ctrl->active = 0; return;
   }
-  if (ctrl->best_lagr > v.cutoff) { ctrl->status = 3; ctrl->active = 0; return; }
+  if (ctrl->best_lagr > cutoff) { ctrl->status = 3; ctrl->active = 0; return; }
   if (ctrl->k >= ctrl->max_iters) { ctrl->status = 1; ctrl->active = 0; return; }
   if (!isfinite(pobj) || !isfinite(a.mvz) || !isfinite(a.mvy)) { ctrl->status = 4; ctrl->active = 0; return; }
 
@@ -857,7 +906,7 @@ template <int CPL, int TW>
 static hipError_t launch_x_tw(const DeviceView &v, const int32_t *slots, int nslots, bool check, bool init,
                               bool first, bool plain, int it, hipStream_t s) {
   dim3 grid(8 * ((v.F * nslots + 7) / 8)), block(kWave * TW);
-  const size_t lds = (size_t)(2 * TW + 2) * v.NP * sizeof(float);
+  const size_t lds = (size_t)(2 * TW + 2) * v.NP * sizeof(float) + (check ? 2 * v.NP * sizeof(double) : 0);
   const int fi = first ? 1 : 0, pl = plain ? 1 : 0;
   if (init) hipLaunchKernelGGL((x_pass<CPL, false, true, TW>), grid, block, lds, s, v, slots, fi, pl, it, nslots);
   else if (check)
@@ -874,7 +923,7 @@ static hipError_t launch_x_tw(const DeviceView &v, const int32_t *slots, int nsl
 static int tile_waves(const DeviceView &v, int nslots) {
   int tw = 4;
   while (tw < 16 && (int64_t)nslots * v.F * tw < 4096) tw *= 2;
-  while (tw > 4 && (size_t)(2 * tw + 2) * v.NP * sizeof(float) > 128 * 1024) tw /= 2;
+  while (tw > 4 && (size_t)(2 * tw + 2) * v.NP * sizeof(float) + 2 * v.NP * sizeof(double) > 128 * 1024) tw /= 2;
   return tw;
 }
 

@@ -1,0 +1,113 @@
+"""GPU parity at the BASELINE.json sizes.
+
+1. tests/golden/scale.json (HiGHS on the reference formulation, tools/gen_scale_golden.py): the root LP
+   and seeded B&B-node LPs of
+     * the §8(d) synthetic generator at 64x32 (config 2), 128x64 and 256x128 (config 3);
+     * the reference's Alibaba 100x25 trace case (W == 0: the R = F aggregation path), all three variants,
+       and its step-2 create model at the published step-1 scores;
+   solved as the B&B does: root first, then every node warm-started from the root's state.  Every LP
+   must certify (NEP_LP_OPTIMAL) with |obj - HiGHS| <= 1e-6 * max(1, |HiGHS|); a node HiGHS proves
+   infeasible must not be reported optimal.
+2. Full-size root LPs no CPU reference can solve here (512x256: 67 M columns; the Alibaba-shape
+   1024x512): certified, and the engine's solution re-checked on the host in fp64 against every
+   reference row family (scale_util.check_step1_solution), its objective recomputed from x and z.
+"""
+import numpy as np
+import pytest
+
+from scale_util import case_model_args, check_step1_solution, gap, node_bounds, scale_cases
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-6
+CASES = scale_cases()
+
+
+def _solve_case(c, tol=TOL):
+    from core.engine.lp import LPModel
+    data, variant, step, kw = case_model_args(c)
+    B = len(c["nodes"])
+    m = LPModel(data, variant, step=step, max_batch=B + 1, **kw)
+    root = B
+    rr = m.solve([root], tol=tol, max_iters=400000)
+    lb, ub = node_bounds(c, m.n_int)
+    for b in range(B):
+        m.copy_state(root, b)
+    res = m.solve(np.arange(B), lb, ub, tol=tol, max_iters=200000, warm_start=True)
+    return m, rr, res
+
+
+@pytest.mark.parametrize("name", sorted(CASES))
+def test_scale_parity(name):
+    from core.engine.lp import LP_OPTIMAL
+    c = CASES[name]
+    m, rr, res = _solve_case(c)
+    try:
+        ref = c["root"]["lp_objective"]
+        assert int(rr["status"][0]) == LP_OPTIMAL, f"root: status {rr['status'][0]} after {rr['iters'][0]} iterations"
+        assert gap(float(rr["obj"][0]), ref) <= TOL, f"root: {rr['obj'][0]} vs HiGHS {ref}"
+        for b, nd in enumerate(c["nodes"]):
+            st, obj = int(res["status"][b]), float(res["obj"][b])
+            if nd["lp_objective"] is None:
+                assert st != LP_OPTIMAL, f"node {b}: HiGHS infeasible, engine optimal {obj}"
+                continue
+            assert st == LP_OPTIMAL, f"node {b}: status {st} after {res['iters'][b]} iterations (HiGHS {nd['lp_objective']})"
+            assert gap(obj, nd["lp_objective"]) <= TOL, f"node {b}: {obj} vs HiGHS {nd['lp_objective']}"
+        print(f"{name}: root {rr['iters'][0]} iterations, nodes {res['iters'].tolist()}")
+    finally:
+        m.close()
+
+
+def _full_size_check(payload, variant, fixings=0, seed=0):
+    from core.engine.lp import LPModel, LP_OPTIMAL
+    from core.utils import data_to_solver_input
+    data = data_to_solver_input(payload, with_db=False)
+    alpha = payload["solver"]["args"]["alpha"]
+    F, N = data.workload_matrix.shape
+    B = 1 + fixings
+    m = LPModel(data, variant, step=1, alpha=alpha, max_batch=B)
+    try:
+        rr = m.solve([0], tol=TOL, max_iters=400000)
+        assert int(rr["status"][0]) == LP_OPTIMAL, f"root: status {rr['status'][0]} after {rr['iters'][0]}"
+        boxes = [(None, None)]
+        if fixings:
+            rng = np.random.default_rng(seed)
+            lb = np.full((fixings, m.n_int), -np.inf)
+            ub = np.full((fixings, m.n_int), np.inf)
+            for b in range(fixings):
+                idx = rng.choice(F * N, size=2, replace=False)
+                lb[b, idx] = ub[b, idx] = rng.integers(0, 2, size=2)
+                m.copy_state(0, b + 1)
+            r2 = m.solve(np.arange(1, B), lb, ub, tol=TOL, max_iters=20000, warm_start=True)
+            boxes += [(lb[b], ub[b]) for b in range(fixings)]
+        for b in range(B):
+            st = int(rr["status"][0]) if b == 0 else int(r2["status"][b - 1])
+            if st != LP_OPTIMAL:
+                continue
+            obj = float(rr["obj"][0]) if b == 0 else float(r2["obj"][b - 1])
+            pobj = float(rr["primal_obj"][0]) if b == 0 else float(r2["primal_obj"][b - 1])
+            xb, rf, rs = m.rows(b)
+            z, _ = m.solution(b, dense_x=False)
+            viol, worst, hobj = check_step1_solution(data, variant, alpha, xb, rf, rs, z, *boxes[b])
+            assert obj <= pobj + 1e-12, (obj, pobj)
+            assert pobj - obj <= TOL * max(1.0, abs(obj)), (obj, pobj)
+            assert viol["C4"] <= 2e-5, viol
+            assert worst <= 1e-5, viol
+            assert abs(hobj - pobj) <= 1e-6 * max(1.0, abs(pobj)), (hobj, pobj)
+        return rr
+    finally:
+        m.close()
+
+
+def test_full_size_512x256_root_and_children():
+    """BASELINE config 4's instance (512x256, §8(d) generator, seed 0): root + 4 warm children."""
+    from core.utils.synthetic import synthetic_payload
+    rr = _full_size_check(synthetic_payload(512, 256, seed=0), "MinDelayAndUtilization", fixings=4)
+    print("512x256 root iterations", rr["iters"][0], "obj", rr["obj"][0])
+
+
+@pytest.mark.parametrize("variant", ["MinDelayAndUtilization", "MinUtilization", "MinDelay"])
+def test_full_size_alibaba_1024x512(variant):
+    """BASELINE config 5's shape (Alibaba trace: W == 0, D = 1 - I, R = F aggregated rows): root + children."""
+    from core.utils.synthetic import alibaba_payload
+    rr = _full_size_check(alibaba_payload(1024, 512, seed=0), variant, fixings=4, seed=1)
+    print("1024x512", variant, "root iterations", rr["iters"][0], "obj", rr["obj"][0])
