@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define NEP_API_VERSION 3
+#define NEP_API_VERSION 4
 
 /* variants: neptune.py:41-66 (NeptuneMinDelay / MinUtilization / MinDelayAndUtilization) */
 enum { NEP_MIN_DELAY = 0, NEP_MIN_UTILIZATION = 1, NEP_MIN_DELAY_AND_UTILIZATION = 2 };
@@ -136,6 +136,42 @@ int nep_lp_get_solution(void *model, int32_t slot, double *z_int, float *x_dense
 int nep_lp_get_rows(void *model, int32_t slot, float *xbar, int32_t *row_f, int32_t *row_src);
 /* copy a slot's primal/dual state to another (not iterating) slot: warm start of a child node */
 int nep_lp_copy_state(void *model, int32_t src_slot, int32_t dst_slot);
+
+/* tol / cutoff of every LP in flight, effective from the next iteration block (a B&B lowers the
+ * cutoff to each new incumbent without resubmitting). */
+int nep_lp_set_params(void *model, double tol, double cutoff);
+
+/* flow[b][f][j] = sum_i x[i,f,j] of finished slots (host float, n x F x N), computed on the device:
+ * the branch-and-bound's branching / rounding input (replaces copying the R x N routing rows). */
+int nep_lp_get_flows(void *model, int32_t n, const int32_t *slots, float *flows);
+
+/* Wire format on the device (neptune/utils/output.py:23-39).  Routing entries of the aggregated rows
+ * with x > threshold (0.001), value rounded as np.round(x, 3) when round3; allocation entries c[f,j] >
+ * threshold.  Row-major order.  Call with capacity 0 (or too small) to get *n_entries only; the row
+ * map of nep_lp_get_rows expands a pooled row (src = -1) to all zero-workload sources of its f. */
+int nep_lp_routing_entries(void *model, int32_t slot, double threshold, int32_t round3, int64_t capacity,
+                           int64_t *n_entries, int32_t *row, int32_t *dst, double *val);
+int nep_lp_allocation_entries(void *model, int32_t slot, double threshold, int64_t capacity, int64_t *n_entries,
+                              int32_t *fn, int32_t *dst);
+
+/* The reference's offline scorers and feasibility checkers on a slot's solution, on the device
+ * (efttc/utils/objectives.py:23-98, efttc/utils/constraints_step1.py:5-133; booleans are the
+ * reference's truthiness, value != 0).  out[NEP_SC_COUNT]: */
+enum {
+  NEP_SC_NETWORK_DELAY = 0,   /* score_minimize_network_delay: sum W[f,i] D[i,j] x[i,f,j] */
+  NEP_SC_NODES_USED = 1,      /* score_minimize_node_utilization: #{j : n[j] != 0} */
+  NEP_SC_NODE_COST = 2,       /* sum n[j] cost[j] (constrain_budget) */
+  NEP_SC_BAD_C_X = 3,         /* constrain_c_according_to_x violations (f, j) */
+  NEP_SC_BAD_MEMORY = 4,      /* constrain_memory_usage violations (nodes) */
+  NEP_SC_BAD_HANDLE = 5,      /* constrain_handle_all_requests: (i, f) with |sum_j x - 1| >= 0.1 */
+  NEP_SC_BAD_CPU = 6,         /* constrain_CPU_usage violations (nodes, + 1e-6) */
+  NEP_SC_BAD_N_C = 7,         /* constrain_n_according_to_c violations (nodes) */
+  NEP_SC_BAD_BUDGET = 8,      /* constrain_budget (0 / 1) */
+  NEP_SC_HANDLE_MAXDEV = 9,   /* max |sum_j x - 1| */
+  NEP_SC_CPU_MAXEXCESS = 10,  /* max (CPU use - cores, 0) */
+  NEP_SC_COUNT = 11
+};
+int nep_lp_score_check(void *model, int32_t slot, double *out);
 
 int nep_get_stats(void *model, nep_stats *stats);
 

@@ -1,39 +1,43 @@
-"""Batched best-first branch-and-bound over the MI355X LP engine.
+"""Streaming best-first branch-and-bound over the MI355X LP engine.
 
 This is the tree search SCIP runs inside `pywraplp.Solver.Solve()` (reference
-`core/solvers/solver.py:35-40`) on the NEPTUNE step models, rebuilt around batched GPU LP
-relaxations: open nodes, heuristic completions and leaves are all LPs solved by `LPModel.solve`
-(nep_lp_solve_batch), up to `batch` of them per call.  The host keeps only the tree.
+`core/solvers/solver.py:35-40`) on the NEPTUNE step models, rebuilt around the engine's streaming
+node-LP API (`nep_lp_submit` / `nep_lp_advance`, include/neptune_lp.h): up to `batch` node LPs
+iterate on the device at once and a slot whose LP finishes takes the next open node at once, so no
+slot waits for the slowest LP of a batch.  Per finished node only small results cross PCIe: its
+status / bound, and the per-(function, destination) flows reduced on the device
+(`nep_lp_get_flows`, F x N floats) — the host keeps only the tree.
 
 Branching variables: the placement binaries c[f,j] and the node binaries n[j] of the engine's
-integer vector (include/neptune_lp.h).  moved_from / moved_to / allocated / deallocated follow
-from c — with c integral their LP optimum is integral — and are never branched on.
-
-Multi-GPU: with a communicator (`core/engine/comm.py`, one rank per GPU) every
-rank runs the same search redundantly until the open-node frontier holds `world * batch` nodes,
-then keeps the frontier nodes whose canonical position is its rank modulo `world` and searches
-those subtrees alone.  Per batch the ranks exchange the incumbent value (all-reduce MIN, 8 B) and
-their open-node counts (all-reduce SUM, termination); at the end the owner of the best incumbent
-(lowest rank on ties) broadcasts its placement.  No collective runs inside an LP.
-
-Warm starts: with `lp.max_batch >= 2 * batch + 1` (and an engine with nep_lp_copy_state) every
-node LP after the root starts from its parent's final PDHG state when the parent is still resident
-— batches alternate between the two halves of the slots, so the previous batch's nodes (the
-parents of the children best-first pops next) stay on the device — else from the root's state,
-kept in the last slot (SCIP warm-starts its node LPs from the parent basis the same way).  The
-engine floors a warm-started LP's primal weight at 2x the parent's.
+integer vector.  moved_from / moved_to / allocated / deallocated follow from c — with c integral
+their LP optimum is integral — and are never branched on.
 
 Exactness:
-  * a node's value is the engine's certified Lagrangian bound, a valid lower bound even when PDHG
-    stopped at its iteration limit, so pruning never discards the optimum;
-  * an incumbent is only ever a *leaf* — every c and n fixed — whose LP the engine certified
-    optimal; with c and n fixed, that LP's optimum is the MIP objective of the placement;
-  * the search ends with the queue empty: the incumbent is optimal within `gap` (relative).
+  * a node's value is the engine's Lagrangian bound, a valid lower bound even when its LP stopped
+    at the iteration limit, so pruning never discards the optimum;
+  * an incumbent is only a *leaf* (every c and n fixed) whose LP the engine certified: the
+    certificate's repaired primal point is feasible, so its value is attained;
+  * a leaf whose LP stops uncertified is re-solved once with the root's iteration budget; if it
+    still does not certify its bound stays in `res.bound` and the search reports LIMIT (never
+    OPTIMAL or INFEASIBLE) while that bound is below the incumbent;
+  * the search ends with no open node: the incumbent is optimal within `gap` (relative).
+
+Warm starts: every node LP after the root starts from its parent's final PDHG state when the
+parent's slot still holds it (slots are reused least-recently-finished first), else from the
+root's, kept in a reserved slot (SCIP warm-starts its node LPs from the parent basis the same way).
+
+Multi-GPU (core/engine/comm.py, one rank per GPU): every rank runs the same search
+redundantly until the open-node frontier holds `world * batch` nodes, then keeps the frontier nodes
+whose canonical position is its rank modulo `world` and searches those subtrees alone.  Every loop
+the ranks agree (all-reduce) on the incumbent value (MIN), on stopping (time / node limit of ANY rank)
+and on termination (open + in-flight node count, SUM); at the end the owner of the best incumbent
+(lowest rank on ties) broadcasts its placement.  No collective runs inside an LP.
 """
 import heapq
 import itertools
 import math
 import time
+from collections import deque
 
 import numpy as np
 
@@ -41,6 +45,7 @@ from .comm import LocalComm
 from .lp import LP_CUTOFF, LP_INFEASIBLE, LP_OPTIMAL
 
 OPTIMAL, INFEASIBLE, LIMIT = "OPTIMAL", "INFEASIBLE", "LIMIT"
+NODE, LEAF, RETRY = 0, 1, 2
 
 
 class BnBResult:
@@ -50,251 +55,311 @@ class BnBResult:
         self.status = INFEASIBLE
         self.objective = None
         self.z = None            # engine integer vector of the incumbent
-        self.x = None            # routing x[i][f][j] of the incumbent (float32)
+        self.x = None            # routing x[i][f][j] of the incumbent (float32; fetched once, at the end)
         self.bound = -math.inf   # best proven lower bound
-        self.nodes = 0
+        self.nodes = 0           # branched (non-leaf) nodes whose LP finished
         self.leaves = 0
-        self.lps = 0
+        self.lps = 0             # node LPs submitted (presolve-infeasible ones included)
+        self.certified = 0       # node LPs the engine certified optimal
         self.lp_iterations = 0
-        self.unresolved = 0      # leaves whose LP hit the iteration limit (not used as incumbents)
+        self.unresolved = 0      # leaves still uncertified after their retry
         self.seconds = 0.0
+        self.incumbent_slot = None
 
     def as_dict(self):
-        return {k: getattr(self, k) for k in ("status", "objective", "bound", "nodes", "leaves", "lps",
+        return {k: getattr(self, k) for k in ("status", "objective", "bound", "nodes", "leaves", "lps", "certified",
                                               "lp_iterations", "unresolved", "seconds")}
 
 
-class BranchAndBound:
-    """Best-first B&B with batched node LPs.
+class _Node:
+    __slots__ = ("bound", "idx", "val", "kind", "parent", "depth")
 
-    lp            core.engine.lp.LPModel of the step model (max_batch >= batch)
-    workload      W [F, N] (to weigh the pooled zero-workload routing rows when computing flows)
+    def __init__(self, bound, idx, val, kind, parent, depth):
+        self.bound, self.idx, self.val, self.kind, self.parent, self.depth = bound, idx, val, kind, parent, depth
+
+
+class BranchAndBound:
+    """Streaming best-first B&B.
+
+    lp            core.engine.lp.LPModel of the step model (max_batch >= batch + 2: `batch` working
+                  slots, one for the root's state, one for the incumbent's)
+    workload      W [F, N] (unused since the flows are reduced on the device; kept for the API)
     fn_mem/node_mem  memory data for the rounding heuristic's capacity check (C3)
-    upper_bound   a-priori bound on any feasible objective: LPs whose Lagrangian exceeds it are
-                  stopped early (infeasible nodes have an unbounded Lagrangian)
+    upper_bound   a-priori bound on any feasible objective: LPs whose Lagrangian exceeds it stop early
     """
 
     def __init__(self, lp, workload, fn_mem, node_mem, batch=16, tol=1e-7, gap=1e-6, max_iters=5000,
                  node_limit=20000, time_limit=None, upper_bound=math.inf, flow_tol=1e-4, log=None, comm=None,
-                 warm=True, root_max_iters=200000):
+                 warm=True, root_max_iters=200000, check_every=16):
         self.lp = lp
         self.N, self.F = lp.N, lp.F
         L = lp.layout()
         self.c0, self.c1 = L["c"]
         self.n_range = L["n"]
-        W = np.asarray(workload, np.float64).reshape(self.F, self.N)
-        self.zero_src = (W == 0).sum(axis=1).astype(np.float64)
         self.fn_mem = np.asarray(fn_mem, np.float64).reshape(self.F)
         self.node_mem = np.asarray(node_mem, np.float64).reshape(self.N)
-        self.batch = min(int(batch), lp.max_batch)
-        self.warm = bool(warm) and hasattr(lp, "copy_state") and lp.max_batch >= 2 * self.batch + 1
+        self.reserved = 2 if lp.max_batch >= 3 else 0
+        self.batch = max(1, min(int(batch), lp.max_batch - self.reserved))
+        self.warm = bool(warm) and self.reserved == 2
         self.root_slot = lp.max_batch - 1
-        self.slot_gen = [0] * lp.max_batch     # bumped whenever a slot takes a new LP
-        # node LPs stop at max_iters (their Lagrangian bound stays valid for pruning; a leaf only
-        # becomes an incumbent when certified); the root, solved cold, gets root_max_iters
+        self.inc_slot = lp.max_batch - 2
         self.tol, self.gap, self.max_iters = tol, gap, max_iters
         self.root_max_iters = max(max_iters, root_max_iters)
+        self.check_every = check_every
         self.node_limit, self.time_limit = node_limit, time_limit
         self.ub0 = upper_bound
         self.flow_tol = flow_tol
         self.log = log or (lambda *_: None)
         self.comm = comm or LocalComm()
-        self.branch_vars = list(range(self.c0, self.c1))
-        if self.n_range is not None:
-            self.branch_vars += list(range(*self.n_range))
-        self._nb = len(self.branch_vars)
+        nb = self.c1 - self.c0 + (0 if self.n_range is None else self.n_range[1] - self.n_range[0])
+        self._nb = nb
 
     # ---------------------------------------------------------------------------------------
     def _gap_abs(self, inc):
         return self.gap * max(1.0, abs(inc)) if math.isfinite(inc) else 0.0
 
-    def _flows(self, slot):
-        """flow[f, j] = sum over sources of x[i, f, j] (pooled rows weighted by their size)."""
-        xb, rf, rs = self.lp.rows(slot)
-        w = np.where(rs >= 0, 1.0, self.zero_src[rf])
-        flow = np.zeros((self.F, self.N))
-        np.add.at(flow, rf, w[:, None] * xb.astype(np.float64))
-        return flow
+    def _fixed(self, node):
+        fx = np.zeros(self.lp.n_int, bool)
+        fx[node.idx] = True
+        return fx
 
-    def _complete(self, fix):
-        return len(fix) >= self._nb
-
-    def _round(self, fix, flow):
-        """Heuristic completion of a node: c = 1 where fixed to 1 or carrying flow, n = any c.
-        Returns a full fixing dict, or None when it is visibly infeasible."""
-        F, N, c0 = self.F, self.N, self.c0
-        c = np.zeros(F * N)
-        free = np.ones(F * N, bool)
-        for k, v in fix.items():
-            if c0 <= k < self.c1:
-                c[k - c0] = v
-                free[k - c0] = False
-        c[free & (flow.ravel() > self.flow_tol)] = 1.0
+    def _round(self, node, flow):
+        """Heuristic completion of a node: c = fixed value, else 1 where it carries flow; n = any c.
+        Returns (idx, val) arrays fixing every c and n, or None when visibly infeasible."""
+        F, N, c0, c1 = self.F, self.N, self.c0, self.c1
+        c = (flow.ravel() > self.flow_tol).astype(np.float64)
+        sel = (node.idx >= c0) & (node.idx < c1)
+        c[node.idx[sel] - c0] = node.val[sel]
         cm = c.reshape(F, N)
         if (cm.sum(axis=1) < 1).any():
             return None
         if ((self.fn_mem[:, None] * cm).sum(axis=0) > self.node_mem + 1e-9).any():
             return None
-        leaf = {c0 + k: float(c[k]) for k in range(F * N)}
+        idx = [np.arange(c0, c1)]
+        val = [c]
         if self.n_range is not None:
-            n0 = self.n_range[0]
+            n0, n1 = self.n_range
             nv = (cm.sum(axis=0) >= 1).astype(np.float64)
-            for j in range(N):
-                if fix.get(n0 + j, nv[j]) != nv[j]:
-                    return None
-                leaf[n0 + j] = float(nv[j])
-        return leaf
+            seln = (node.idx >= n0) & (node.idx < n1)
+            if (nv[node.idx[seln] - n0] != node.val[seln]).any():
+                return None
+            idx.append(np.arange(n0, n1))
+            val.append(nv)
+        return np.concatenate(idx), np.concatenate(val)
 
-    def _branch_var(self, fix, z, flow):
+    def _branch_var(self, node, flow, slot):
         """n[j] receiving flow (largest inflow), then c[f,j] carrying flow (largest), then any free
-        n / c by LP value.  None when every branching variable is fixed."""
-        F, N, c0 = self.F, self.N, self.c0
+        n / c by LP value (ties: lowest index).  None when every branching variable is fixed."""
+        fixed = self._fixed(node)
         if self.n_range is not None:
-            n0 = self.n_range[0]
-            inflow = flow.sum(axis=0)
-            cand = [j for j in range(N) if (n0 + j) not in fix and inflow[j] > self.flow_tol]
-            if cand:
-                return n0 + max(cand, key=lambda j: (inflow[j], -j))
-        fl = flow.ravel()
-        cand = [k for k in range(F * N) if (c0 + k) not in fix and fl[k] > self.flow_tol]
-        if cand:
-            return c0 + max(cand, key=lambda k: (fl[k], -k))
-        free = [v for v in self.branch_vars if v not in fix]
-        if not free:
+            n0, n1 = self.n_range
+            inflow = flow.sum(axis=0).astype(np.float64)
+            cand = np.flatnonzero(~fixed[n0:n1] & (inflow > self.flow_tol))
+            if cand.size:
+                return n0 + int(cand[np.argmax(inflow[cand])])
+        fl = flow.ravel().astype(np.float64)
+        cand = np.flatnonzero(~fixed[self.c0:self.c1] & (fl > self.flow_tol))
+        if cand.size:
+            return self.c0 + int(cand[np.argmax(fl[cand])])
+        free = np.flatnonzero(~fixed[self.c0:self.c1]) + self.c0
+        if self.n_range is not None:
+            free = np.concatenate([free, np.flatnonzero(~fixed[self.n_range[0]:self.n_range[1]]) + self.n_range[0]])
+        if free.size == 0:
             return None
-        return max(free, key=lambda v: (z[v], -v))
+        z, _ = self.lp.solution(slot, dense_x=False)
+        zf = z[free]
+        return int(free[np.argmax(zf)])
 
-    def _place(self, batch, half, root_ready):
-        """Slots of this batch's LPs and whether they start warm.  Cold: slots 0..B-1.  Warm: the
-        half of the slots the previous batch did not use; each LP starts from its parent's state if
-        that is still resident in the other half, else from the root's."""
-        B = len(batch)
-        if not (self.warm and root_ready):
-            slots = np.arange(B, dtype=np.int32)
-            for s in slots:
-                self.slot_gen[s] += 1
-            return slots, False
-        base = half * self.batch
-        slots = np.arange(base, base + B, dtype=np.int32)
-        for b, (_, _, _, pref) in enumerate(batch):
-            src = self.root_slot
-            if pref is not None:
-                ps, pg = pref
-                if self.slot_gen[ps] == pg and not (base <= ps < base + self.batch):
-                    src = ps
-            self.lp.copy_state(src, int(slots[b]))
-        for s in slots:
-            self.slot_gen[s] += 1
-        return slots, True
+    # ---------------------------------------------------------------------------------------
+    def _submit(self, items, inc):
+        """items: [(slot, node)].  One nep_lp_submit per (warm, iteration budget) group."""
+        lp, n_int = self.lp, self.lp.n_int
+        groups = {}
+        copies = []
+        for slot, node in items:
+            warm = False
+            if self.warm and self.root_ready:
+                src = self.root_slot
+                if node.parent is not None:
+                    ps, pg = node.parent
+                    if self.slot_gen[ps] == pg:
+                        src = ps
+                if src != slot:
+                    copies.append((src, slot))
+                warm = True
+            budget = self.root_max_iters if (node.kind == RETRY or not self.root_ready) else self.max_iters
+            groups.setdefault((warm, budget), []).append((slot, node))
+        # warm-start copies: a slot that is both a parent state (source) and a new node's slot
+        # (destination) is read before it is overwritten; a cycle falls back to the root's state
+        while copies:
+            srcs = {c[0] for c in copies}
+            k = next((i for i, (_, d) in enumerate(copies) if d not in srcs), None)
+            if k is None:
+                src, dst = copies[0]
+                copies[0] = (self.root_slot, dst)
+                continue
+            src, dst = copies.pop(k)
+            lp.copy_state(src, dst)
+        cutoff = min(inc, self.ub0)
+        for (warm, budget), its in groups.items():
+            slots = np.array([s for s, _ in its], np.int32)
+            lb = np.full((len(its), n_int), -np.inf)
+            ub = np.full((len(its), n_int), np.inf)
+            for b, (_, node) in enumerate(its):
+                lb[b, node.idx] = node.val
+                ub[b, node.idx] = node.val
+            st = lp.submit(slots, lb, ub, tol=self.tol, cutoff=cutoff if math.isfinite(cutoff) else math.inf,
+                           max_iters=budget, check_every=self.check_every, warm_start=warm)
+            for b, (slot, node) in enumerate(its):
+                self.slot_gen[slot] += 1
+                self.res.lps += 1
+                if int(st[b]) == LP_INFEASIBLE:
+                    self.free.append(slot)
+                else:
+                    self.inflight[slot] = node
+
+    def _finish(self, slot, node, st, obj, pobj, iters, inc):
+        """Process one finished node LP; returns the (possibly improved) incumbent value."""
+        res = self.res
+        res.lp_iterations += iters
+        if st == LP_OPTIMAL:
+            res.certified += 1
+        if not self.root_ready and node.depth == 0 and node.kind == NODE:
+            if self.warm and st not in (LP_INFEASIBLE, LP_CUTOFF):
+                self.lp.copy_state(slot, self.root_slot)   # every later node can start from the root
+            self.root_ready = True
+        if st in (LP_INFEASIBLE, LP_CUTOFF):
+            self.free.append(slot)
+            return inc
+        bound = max(node.bound, obj)
+        if node.kind != NODE:
+            res.leaves += 1
+            if st == LP_OPTIMAL:
+                if pobj < inc - self._gap_abs(inc):
+                    inc = pobj
+                    res.objective = pobj
+                    res.z, _ = self.lp.solution(slot, dense_x=False)
+                    if self.warm:
+                        self.lp.copy_state(slot, self.inc_slot)   # its x is fetched once, at the end
+                        res.incumbent_slot = self.inc_slot
+                    else:
+                        if res.incumbent_slot is not None and res.incumbent_slot in self.keep:
+                            self.keep.discard(res.incumbent_slot)
+                            self.free.append(res.incumbent_slot)
+                        res.incumbent_slot = slot
+                        self.keep.add(slot)
+                    self.lp.set_params(self.tol, min(inc, self.ub0))
+                    self.log(f"incumbent {pobj:.10g} (lps {res.lps}, nodes {res.nodes})")
+            elif node.kind == LEAF:
+                self.retry.append(_Node(bound, node.idx, node.val, RETRY, (slot, self.slot_gen[slot]), node.depth))
+            else:
+                res.unresolved += 1
+                self.unresolved_bounds.append(bound)
+            if slot not in self.keep:
+                self.free.append(slot)
+            return inc
+        if bound >= inc - self._gap_abs(inc):
+            self.free.append(slot)
+            return inc
+        res.nodes += 1
+        flow = self.lp.flows([slot])[0]
+        me = (slot, self.slot_gen[slot])
+        leaf = self._round(node, flow)
+        if leaf is not None:
+            key = np.packbits(leaf[1] > 0.5).tobytes()
+            if key not in self.seen_leaves:
+                self.seen_leaves.add(key)
+                self.pending.append(_Node(bound, leaf[0], leaf[1], LEAF, me, node.depth + 1))
+        var = self._branch_var(node, flow, slot)
+        if var is not None:
+            for v in (1.0, 0.0):
+                idx = np.append(node.idx, var)
+                val = np.append(node.val, v)
+                kind = LEAF if len(idx) >= self._nb else NODE
+                heapq.heappush(self.heap, (bound, -(node.depth + 1), next(self.seq),
+                                           _Node(bound, idx, val, kind, me, node.depth + 1)))
+        self.free.append(slot)        # most recently finished last: its state survives longest
+        return inc
 
     # ---------------------------------------------------------------------------------------
     def solve(self):
         t0 = time.time()
-        res = BnBResult()
-        lp, n_int = self.lp, self.lp.n_int
-        inc = math.inf
-        seq = itertools.count()
-        # (bound, -depth, seq, fixings, is_leaf, parent) with parent = (slot, generation) or None
-        heap = [(-math.inf, 0, next(seq), {}, False, None)]
-        pending_leaves = []                              # (fixings, parent)
-        half = 0
-        root_ready = False
-        seen_leaves = set()
-        limit_hit = False
+        self.res = res = BnBResult()
+        lp = self.lp
         comm = self.comm
+        inc = math.inf
+        self.seq = itertools.count()
+        self.heap = [(-math.inf, 0, next(self.seq), _Node(-math.inf, np.zeros(0, np.int64), np.zeros(0), NODE, None, 0))]
+        self.pending = deque()       # rounding leaves
+        self.retry = deque()         # uncertified leaves, re-solved once with the root budget
+        self.unresolved_bounds = []
+        self.seen_leaves = set()
+        self.inflight = {}
+        self.keep = set()
+        nwork = lp.max_batch - self.reserved
+        self.free = deque(range(nwork))
+        self.slot_gen = [0] * lp.max_batch
+        self.root_ready = False
         sharded = comm.world == 1
+        self.presplit = (0, 0, 0)
+        limit_hit = False
         while True:
-            if not sharded and len(heap) >= comm.world * self.batch:
+            if not sharded and len(self.heap) >= comm.world * self.batch and not self.inflight:
                 # deal the (identical on every rank) frontier: canonical order, round robin
-                heap.sort()
-                heap = [h for i, h in enumerate(heap) if i % comm.world == comm.rank]
-                heapq.heapify(heap)
-                pending_leaves = [lf for i, lf in enumerate(pending_leaves) if i % comm.world == comm.rank]
+                self.heap.sort(key=lambda h: h[:3])
+                self.heap = [h for i, h in enumerate(self.heap) if i % comm.world == comm.rank]
+                heapq.heapify(self.heap)
+                self.pending = deque(lf for i, lf in enumerate(self.pending) if i % comm.world == comm.rank)
+                self.retry = deque(lf for i, lf in enumerate(self.retry) if i % comm.world == comm.rank)
+                self.presplit = (res.nodes, res.lps, res.certified)
                 sharded = True
-            if comm.world > 1 and sharded:
+            stop = res.nodes >= self.node_limit or bool(self.time_limit and time.time() - t0 > self.time_limit)
+            open_n = len(self.heap) + len(self.pending) + len(self.retry) + len(self.inflight)
+            if comm.world > 1:
+                # every rank takes the same stop / termination decision in the same loop iteration
                 inc = comm.min(inc)
-                if comm.sum(len(heap) + len(pending_leaves)) == 0:
-                    break
-            elif not (heap or pending_leaves):
+                stop = comm.sum(int(stop)) > 0
+                open_n = comm.sum(open_n) if sharded else open_n
+            if open_n == 0:
                 break
-            if res.nodes >= self.node_limit or (self.time_limit and time.time() - t0 > self.time_limit):
+            if stop:
                 limit_hit = True
-                if comm.world > 1 and sharded:
-                    heap, pending_leaves = [], []
-                    continue
                 break
-            batch = []
-            while pending_leaves and len(batch) < self.batch:
-                leaf, pref = pending_leaves.pop()
-                batch.append((-math.inf, leaf, True, pref))
-            while heap and len(batch) < self.batch:
-                bnd, _, _, fix, is_leaf, pref = heapq.heappop(heap)
-                if bnd >= inc - self._gap_abs(inc):
-                    continue
-                batch.append((bnd, fix, is_leaf, pref))
-            if not batch:
-                continue
-            B = len(batch)
-            slots, warm = self._place(batch, half, root_ready)
-            half ^= 1
-            lb = np.full((B, n_int), -np.inf)
-            ub = np.full((B, n_int), np.inf)
-            for b, (_, fix, _, _) in enumerate(batch):
-                if fix:
-                    idx = np.fromiter(fix.keys(), np.int64, len(fix))
-                    val = np.fromiter(fix.values(), np.float64, len(fix))
-                    lb[b, idx] = val
-                    ub[b, idx] = val
-            cutoff = min(inc, self.ub0)
-            is_root = res.lps == 0
-            r = lp.solve(slots, lb, ub, tol=self.tol, max_iters=self.root_max_iters if is_root else self.max_iters,
-                         cutoff=cutoff if math.isfinite(cutoff) else math.inf, warm_start=warm)
-            res.lps += B
-            res.lp_iterations += int(r["iters"].sum())
-            for b, (pbound, fix, is_leaf, _) in enumerate(batch):
-                slot = int(slots[b])
-                st = int(r["status"][b])
-                if self.warm and not fix and not root_ready and st not in (LP_INFEASIBLE, LP_CUTOFF):
-                    lp.copy_state(slot, self.root_slot)   # every later node can start from the root
-                    root_ready = True
-                if st in (LP_INFEASIBLE, LP_CUTOFF):
-                    continue
-                bound = max(pbound, float(r["obj"][b]))
-                if is_leaf:
-                    res.leaves += 1
-                    if st != LP_OPTIMAL:
-                        res.unresolved += 1
+            # fill the free slots: retries, rounding leaves, then best-first open nodes
+            items = []
+            while self.free and (self.retry or self.pending or self.heap):
+                if self.retry:
+                    node = self.retry.popleft()
+                elif self.pending:
+                    node = self.pending.popleft()
+                else:
+                    _, _, _, node = heapq.heappop(self.heap)
+                    if node.bound >= inc - self._gap_abs(inc):
                         continue
-                    val = float(r["primal_obj"][b])
-                    if val < inc - self._gap_abs(inc):
-                        inc = val
-                        res.objective = val
-                        res.z, res.x = lp.solution(slot, dense_x=True)
-                        self.log(f"incumbent {val:.10g} (lps {res.lps}, nodes {res.nodes})")
-                    continue
-                if bound >= inc - self._gap_abs(inc):
-                    continue
-                res.nodes += 1
-                z, _ = lp.solution(slot, dense_x=False)
-                flow = self._flows(slot)
-                me = (slot, self.slot_gen[slot])
-                leaf = self._round(fix, flow)
-                if leaf is not None:
-                    key = tuple(sorted(k for k, v in leaf.items() if v > 0.5))
-                    if key not in seen_leaves:
-                        seen_leaves.add(key)
-                        pending_leaves.append((leaf, me))
-                var = self._branch_var(fix, z, flow)
-                if var is None:
-                    continue
-                for v in (1.0, 0.0):
-                    child = dict(fix)
-                    child[var] = v
-                    heapq.heappush(heap, (bound, -len(child), next(seq), child, self._complete(child), me))
-        if heap:
-            res.bound = min(min(h[0] for h in heap), inc)
-        else:
-            res.bound = inc
+                items.append((self.free.popleft(), node))
+                if not self.root_ready:
+                    break                 # the root runs alone (its state warm-starts everything after)
+            if items:
+                self._submit(items, inc)
+            if not self.inflight:
+                continue
+            # before the frontier is dealt every rank must stay identical: drain each batch whole
+            r = lp.advance(1 if sharded else len(self.inflight))
+            for i, slot in enumerate(r["slots"].tolist()):
+                node = self.inflight.pop(slot)
+                inc = self._finish(slot, node, int(r["status"][i]), float(r["obj"][i]), float(r["primal_obj"][i]),
+                                   int(r["iters"][i]), inc)
+        # drain what still iterates (a stop decision): their bounds stay valid
+        open_bounds = [n.bound for n in self.inflight.values()]
+        while lp.active() > 0:
+            r = lp.advance(lp.active())
+            for i, slot in enumerate(r["slots"].tolist()):
+                node = self.inflight.pop(slot, None)
+                if node is not None and int(r["status"][i]) not in (LP_INFEASIBLE, LP_CUTOFF):
+                    open_bounds.append(max(node.bound, float(r["obj"][i])))
+        open_bounds += [h[0] for h in self.heap] + [n.bound for n in self.pending] + [n.bound for n in self.retry]
+        open_bounds += self.unresolved_bounds
+        res.bound = min(open_bounds + [inc])
         if comm.world > 1:
             res.bound = comm.min(res.bound)
             limit_hit = comm.sum(int(limit_hit)) > 0
@@ -302,17 +367,25 @@ class BranchAndBound:
             mine = res.objective is not None and res.objective <= inc
             owner = int(comm.min(comm.rank if mine else comm.world))
             if owner < comm.world:
-                nz = self.lp.n_int
-                z = res.z if mine and comm.rank == owner else np.zeros(nz)
-                x = res.x if mine and comm.rank == owner else np.zeros((self.N, self.F, self.N), np.float32)
+                own = comm.rank == owner
+                z = res.z if own else np.zeros(self.lp.n_int)
+                x = lp.solution(res.incumbent_slot, dense_x=True)[1] if own else \
+                    np.zeros((self.N, self.F, self.N), np.float32)
                 res.z = comm.bcast(np.asarray(z, np.float64), owner)
                 res.x = comm.bcast(np.asarray(x, np.float32), owner)
                 res.objective = inc
-            res.nodes = comm.sum(res.nodes)
-            res.lps = comm.sum(res.lps)
+            # the pre-split phase ran identically on every rank: count it once
+            res.nodes = comm.sum(res.nodes - self.presplit[0]) + self.presplit[0]
+            res.lps = comm.sum(res.lps - self.presplit[1]) + self.presplit[1]
+            res.certified = comm.sum(res.certified - self.presplit[2]) + self.presplit[2]
+        elif res.incumbent_slot is not None:
+            _, res.x = lp.solution(res.incumbent_slot, dense_x=True)
+        unresolved_below = any(b < inc - self._gap_abs(inc) for b in self.unresolved_bounds)
+        if comm.world > 1:
+            unresolved_below = comm.sum(int(unresolved_below)) > 0
         if res.objective is None:
-            res.status = LIMIT if limit_hit else INFEASIBLE
+            res.status = LIMIT if (limit_hit or self.unresolved_bounds) else INFEASIBLE
         else:
-            res.status = LIMIT if limit_hit else OPTIMAL
+            res.status = LIMIT if (limit_hit or unresolved_below) else OPTIMAL
         res.seconds = time.time() - t0
         return res

@@ -18,7 +18,7 @@ STEP1, STEP2_DELETE, STEP2_CREATE = 1, 2, 3
 LP_OPTIMAL, LP_ITERATION_LIMIT, LP_INFEASIBLE, LP_CUTOFF, LP_NUMERICAL = 0, 1, 2, 3, 4
 VARIANTS = {"MinDelay": MIN_DELAY, "MinUtilization": MIN_UTILIZATION,
             "MinDelayAndUtilization": MIN_DELAY_AND_UTILIZATION}
-API_VERSION = 3
+API_VERSION = 4
 
 _dp = ctypes.POINTER(ctypes.c_double)
 
@@ -60,7 +60,10 @@ EXPORTS = ("nep_model_create", "nep_model_destroy", "nep_model_get_info", "nep_l
            "nep_lp_submit", "nep_lp_advance", "nep_lp_active",
            "nep_lp_get_solution", "nep_lp_get_rows", "nep_lp_copy_state", "nep_get_stats", "nep_reset_stats",
            "nep_last_error", "nep_api_version", "nep_lp_get_diag", "nep_debug_build", "nep_debug_state",
-           "nep_debug_presolve")
+           "nep_debug_presolve", "nep_lp_set_params", "nep_lp_get_flows", "nep_lp_routing_entries",
+           "nep_lp_allocation_entries", "nep_lp_score_check")
+SCORE_FIELDS = ("network_delay", "nodes_used", "node_cost", "bad_c_x", "bad_memory", "bad_handle", "bad_cpu",
+                "bad_n_c", "bad_budget", "handle_maxdev", "cpu_maxexcess")
 
 _lib = None
 
@@ -96,6 +99,11 @@ def load_library(path=None):
     lib.nep_debug_build.argtypes = [ctypes.POINTER(ModelDesc), _dp, _dp, _dp, _dp, ctypes.POINTER(i32)]
     lib.nep_debug_state.argtypes = [vp, i32, _dp, _dp, ctypes.POINTER(ctypes.c_float), _dp, _dp]
     lib.nep_debug_presolve.argtypes = [ctypes.POINTER(ModelDesc), i32, _dp, _dp, pi32, pi32, _dp, _dp]
+    lib.nep_lp_set_params.argtypes = [vp, ctypes.c_double, ctypes.c_double]
+    lib.nep_lp_get_flows.argtypes = [vp, i32, pi32, ctypes.POINTER(ctypes.c_float)]
+    lib.nep_lp_routing_entries.argtypes = [vp, i32, ctypes.c_double, i32, i64, pi64, pi32, pi32, _dp]
+    lib.nep_lp_allocation_entries.argtypes = [vp, i32, ctypes.c_double, i64, pi64, pi32, pi32]
+    lib.nep_lp_score_check.argtypes = [vp, i32, _dp]
     lib.nep_last_error.restype = ctypes.c_char_p
     lib.nep_api_version.restype = ctypes.c_int
     if lib.nep_api_version() != API_VERSION:
@@ -287,6 +295,57 @@ class LPModel:
                                                     _ptr(rf, ctypes.c_int32), _ptr(rs, ctypes.c_int32)),
                "nep_lp_get_rows")
         return xb, rf, rs
+
+    def set_params(self, tol=1e-7, cutoff=math.inf):
+        """tol / cutoff of every LP in flight (nep_lp_set_params): a B&B lowers the cutoff to each new
+        incumbent without resubmitting."""
+        _check(self._lib, self._lib.nep_lp_set_params(self._h, float(tol), float(cutoff)), "nep_lp_set_params")
+
+    def flows(self, slots):
+        """flow[b, f, j] = sum_i x[i, f, j] of finished slots, reduced on the device (nep_lp_get_flows)."""
+        slots = np.ascontiguousarray(np.asarray(slots, dtype=np.int32).reshape(-1))
+        out = np.zeros((len(slots), self.F, self.N), np.float32)
+        _check(self._lib, self._lib.nep_lp_get_flows(self._h, len(slots), _ptr(slots, ctypes.c_int32),
+                                                     _ptr(out, ctypes.c_float)), "nep_lp_get_flows")
+        return out
+
+    def routing_entries(self, slot, threshold=0.001, round3=True):
+        """Compacted routing entries of the aggregated rows, x > threshold, on the device
+        (nep_lp_routing_entries; neptune/utils/output.py:23-31): (row, dst, value) arrays."""
+        n = ctypes.c_int64(0)
+        _check(self._lib, self._lib.nep_lp_routing_entries(self._h, int(slot), float(threshold), int(round3), 0,
+                                                           ctypes.byref(n), None, None, None), "nep_lp_routing_entries")
+        k = n.value
+        row = np.zeros(k, np.int32)
+        dst = np.zeros(k, np.int32)
+        val = np.zeros(k)
+        if k:
+            _check(self._lib, self._lib.nep_lp_routing_entries(
+                self._h, int(slot), float(threshold), int(round3), k, ctypes.byref(n), _ptr(row, ctypes.c_int32),
+                _ptr(dst, ctypes.c_int32), _ptr(val)), "nep_lp_routing_entries")
+        return row, dst, val
+
+    def allocation_entries(self, slot, threshold=0.001):
+        """(f, j) pairs with c[f, j] > threshold, compacted on the device (output.py:33-39)."""
+        n = ctypes.c_int64(0)
+        _check(self._lib, self._lib.nep_lp_allocation_entries(self._h, int(slot), float(threshold), 0,
+                                                              ctypes.byref(n), None, None),
+               "nep_lp_allocation_entries")
+        k = n.value
+        fn = np.zeros(k, np.int32)
+        dst = np.zeros(k, np.int32)
+        if k:
+            _check(self._lib, self._lib.nep_lp_allocation_entries(
+                self._h, int(slot), float(threshold), k, ctypes.byref(n), _ptr(fn, ctypes.c_int32),
+                _ptr(dst, ctypes.c_int32)), "nep_lp_allocation_entries")
+        return fn, dst
+
+    def score_check(self, slot):
+        """The reference's scorers and feasibility checkers on a slot's solution, on the device
+        (nep_lp_score_check; efttc/utils/objectives.py, efttc/utils/constraints_step1.py)."""
+        out = np.zeros(len(SCORE_FIELDS))
+        _check(self._lib, self._lib.nep_lp_score_check(self._h, int(slot), _ptr(out)), "nep_lp_score_check")
+        return dict(zip(SCORE_FIELDS, out.tolist()))
 
     DIAG = ("pobj", "lagr", "best_lagr", "pres", "gap", "omega", "tau", "sigma", "eta", "k", "k_since_restart",
             "status", "active", "restart_fpr", "last_fpr", "sigma_max")

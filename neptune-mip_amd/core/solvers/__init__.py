@@ -5,11 +5,21 @@ SOLVERS is the whitelist the REST entry point resolves `solver.type` through (th
 `eval`, `main.py:44`).
 """
 from .neptune import *  # noqa: F401,F403
-from .neptune import NeptuneMinDelay, NeptuneMinDelayAndUtilization, NeptuneMinUtilization
+from .efttc import *  # noqa: F401,F403
+from .efttc import EfttcMinDelay, EfttcMinDelayAndUtilization, EfttcMinUtilization
+from .neptune import (NeptuneMinDelay, NeptuneMinDelayAndUtilization, NeptuneMinUtilization,
+                      NeptuneWithEFTTCMinDelay, NeptuneWithEFTTCMinDelayAndUtilization,
+                      NeptuneWithEFTTCMinUtilization)
 from .solver import Solver  # noqa: F401
 
 SOLVERS = {
     "NeptuneMinDelayAndUtilization": NeptuneMinDelayAndUtilization,
     "NeptuneMinDelay": NeptuneMinDelay,
     "NeptuneMinUtilization": NeptuneMinUtilization,
+    "NeptuneWithEFTTCMinDelay": NeptuneWithEFTTCMinDelay,
+    "NeptuneWithEFTTCMinUtilization": NeptuneWithEFTTCMinUtilization,
+    "NeptuneWithEFTTCMinDelayAndUtilization": NeptuneWithEFTTCMinDelayAndUtilization,
+    "EfttcMinDelay": EfttcMinDelay,
+    "EfttcMinUtilization": EfttcMinUtilization,
+    "EfttcMinDelayAndUtilization": EfttcMinDelayAndUtilization,
 }

@@ -1,10 +1,15 @@
 """NEPTUNE two-step orchestration (reference `core/solvers/neptune/neptune.py:7-93`).
 
+The NeptuneWithEFTTC* variants (:68-93) take the EF-TTC heuristic as step 1 (core/solvers/efttc)
+and always the MinDelayAndUtilization step-2 MIP, as the reference wires them.
+
 solve(): step 1 -> data.max_score = step-1 objective -> step-2 "delete" -> if that is not
 OPTIMAL, step-2 "create"; returns whether step 2 solved (step-1 status is ignored, :18-30).
 results(): the step-2 placement if step 2 solved, else the step-1 placement, in the wire format
 (:32-36).  score(): {"step1": ..., "step2": delete's if it solved, else create's} (:38-39).
 """
+from ..efttc.efttc_step1 import (EfttcStep1CPUMinDelay, EfttcStep1CPUMinDelayAndUtilization,
+                                 EfttcStep1CPUMinUtilization)
 from ..solver import Solver
 from .neptune_step import (NeptuneStep1CPUMinDelay, NeptuneStep1CPUMinDelayAndUtilization,
                            NeptuneStep1CPUMinUtilization, NeptuneStep2MinDelay,
@@ -75,4 +80,28 @@ class NeptuneMinUtilization(NeptuneBase):
         super().__init__(NeptuneStep1CPUMinUtilization(**kwargs),
                          NeptuneStep2MinUtilization(mode="delete", **kwargs),
                          NeptuneStep2MinUtilization(mode="create", **kwargs),
+                         **kwargs)
+
+
+class NeptuneWithEFTTCMinDelay(NeptuneBase):
+    def __init__(self, **kwargs):
+        super().__init__(step1=EfttcStep1CPUMinDelay(**kwargs),
+                         step2_delete=NeptuneStep2MinDelayAndUtilization(mode="delete", **kwargs),
+                         step2_create=NeptuneStep2MinDelayAndUtilization(mode="create", **kwargs),
+                         **kwargs)
+
+
+class NeptuneWithEFTTCMinUtilization(NeptuneBase):
+    def __init__(self, **kwargs):
+        super().__init__(step1=EfttcStep1CPUMinUtilization(**kwargs),
+                         step2_delete=NeptuneStep2MinDelayAndUtilization(mode="delete", **kwargs),
+                         step2_create=NeptuneStep2MinDelayAndUtilization(mode="create", **kwargs),
+                         **kwargs)
+
+
+class NeptuneWithEFTTCMinDelayAndUtilization(NeptuneBase):
+    def __init__(self, alpha=0.5, **kwargs):
+        super().__init__(step1=EfttcStep1CPUMinDelayAndUtilization(alpha=alpha, **kwargs),
+                         step2_delete=NeptuneStep2MinDelayAndUtilization(mode="delete", **kwargs),
+                         step2_create=NeptuneStep2MinDelayAndUtilization(mode="create", **kwargs),
                          **kwargs)

@@ -67,9 +67,9 @@ class NeptuneStepBase(Solver):
         self.init_objective()
         data = self.data
         N, F = len(data.nodes), len(data.functions)
-        # 2 x batch slots (alternating halves: the previous batch's node states stay resident as
-        # warm starts for their children) + 1 for the root's state (core/engine/bnb.py)
-        model = make_lp(data, self.VARIANT, self.step_id(), 2 * self.batch + 1, **self.model_kwargs())
+        # `batch` node LPs in flight + one slot for the root's state + one for the incumbent's
+        # (core/engine/bnb.py)
+        model = make_lp(data, self.VARIANT, self.step_id(), self.batch + 2, **self.model_kwargs())
         try:
             ub = self.upper_bound()
             bnb = BranchAndBound(model, data.workload_matrix, data.function_memory_matrix, data.node_memory_matrix,

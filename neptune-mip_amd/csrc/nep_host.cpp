@@ -31,6 +31,15 @@ hipError_t launch_node_bounds(const DeviceView &v, const int32_t *slots, int nsl
                               const double *cl, const double *cu, int max_chg, hipStream_t s);
 hipError_t launch_init_slot(const DeviceView &v, const int32_t *slots, int nslots, bool warm, double eta,
                             double omega0, hipStream_t s);
+hipError_t launch_node_flows(const DeviceView &v, const int32_t *slots, int n, float *out, hipStream_t s);
+hipError_t launch_compact_f32(const float *vals, int rows, int cols, int64_t ld, double thr, int round3,
+                              int32_t *cnt, int32_t *off, int32_t *orow, int32_t *ocol, double *oval, bool count_only,
+                              hipStream_t s);
+hipError_t launch_compact_f64(const double *vals, int rows, int cols, int64_t ld, double thr, int round3,
+                              int32_t *cnt, int32_t *off, int32_t *orow, int32_t *ocol, double *oval, bool count_only,
+                              hipStream_t s);
+hipError_t launch_score_check(const DeviceView &v, int slot, double *cpu_fj, double *fpart, double *jpart,
+                              const double *node_cost, double budget, double *out, hipStream_t s);
 }  // namespace nep
 
 using namespace nep;
@@ -104,6 +113,16 @@ struct Model {
   double *d_chg_lb = nullptr, *d_chg_ub = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   nep_stats stats{};
+  // scratch of the auxiliary kernels (nep_aux.hip), allocated on first use
+  float *d_flows = nullptr;                  // [max_batch][F][N]
+  int32_t *d_cnt = nullptr, *d_off = nullptr;   // [max(R, F) + 1]
+  int32_t *d_erow = nullptr, *d_ecol = nullptr;
+  double *d_eval = nullptr;
+  int64_t ecap = 0;
+  double *d_score = nullptr;                 // cpu_fj [F][NP] | fpart [F][4] | jpart [N][6] | out [16]
+  double *d_node_cost = nullptr;
+  std::vector<double> node_cost;
+  double node_budget = 0.0;
   // one block of check_every PDHG iterations as a captured HIP graph, per iterating-slot count
   // (the launch grids depend on it); rebuilt when check_every changes
   std::vector<hipGraphExec_t> block_graph;   // [max_batch + 1], index = slots iterating
@@ -339,6 +358,8 @@ int build(Model &m, const nep_model_desc &d) {
     m.hi[dl.oS] = score_rhs;
   }
   m.mem_f.assign(d.function_memory, d.function_memory + F);
+  m.node_cost.assign(d.node_cost, d.node_cost + N);
+  m.node_budget = d.node_budget;
 
   // non-x entries of K (COO) and x-row norms (x columns are never rescaled)
   Coo K;
@@ -573,6 +594,7 @@ int setup_dense(Model &m, const nep_model_desc &d) {
   v.stpart = (int64_t)F * NTS;
   v.sbpart = (int64_t)(F + m.JB) * NBS;
   v.snpart = (int64_t)F * 3 * NP;
+  v.srpart = (int64_t)F * 2 * NP;
   if ((rc = dalloc(m, &v.x, (size_t)B * v.sx))) return rc;
   if ((rc = dalloc(m, &v.xa, (size_t)B * v.sx))) return rc;
   if ((rc = dalloc(m, &v.theta, (size_t)B * m.R))) return rc;
@@ -589,6 +611,7 @@ int setup_dense(Model &m, const nep_model_desc &d) {
   if ((rc = dalloc(m, &v.tpart, (size_t)B * v.stpart))) return rc;
   if ((rc = dalloc(m, &v.bpart, (size_t)B * v.sbpart))) return rc;
   if ((rc = dalloc(m, &v.npart, (size_t)B * v.snpart))) return rc;
+  if ((rc = dalloc(m, &v.rpart, (size_t)B * v.srpart))) return rc;
   if ((rc = dalloc(m, &v.ctrl, (size_t)B))) return rc;
   if ((rc = dalloc(m, &m.d_prm, 2))) return rc;
   v.prm = m.d_prm;
@@ -1047,6 +1070,101 @@ int solve_batch(Model &m, int B, const int32_t *slots, const double *lbi, const 
   return NEP_OK;
 }
 
+// ---------------------------------------------------------------------------------------------
+// auxiliary device work on finished slots (nep_aux.hip)
+// ---------------------------------------------------------------------------------------------
+int ensure_entries(Model &m, int64_t need) {
+  if (need <= m.ecap) return NEP_OK;
+  int64_t cap = std::max<int64_t>(need, 4096);
+  int rc;
+  if ((rc = dalloc(m, &m.d_erow, (size_t)cap))) return rc;
+  if ((rc = dalloc(m, &m.d_ecol, (size_t)cap))) return rc;
+  if ((rc = dalloc(m, &m.d_eval, (size_t)cap))) return rc;
+  m.ecap = cap;
+  return NEP_OK;
+}
+
+// compaction of a [rows][ld] device matrix: entries > thr, in row-major order
+template <typename T>
+int compact(Model &m, const T *vals, int rows, int cols, int64_t ld, double thr, int round3, int64_t capacity,
+            int64_t *n_out, int32_t *orow, int32_t *ocol, double *oval) {
+  int rc;
+  if (!m.d_cnt) {
+    const size_t n = (size_t)std::max(m.R, m.F) + 1;
+    if ((rc = dalloc(m, &m.d_cnt, n))) return rc;
+    if ((rc = dalloc(m, &m.d_off, n))) return rc;
+  }
+  hipError_t e;
+  if constexpr (sizeof(T) == 4)
+    e = launch_compact_f32(vals, rows, cols, ld, thr, round3, m.d_cnt, m.d_off, nullptr, nullptr, nullptr, true, m.stream);
+  else
+    e = launch_compact_f64(vals, rows, cols, ld, thr, round3, m.d_cnt, m.d_off, nullptr, nullptr, nullptr, true, m.stream);
+  HIPCHK(e);
+  int32_t total = 0;
+  HIPCHK(hipMemcpyAsync(&total, m.d_off + rows, sizeof(int32_t), hipMemcpyDeviceToHost, m.stream));
+  HIPCHK(hipStreamSynchronize(m.stream));
+  *n_out = total;
+  if (capacity < total || total == 0) return NEP_OK;   // size query (or nothing to write)
+  if ((rc = ensure_entries(m, total))) return rc;
+  if constexpr (sizeof(T) == 4)
+    e = launch_compact_f32(vals, rows, cols, ld, thr, round3, m.d_cnt, m.d_off, m.d_erow, m.d_ecol, m.d_eval, false,
+                           m.stream);
+  else
+    e = launch_compact_f64(vals, rows, cols, ld, thr, round3, m.d_cnt, m.d_off, m.d_erow, m.d_ecol, m.d_eval, false,
+                           m.stream);
+  HIPCHK(e);
+  if (orow) HIPCHK(hipMemcpyAsync(orow, m.d_erow, total * sizeof(int32_t), hipMemcpyDeviceToHost, m.stream));
+  if (ocol) HIPCHK(hipMemcpyAsync(ocol, m.d_ecol, total * sizeof(int32_t), hipMemcpyDeviceToHost, m.stream));
+  if (oval) HIPCHK(hipMemcpyAsync(oval, m.d_eval, total * sizeof(double), hipMemcpyDeviceToHost, m.stream));
+  HIPCHK(hipStreamSynchronize(m.stream));
+  return NEP_OK;
+}
+
+int flows(Model &m, int n, const int32_t *slots, float *out) {
+  if (n <= 0) return NEP_OK;
+  if (n > m.max_batch) return fail(NEP_ERR_ARG, "n > max_batch");
+  for (int b = 0; b < n; ++b) {
+    if (slots[b] < 0 || slots[b] >= m.max_batch) return fail(NEP_ERR_ARG, "slot out of range");
+    if (m.busy[slots[b]]) return fail(NEP_ERR_STATE, "slot is still iterating");
+  }
+  int rc;
+  if (!m.d_flows && (rc = dalloc(m, &m.d_flows, (size_t)m.max_batch * m.F * m.N))) return rc;
+  HIPCHK(hipMemcpyAsync(m.d_new, slots, n * sizeof(int32_t), hipMemcpyHostToDevice, m.stream));
+  HIPCHK(launch_node_flows(m.v, m.d_new, n, m.d_flows, m.stream));
+  HIPCHK(hipMemcpyAsync(out, m.d_flows, (size_t)n * m.F * m.N * sizeof(float), hipMemcpyDeviceToHost, m.stream));
+  HIPCHK(hipStreamSynchronize(m.stream));
+  return NEP_OK;
+}
+
+int score_check(Model &m, int slot, double *out) {
+  int rc;
+  const size_t nfj = (size_t)m.F * m.NP, nf = (size_t)m.F * 4, nj = (size_t)m.N * 6;
+  if (!m.d_score) {
+    if ((rc = dalloc(m, &m.d_score, nfj + nf + nj + 16))) return rc;
+    const double *p = nullptr;
+    if ((rc = upload(m, &p, m.node_cost))) return rc;
+    m.d_node_cost = const_cast<double *>(p);
+  }
+  double *cpu_fj = m.d_score, *fpart = cpu_fj + nfj, *jpart = fpart + nf, *dout = jpart + nj;
+  HIPCHK(launch_score_check(m.v, slot, cpu_fj, fpart, jpart, m.d_node_cost, m.node_budget, dout, m.stream));
+  double raw[16] = {0};
+  HIPCHK(hipMemcpyAsync(raw, dout, 10 * sizeof(double), hipMemcpyDeviceToHost, m.stream));
+  HIPCHK(hipStreamSynchronize(m.stream));
+  // NEP_SC_* layout (include/neptune_lp.h)
+  out[0] = raw[0];                                   // network delay  sum W D x
+  out[1] = raw[6];                                   // nodes used     #{n != 0}
+  out[2] = raw[7];                                   // node cost      sum n * cost
+  out[3] = raw[1];                                   // c_x violations
+  out[4] = raw[3];                                   // memory violations
+  out[5] = raw[2];                                   // handle_all violations (sources)
+  out[6] = raw[4];                                   // CPU violations
+  out[7] = raw[5];                                   // n_c violations
+  out[8] = raw[7] > m.node_budget + 1e-6 ? 1.0 : 0.0;   // budget violated
+  out[9] = raw[8];                                   // max |sum_j x - 1| over routing rows
+  out[10] = raw[9];                                  // max CPU excess over cores
+  return NEP_OK;
+}
+
 }  // namespace
 
 // =============================================================================================
@@ -1176,6 +1294,51 @@ int nep_lp_copy_state(void *model, int32_t src, int32_t dst) {
   HIPCHK(hipMemcpyAsync(v.ctrl + dst, v.ctrl + src, sizeof(Ctrl), hipMemcpyDeviceToDevice, m.stream));
   HIPCHK(hipStreamSynchronize(m.stream));
   return NEP_OK;
+}
+
+int nep_lp_set_params(void *model, double tol, double cutoff) {
+  if (!model) return fail(NEP_ERR_ARG, "null model");
+  Model &m = *static_cast<Model *>(model);
+  if (tol > 0) m.run.tol = tol;
+  m.run.cutoff = cutoff;
+  m.prm_host[0] = m.run.tol;
+  m.prm_host[1] = m.run.cutoff;
+  HIPCHK(hipMemcpyAsync(m.d_prm, m.prm_host, sizeof(m.prm_host), hipMemcpyHostToDevice, m.stream));
+  HIPCHK(hipStreamSynchronize(m.stream));
+  return NEP_OK;
+}
+
+int nep_lp_get_flows(void *model, int32_t n, const int32_t *slots, float *flows_out) {
+  if (!model || (n > 0 && (!slots || !flows_out))) return fail(NEP_ERR_ARG, "null argument");
+  return flows(*static_cast<Model *>(model), n, slots, flows_out);
+}
+
+int nep_lp_routing_entries(void *model, int32_t slot, double threshold, int32_t round3, int64_t capacity,
+                           int64_t *n_entries, int32_t *row, int32_t *dst, double *val) {
+  if (!model || !n_entries) return fail(NEP_ERR_ARG, "null argument");
+  Model &m = *static_cast<Model *>(model);
+  if (slot < 0 || slot >= m.max_batch) return fail(NEP_ERR_ARG, "slot out of range");
+  if (m.busy[slot]) return fail(NEP_ERR_STATE, "slot is still iterating");
+  return compact<float>(m, m.v.x + (size_t)slot * m.v.sx, m.R, m.N, m.NP, threshold, round3, capacity, n_entries, row,
+                        dst, val);
+}
+
+int nep_lp_allocation_entries(void *model, int32_t slot, double threshold, int64_t capacity, int64_t *n_entries,
+                              int32_t *fn, int32_t *dst) {
+  if (!model || !n_entries) return fail(NEP_ERR_ARG, "null argument");
+  Model &m = *static_cast<Model *>(model);
+  if (slot < 0 || slot >= m.max_batch) return fail(NEP_ERR_ARG, "slot out of range");
+  if (m.busy[slot]) return fail(NEP_ERR_STATE, "slot is still iterating");
+  return compact<double>(m, m.v.zi + (size_t)slot * m.v.sint + m.il.oc, m.F, m.N, m.N, threshold, 0, capacity,
+                         n_entries, fn, dst, nullptr);
+}
+
+int nep_lp_score_check(void *model, int32_t slot, double *out) {
+  if (!model || !out) return fail(NEP_ERR_ARG, "null argument");
+  Model &m = *static_cast<Model *>(model);
+  if (slot < 0 || slot >= m.max_batch) return fail(NEP_ERR_ARG, "slot out of range");
+  if (m.busy[slot]) return fail(NEP_ERR_STATE, "slot is still iterating");
+  return score_check(m, slot, out);
 }
 
 int nep_lp_get_diag(void *model, int32_t slot, double *out16) {

@@ -13,6 +13,7 @@
 //   kty   [F*NP + NP + 4] f32  packed duals the x pass needs: y1+y2 per (f,j), y5 per j, yS
 //   tpart [F][NTS] f64  per-function scalars of the rows (score row, objective, Lagrangian, movement)
 //   npart [F][3][NP] f64 per-(function, node) shares of the node rows: memory, c, CPU
+//   rpart [F][2][NP] f64 the same memory / c shares at the repaired certificate point
 //   bpart [F+JB][NBS] f64 per-block scalars of the small variables
 //   ctrl  Ctrl          step sizes, primal weight, restart state, status
 // Static (shared by all slots): rows [R] (RowInfo), frow [F+1], D [N][NP] f32, cpr [F][NP] f32,
@@ -64,8 +65,12 @@ enum {
   BS_POBJ,           // objective of the small vars
   BS_RES,            // max normalised primal violation
   BS_MOVE_Z, BS_MOVE_Y, BS_DIST_Z, BS_DIST_Y,
+  BS_SUMC_REP,       // certificate: sum over (f,j) of the repaired c (step-2 rows D3/D4)
+  BS_SCORE_N_REP,    // certificate: score-row n part of the repaired n
   NBS
 };
+// BS_POBJ / BS_RES carry, on certificate iterations, the objective of the REPAIRED small variables and
+// the max violation of the rows at the repaired point (DESIGN.md §4 "Certificate").
 
 struct Ctrl {
   double eta, omega, tau, sigma;
@@ -109,8 +114,9 @@ struct DeviceView {
   double *y, *ya, *kz, *kza;             // duals, anchor, activity K z of the iterate and of the anchor
   float *kty;
   double *tpart, *bpart, *npart;
+  double *rpart;                         // [F][2][NP] certificate: repaired c shares of the node rows (mem, c)
   Ctrl *ctrl;
-  int64_t sx, smask, sint, sdual, skty, stpart, sbpart, snpart;   // per-slot strides (elements)
+  int64_t sx, smask, sint, sdual, skty, stpart, sbpart, snpart, srpart;   // per-slot strides (elements)
   // check/solve parameters.  tol / cutoff live in device memory (prm[0] / prm[1], written by every
   // nep_lp_submit) because the iteration blocks are replayed from captured HIP graphs: a value
   // passed by value would stay frozen at capture time.

@@ -136,10 +136,7 @@ __device__ __forceinline__ double dual_step(const DeviceView &v, double *y, doub
     y[row] = ynew;
   }
   kz[row] = knew;
-  if (CHECK) {
-    a.lagr += row_lagr(yold, lo, hi);
-    a.res = fmax(a.res, row_viol(act, lo, hi) / v.rownorm[row]);
-  }
+  if (CHECK) a.lagr += row_lagr(yold, lo, hi);
   return ynew;
 }
 
@@ -161,7 +158,6 @@ __device__ __forceinline__ double primal_step(const DeviceView &v, double *zi, d
     const double u = (nz - zanc) / g;
     a.dsz += u * u;
     a.lagr += rc > 0 ? lb[k] * rc : ub[k] * rc;
-    a.pobj += v.cost_int[k] * nz;
   }
   return nz;
 }
@@ -291,10 +287,14 @@ void x_pass(DeviceView v, const int32_t *__restrict__ slots, int first, int plai
   // Per-function column constants (packed duals kx = y1 + y2 and cy5 = cpr * y5) and the per-wave
   // column accumulators (C1/C2 column sums, C5 W-weighted sums) live in LDS, not in registers:
   // 32 fewer VGPRs per lane at CPL = 2, i.e. more waves per SIMD to keep HBM reads in flight.
-  float *lS = lds, *lW = lds + TW * NP, *lK = lds + 2 * TW * NP, *lC = lK + NP;
-  // certificate iterations: the same constants in fp64 from the fp64 duals, so the Lagrangian bound
-  // carries no fp32 rounding of y (|y1| can be large against the big-M rows)
-  double *lKd = reinterpret_cast<double *>(lds + (2 * TW + 2) * NP), *lCd = lKd + NP;
+  // Certificate iterations keep the column sums S[f, j] in fp64 (lSd, in place of lS): the
+  // certificate's repaired point takes c from S exactly (pooled rows carry weights m ~ N, whose fp32
+  // products would shift S by ~1e-5), and the constants in fp64 from the fp64 duals (lKd, lCd), so
+  // the Lagrangian bound carries no fp32 rounding of y (|y1| can be large against the big-M rows).
+  constexpr int SW = CHECK ? 2 : 1;   // words per column-sum accumulator (the CPU sums lW alike)
+  float *lS = lds, *lW = lds + SW * TW * NP, *lK = lW + SW * TW * NP, *lC = lK + NP;
+  double *lSd = reinterpret_cast<double *>(lS), *lWd = reinterpret_cast<double *>(lW);
+  double *lKd = reinterpret_cast<double *>(lC + NP), *lCd = lKd + NP;
   for (int j = threadIdx.x; j < NP; j += kWave * TW) {
     lK[j] = kty[(int64_t)f * NP + j];
     lC[j] = v.cpr[(int64_t)f * NP + j] * kty[(int64_t)F * NP + j];
@@ -314,8 +314,14 @@ void x_pass(DeviceView v, const int32_t *__restrict__ slots, int first, int plai
       const uchar4 m = *reinterpret_cast<const uchar4 *>(mask + j0);
       mbits |= (uint32_t)(m.x != 0) << (4 * q) | (uint32_t)(m.y != 0) << (4 * q + 1) |
                (uint32_t)(m.z != 0) << (4 * q + 2) | (uint32_t)(m.w != 0) << (4 * q + 3);
-      *reinterpret_cast<float4 *>(lS + wave * NP + j0) = make_float4(0.f, 0.f, 0.f, 0.f);
-      *reinterpret_cast<float4 *>(lW + wave * NP + j0) = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (CHECK) {
+        double2 *pd = reinterpret_cast<double2 *>(lSd + wave * NP + j0);
+        double2 *pe = reinterpret_cast<double2 *>(lWd + wave * NP + j0);
+        pd[0] = pd[1] = pe[0] = pe[1] = make_double2(0.0, 0.0);
+      } else {
+        *reinterpret_cast<float4 *>(lS + wave * NP + j0) = make_float4(0.f, 0.f, 0.f, 0.f);
+        *reinterpret_cast<float4 *>(lW + wave * NP + j0) = make_float4(0.f, 0.f, 0.f, 0.f);
+      }
     }
   }
   __syncthreads();
@@ -473,14 +479,24 @@ void x_pass(DeviceView v, const int32_t *__restrict__ slots, int first, int plai
     for (int q = 0; q < CPL; ++q) {
       const int j0 = 4 * (lane + kWave * q);
       if (j0 < NP) {
-        float4 *ps = reinterpret_cast<float4 *>(lS + wave * NP + j0);
-        float4 *pw = reinterpret_cast<float4 *>(lW + wave * NP + j0);
-        float4 a = *ps, b = *pw;
         const float *xq = xn + 4 * q;
-        a.x += m * xq[0]; a.y += m * xq[1]; a.z += m * xq[2]; a.w += m * xq[3];
-        b.x += w * xq[0]; b.y += w * xq[1]; b.z += w * xq[2]; b.w += w * xq[3];
-        *ps = a;
-        *pw = b;
+        if (CHECK) {
+          double2 *pd = reinterpret_cast<double2 *>(lSd + wave * NP + j0);
+          double2 *pe = reinterpret_cast<double2 *>(lWd + wave * NP + j0);
+          double2 a0 = pd[0], a1 = pd[1], b0 = pe[0], b1 = pe[1];
+          const double md = m, wd = w;
+          a0.x += md * xq[0]; a0.y += md * xq[1]; a1.x += md * xq[2]; a1.y += md * xq[3];
+          b0.x += wd * xq[0]; b0.y += wd * xq[1]; b1.x += wd * xq[2]; b1.y += wd * xq[3];
+          pd[0] = a0; pd[1] = a1; pe[0] = b0; pe[1] = b1;
+        } else {
+          float4 *ps = reinterpret_cast<float4 *>(lS + wave * NP + j0);
+          float4 *pw = reinterpret_cast<float4 *>(lW + wave * NP + j0);
+          float4 a = *ps, b = *pw;
+          a.x += m * xq[0]; a.y += m * xq[1]; a.z += m * xq[2]; a.w += m * xq[3];
+          b.x += w * xq[0]; b.y += w * xq[1]; b.z += w * xq[2]; b.w += w * xq[3];
+          *ps = a;
+          *pw = b;
+        }
       }
     }
 #pragma unroll
@@ -516,13 +532,22 @@ void x_pass(DeviceView v, const int32_t *__restrict__ slots, int first, int plai
   const double yD3a = v.step2 ? y[dl.oD3a] : 0.0, yD3b = v.step2 ? y[dl.oD3b] : 0.0;
   const double yD4 = v.step2 ? y[dl.oD4] : 0.0;
   SmallAcc a;
-  double sumc = 0.0;
+  double sumc = 0.0, sumc_rep = 0.0;
   for (int j = threadIdx.x; j < N; j += kWave * TW) {
     float Sf = 0.f, Uf = 0.f;
+    double Sd = 0.0, Ud = 0.0;
 #pragma unroll
-    for (int wv = 0; wv < TW; ++wv) { Sf += lS[wv * NP + j]; Uf += lW[wv * NP + j]; }
-    const double S = Sf;
-    const double U = (double)(Uf * v.cpr[(int64_t)f * NP + j]);
+    for (int wv = 0; wv < TW; ++wv) {
+      if (CHECK) {
+        Sd += lSd[wv * NP + j];
+        Ud += lWd[wv * NP + j];
+      } else {
+        Sf += lS[wv * NP + j];
+        Uf += lW[wv * NP + j];
+      }
+    }
+    const double S = CHECK ? Sd : (double)Sf;
+    const double U = CHECK ? Ud * (double)v.cpr[(int64_t)f * NP + j] : (double)(Uf * v.cpr[(int64_t)f * NP + j]);
     const int idx = f * N + j;
     const double y1 = y[dl.o1 + idx], y2 = y[dl.o2 + idx];
     const double y3 = y[dl.o3 + j];
@@ -554,6 +579,28 @@ void x_pass(DeviceView v, const int32_t *__restrict__ slots, int first, int plai
     np_[NP + j] = cn;
     np_[2 * NP + j] = U;
     sumc += cn;
+    if (CHECK) {
+      // Certificate point: the routing x̂ of this iteration with the small variables REPAIRED, in
+      // dependency order, onto the rows each one closes: c = the T output clamped into
+      // [S/M, S + eps] (C1/C2) within the node box, then the cheapest mf = max(lb, c - old),
+      // mt = max(lb, old - c) (D1/D2; both cost F*N).  At convergence the clamp moves c by the PDHG
+      // residual only, so the repaired point keeps the iterate's (near-optimal) choices; an empty
+      // interval is a violation of the x-driven row.
+      const double loc = fmax(lb[il.oc + idx], S / v.M), hic = fmin(ub[il.oc + idx], S + v.eps);
+      const double cr = loc > hic ? loc : fmin(fmax(cn, loc), hic);
+      if (v.step2) {
+        const double old = -v.lo[dl.oD1 + idx];
+        const double mfr = fmax(lb[il.omf + idx], cr - old), mtr = fmax(lb[il.omt + idx], old - cr);
+        a.res = fmax(a.res, fmax(mfr - ub[il.omf + idx], mtr - ub[il.omt + idx]));
+        a.pobj += v.cost_int[il.omf + idx] * mfr + v.cost_int[il.omt + idx] * mtr;
+      }
+      a.res = fmax(a.res, (loc - hic) / v.rownorm[dl.o2 + idx]);
+      a.pobj += v.cost_int[il.oc + idx] * cr;
+      sumc_rep += cr;
+      double *rp = v.rpart + slot * v.srpart + (int64_t)f * 2 * NP;
+      rp[j] = memf * cr;
+      rp[NP + j] = cr;
+    }
   }
 
   // scalar partials of this (f, slot): read by scalar_pass on init / certificate / step-2 iterations
@@ -574,6 +621,8 @@ void x_pass(DeviceView v, const int32_t *__restrict__ slots, int first, int plai
   vals[NTS + BS_MOVE_Y] = a.mvy;
   vals[NTS + BS_DIST_Z] = a.dsz;
   vals[NTS + BS_DIST_Y] = a.dsy;
+  vals[NTS + BS_SUMC_REP] = sumc_rep;
+  vals[NTS + BS_SCORE_N_REP] = 0.0;
 #pragma unroll
   for (int k = 0; k < NTS + NBS; ++k) {
     const bool needed = INIT || CHECK || k == TS_SCORE || k == NTS + BS_SUMC_NEW;
@@ -592,8 +641,11 @@ void x_pass(DeviceView v, const int32_t *__restrict__ slots, int first, int plai
   }
 }
 
-__device__ __forceinline__ void write_bpart(double *bp, const SmallAcc &a, double sumc, double score_n, int lane) {
+__device__ __forceinline__ void write_bpart(double *bp, const SmallAcc &a, double sumc, double score_n,
+                                            double score_n_rep, int lane) {
   double vals[NBS];
+  vals[BS_SUMC_REP] = 0.0;
+  vals[BS_SCORE_N_REP] = score_n_rep;
   vals[BS_SUMC_NEW] = sumc;
   vals[BS_SCORE_N] = score_n;
   vals[BS_LAGR] = a.lagr;
@@ -618,7 +670,7 @@ __device__ __forceinline__ void write_bpart(double *bp, const SmallAcc &a, doubl
 template <bool CHECK, bool INIT>
 __global__ __launch_bounds__(kNodeThreads) void node_pass(DeviceView v, const int32_t *__restrict__ slots, int first,
                                                           int plain, int it) {
-  __shared__ double red[kNodeWaves][3][kWave];
+  __shared__ double red[kNodeWaves][5][kWave];
   const int jb = blockIdx.x;
   const int slot = slots[blockIdx.y];
   Ctrl *ctrl = v.ctrl + slot;
@@ -630,7 +682,7 @@ __global__ __launch_bounds__(kNodeThreads) void node_pass(DeviceView v, const in
   {
     const int per = (F + kNodeWaves - 1) / kNodeWaves;
     const int f0 = wave * per, f1 = min(F, f0 + per);
-    double memc = 0.0, sumc = 0.0, U = 0.0;
+    double memc = 0.0, sumc = 0.0, U = 0.0, memr = 0.0, sumr = 0.0;
     if (valid) {
       const double *np_ = v.npart + slot * v.snpart;
 #pragma unroll 4
@@ -640,19 +692,30 @@ __global__ __launch_bounds__(kNodeThreads) void node_pass(DeviceView v, const in
         sumc += p[NP + j];
         U += p[2 * NP + j];
       }
+      if (CHECK) {
+        const double *rp = v.rpart + slot * v.srpart;
+        for (int f = f0; f < f1; ++f) {
+          memr += rp[(int64_t)f * 2 * NP + j];
+          sumr += rp[(int64_t)f * 2 * NP + NP + j];
+        }
+      }
     }
     red[wave][0][lane] = memc;
     red[wave][1][lane] = sumc;
     red[wave][2][lane] = U;
+    red[wave][3][lane] = memr;
+    red[wave][4][lane] = sumr;
   }
   __syncthreads();
   if (wave != 0) return;
-  double memc = 0.0, sumc = 0.0, U = 0.0;
+  double memc = 0.0, sumc = 0.0, U = 0.0, memr = 0.0, sumr = 0.0;
 #pragma unroll
   for (int wv = 0; wv < kNodeWaves; ++wv) {
     memc += red[wv][0][lane];
     sumc += red[wv][1][lane];
     U += red[wv][2][lane];
+    memr += red[wv][3][lane];
+    sumr += red[wv][4][lane];
   }
   const DualLayout &dl = v.dl;
   const IntLayout &il = v.il;
@@ -666,7 +729,12 @@ __global__ __launch_bounds__(kNodeThreads) void node_pass(DeviceView v, const in
   double *kza = v.kza + slot * v.sdual;
   float *kty = v.kty + slot * v.skty;
   SmallAcc a;
-  double score_n = 0.0;
+  double score_n = 0.0, score_n_rep = 0.0;
+  if (valid && CHECK) {
+    // certificate point (see x_pass): C3 at the repaired c, C5 (x only)
+    a.res = fmax(a.res, row_viol(memr, v.lo[dl.o3 + j], v.hi[dl.o3 + j]) / v.rownorm[dl.o3 + j]);
+    a.res = fmax(a.res, row_viol(U, v.lo[dl.o5 + j], v.hi[dl.o5 + j]) / v.rownorm[dl.o5 + j]);
+  }
   if (valid) {
     dual_step<CHECK, INIT>(v, y, ya, kz, kza, dl.o3 + j, memc, y[dl.o3 + j], sigma, copy_anchor, halp, lam, a);
     const double y5n = dual_step<CHECK, INIT>(v, y, ya, kz, kza, dl.o5 + j, U, y[dl.o5 + j], sigma, copy_anchor, halp,
@@ -681,9 +749,17 @@ __global__ __launch_bounds__(kNodeThreads) void node_pass(DeviceView v, const in
       dual_step<CHECK, INIT>(v, y, ya, kz, kza, dl.o6 + j, sumc - v.M * nn, y6, sigma, copy_anchor, halp, lam, a);
       dual_step<CHECK, INIT>(v, y, ya, kz, kza, dl.o7 + j, sumc - nn, y7, sigma, copy_anchor, halp, lam, a);
       score_n = v.score_n_coef * nn;
+      if (CHECK) {
+        // repaired n: the T output clamped into [sum c / M, sum c + eps] (C6/C7 at the repaired c)
+        const double lon = fmax(lb[il.on + j], sumr / v.M), hin = fmin(ub[il.on + j], sumr + v.eps);
+        const double nr = lon > hin ? lon : fmin(fmax(nn, lon), hin);
+        a.res = fmax(a.res, lon - hin);
+        a.pobj += v.cost_int[il.on + j] * nr;
+        score_n_rep = v.score_n_coef * nr;
+      }
     }
   }
-  write_bpart(v.bpart + slot * v.sbpart + ((int64_t)F + jb) * NBS, a, 0.0, score_n, lane);
+  write_bpart(v.bpart + slot * v.sbpart + ((int64_t)F + jb) * NBS, a, 0.0, score_n, score_n_rep, lane);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -780,7 +856,24 @@ __global__ __launch_bounds__(256) void scalar_pass(DeviceView v, const int32_t *
   ctrl->k_since_restart += done;
   ctrl->restart_pending = 0;
   if (tot[TS_EMPTY] > 0) { ctrl->status = 2; ctrl->active = 0; return; }
-  const double lagr = a.lagr, pobj = a.pobj, res = a.res;
+  // certificate point, completed: allocated / deallocated repaired from the repaired sum c
+  // (D3: a <= sumOld - sum c, d <= sum c - sumOld; D4: a + d >= sigma4 (sumOld - sum c); costs
+  // (w-1) a + (w+1) d, both positive: a as large as allowed, d = the rest), the score row at the
+  // repaired n.  Its objective is an upper bound on the LP value whenever it is feasible (res <= tol),
+  // the Lagrangian a lower bound: the gap between the two certifies the node LP's value.
+  double pobj = a.pobj, res = a.res;   // x part (TS_POBJ) + repaired small variables
+  if (v.step2) {
+    const double sum_old = v.lo[dl.oD3b];
+    const double s = tot[NTS + BS_SUMC_REP] - sum_old;
+    const double A = fmin(ub[il.oa], -s), Dm = fmin(ub[il.od], s), K = v.sigma4 * (-s);
+    const double ar = fmax(lb[il.oa], A);
+    const double dr = fmax(lb[il.od], K - ar);
+    res = fmax(res, fmax(lb[il.oa] - A, dr - Dm));
+    pobj += v.cost_int[il.oa] * ar + v.cost_int[il.od] * dr;
+    const double score_rep = tot[TS_SCORE] + tot[NTS + BS_SCORE_N_REP];
+    res = fmax(res, row_viol(score_rep, v.lo[dl.oS], v.hi[dl.oS]) / v.rownorm[dl.oS]);
+  }
+  const double lagr = a.lagr;
   const double gap = pobj - lagr;
   ctrl->pobj = pobj;
   ctrl->lagr = lagr;
@@ -906,7 +999,8 @@ template <int CPL, int TW>
 static hipError_t launch_x_tw(const DeviceView &v, const int32_t *slots, int nslots, bool check, bool init,
                               bool first, bool plain, int it, hipStream_t s) {
   dim3 grid(8 * ((v.F * nslots + 7) / 8)), block(kWave * TW);
-  const size_t lds = (size_t)(2 * TW + 2) * v.NP * sizeof(float) + (check ? 2 * v.NP * sizeof(double) : 0);
+  const size_t lds = (size_t)(2 * TW + 2) * v.NP * sizeof(float) +
+                    (check ? (size_t)2 * TW * v.NP * sizeof(float) + 2 * v.NP * sizeof(double) : 0);
   const int fi = first ? 1 : 0, pl = plain ? 1 : 0;
   if (init) hipLaunchKernelGGL((x_pass<CPL, false, true, TW>), grid, block, lds, s, v, slots, fi, pl, it, nslots);
   else if (check)
@@ -923,7 +1017,8 @@ static hipError_t launch_x_tw(const DeviceView &v, const int32_t *slots, int nsl
 static int tile_waves(const DeviceView &v, int nslots) {
   int tw = 4;
   while (tw < 16 && (int64_t)nslots * v.F * tw < 4096) tw *= 2;
-  while (tw > 4 && (size_t)(2 * tw + 2) * v.NP * sizeof(float) + 2 * v.NP * sizeof(double) > 128 * 1024) tw /= 2;
+  // LDS of the certificate variant: fp64 column sums + fp32 CPU sums + constants (fp32 and fp64)
+  while (tw > 4 && (size_t)(4 * tw + 2) * v.NP * sizeof(float) + 2 * v.NP * sizeof(double) > 144 * 1024) tw /= 2;
   return tw;
 }
 

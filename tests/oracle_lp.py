@@ -68,6 +68,47 @@ class OracleLP:
             self._sol[int(s)] = x
         return {"obj": obj, "primal_obj": obj.copy(), "status": status, "iters": np.zeros(B, np.int64)}
 
+    # streaming form (nep_lp_submit / nep_lp_advance): HiGHS solves each submitted node at once; advance
+    # hands back up to min_done finished nodes per call, in slot order, like the engine's blocks
+    def submit(self, slots, lb=None, ub=None, tol=1e-7, cutoff=math.inf, max_iters=0, check_every=64,
+               warm_start=False, warm_omega_floor=0.0):
+        slots = np.asarray(slots).reshape(-1)
+        self._cutoff = cutoff
+        r = self.solve(slots, lb, ub, tol=tol, cutoff=math.inf)
+        if not hasattr(self, "_queue"):
+            self._queue = []
+        st = np.zeros(len(slots), np.int32)
+        for b, s in enumerate(slots):
+            if int(r["status"][b]) == LP_INFEASIBLE:
+                st[b] = LP_INFEASIBLE
+                continue
+            st[b] = LP_ITERATION_LIMIT
+            self._queue.append((int(s), float(r["obj"][b])))
+        return st
+
+    def set_params(self, tol=1e-7, cutoff=math.inf):
+        self._cutoff = cutoff
+
+    def active(self):
+        return len(getattr(self, "_queue", []))
+
+    def advance(self, min_done=1):
+        q = getattr(self, "_queue", [])
+        k = len(q) if min_done <= 0 else min(len(q), max(1, int(min_done)))
+        done, self._queue = sorted(q[:k]), q[k:]
+        cut = getattr(self, "_cutoff", math.inf)
+        obj = np.array([o for _, o in done])
+        st = np.array([LP_CUTOFF if o > cut else LP_OPTIMAL for _, o in done], np.int32)
+        return {"slots": np.array([s for s, _ in done], np.int32), "obj": obj, "primal_obj": obj.copy(),
+                "status": st, "iters": np.zeros(len(done), np.int64)}
+
+    def flows(self, slots):
+        out = np.zeros((len(slots), self.F, self.N), np.float32)
+        for b, s in enumerate(np.asarray(slots).reshape(-1)):
+            x = self._sol[int(s)]
+            out[b] = x[:self.nx].reshape(self.F, self.N, self.N).sum(axis=1)
+        return out
+
     def copy_state(self, src, dst):
         """Warm-start hand-off of the engine (nep_lp_copy_state); HiGHS solves from scratch, so this
         only records the copy (tests check the B&B's slot bookkeeping with it)."""
