@@ -70,6 +70,12 @@ def parse(argv=None):
     ap.add_argument("--root-check-every", type=int, default=64)
     ap.add_argument("--cold", action="store_true", help="cold-start every node LP")
     ap.add_argument("--cpu-budget", type=float, default=25.0, help="seconds for the CPU baseline (0 = skip)")
+    ap.add_argument("--cpu-workers", type=int, default=16,
+                    help="CPU baseline worker processes (capped at the host's cores; 16 = the GPU box's share)")
+    ap.add_argument("--bnb-seconds", type=float, default=20.0,
+                    help="time limit of the product branch-and-bound section (0 = skip)")
+    ap.add_argument("--bnb-nodes", type=int, default=256)
+    ap.add_argument("--bnb-functions", type=int, default=128)
     ap.add_argument("--traffic", default=os.path.join(REPO, "profiles", "traffic.json"))
     return ap.parse_args(argv)
 
@@ -97,56 +103,138 @@ def node_bounds(n_int, F, N, B, k, seed):
     return lb, ub
 
 
-def cpu_baseline(N, F, seed, fix, budget):
-    """The reference formulation of the same generator, solved by the oracle (HiGHS LP, one thread).
+def _dnf_probe(N, F, seed, seconds):
+    """Try to build the literal reference model at the bench size in a child process, killed after
+    `seconds`: the CPU path's 'did not finish' evidence at 512x256."""
+    import subprocess
+    code = ("import sys; sys.path[:0]=%r\n"
+            "from core.utils.synthetic import synthetic_payload\n"
+            "from oracle.inputs import data_to_solver_input\n"
+            "from oracle.formulation import build_model\n"
+            "p=synthetic_payload(%d,%d,seed=%d); d=data_to_solver_input(p,with_db=False)\n"
+            "m=build_model(d,'MinDelayAndUtilization',step=1,alpha=0.5); print('built', m['A'].shape)\n"
+            % ([PKG, REPO], N, F, seed))
+    t0 = time.perf_counter()
+    try:
+        r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=seconds)
+        return {"finished": r.returncode == 0, "seconds": time.perf_counter() - t0, "stage": "model build"}
+    except subprocess.TimeoutExpired:
+        return {"finished": False, "seconds": seconds, "stage": "model build",
+                "note": f"DNF > {seconds:.0f} s: the literal {N}x{F} model ({N * N * F:,} routing columns) was "
+                        f"not even built"}
 
-    The literal reference model at 512x256 has 67 M columns and 269 M nonzeros: building it alone
-    exceeds any bounded budget.  So the sample is the same node-LP workload
-    (same generator, same kind of fixings) at growing sizes until the budget is spent; the
-    measured times are fitted as t ~ (N^2 F)^p and extrapolated to the benchmark size.  The
-    measured points are reported in `sample`."""
+
+def cpu_baseline(N, F, seed, fix, budget, workers):
+    """The reference formulation of the same generator, solved by the oracle (HiGHS LP; oracle/).
+
+    1. single-thread node-LP times at growing sizes (same generator, same kind of fixings) -> the
+       power-law fit t ~ (N^2 F)^p;
+    2. throughput: `workers` node LPs of the largest measured size solved at once, one per worker
+       process (oracle/solve.py lp_batch_cpu), i.e. the host's LP/s at that size;
+    3. the bench size: a bounded attempt (model build in a child process, killed at the budget's
+       share) -> "DNF > T"; the 512x256 LP/s is the measured pool rate scaled by the fitted per-LP
+       time ratio."""
     import numpy as np
     from oracle.formulation import build_model
     from oracle.inputs import data_to_solver_input as oracle_input
+    from oracle.solve import lp_batch_cpu
     from oracle.solve import solve as oracle_solve
     from core.utils.synthetic import synthetic_payload
 
-    pts = []
-    spent = 0.0
-    for n in (16, 24, 32, 48, 64, 96, 128):
-        f = max(1, n // 2)
-        t0 = time.perf_counter()
+    def model_and_bounds(n, f, count, s):
         p = synthetic_payload(n, f, seed=seed)
         d = oracle_input(p, workload_coeff=1, with_db=False)
         m = build_model(d, "MinDelayAndUtilization", step=1, alpha=p["solver"]["args"]["alpha"])
         nx = n * n * f
-        lb, ub = node_bounds(f * n + n, f, n, 1, fix, seed=seed)
-        rl, ru = m["lb"].copy(), m["ub"].copy()
-        fin = np.isfinite(lb[0])
-        rl[nx:][fin] = lb[0][fin]
-        ru[nx:][fin] = ub[0][fin]
+        lb, ub = node_bounds(f * n + n, f, n, count, fix, seed=s)
+        out = []
+        for b in range(count):
+            rl, ru = m["lb"].copy(), m["ub"].copy()
+            fin = np.isfinite(lb[b])
+            rl[nx:][fin] = lb[b][fin]
+            ru[nx:][fin] = ub[b][fin]
+            out.append((rl, ru))
+        return m, out
+
+    t_start = time.perf_counter()
+    pts = []
+    for n in (16, 24, 32, 48, 64, 96, 128):
+        f = max(1, n // 2)
+        t0 = time.perf_counter()
+        m, bnds = model_and_bounds(n, f, 1, seed)
         t1 = time.perf_counter()
-        st, obj, _ = oracle_solve(m, relax=True, lb=rl, ub=ru)
+        st, _, _ = oracle_solve(m, relax=True, lb=bnds[0][0], ub=bnds[0][1])
         t_lp = time.perf_counter() - t1
-        spent += time.perf_counter() - t0
         pts.append((n, f, t_lp, st))
         log(f"cpu baseline: {n}x{f} node LP by HiGHS in {t_lp:.2f}s (status {st})")
-        # the next size costs roughly 2^3-3.4x: stop before the budget would be exceeded
-        if spent + 4.0 * (time.perf_counter() - t0) > budget:
+        if (time.perf_counter() - t_start) + 4.0 * (time.perf_counter() - t0) > 0.4 * budget:
             break
     xs = np.log([a * a * b for a, b, _, _ in pts[-3:]])
     ys = np.log([t for _, _, t, _ in pts[-3:]])
     p_exp = float(np.polyfit(xs, ys, 1)[0]) if len(pts) >= 2 else 1.0
     n_l, f_l, t_l, _ = pts[-1]
-    t_ext = t_l * ((N * N * F) / (n_l * n_l * f_l)) ** p_exp
-    sample = ("HiGHS (oracle/solve.py, scipy %s) on the reference formulation (oracle/formulation.py), "
-              "1 thread, one node LP with %d c-fixings per size, same generator; measured %s; "
-              "fit t ~ (N^2 F)^%.2f over the last %d sizes, extrapolated to %dx%d (%.0f s per LP)"
-              % (__import__("scipy").__version__, fix,
-                 ", ".join(f"{a}x{b}: {t:.2f}s" for a, b, t, _ in pts), p_exp, min(3, len(pts)), N, F, t_ext))
-    return {"value": 1.0 / t_ext, "unit": "LP-relaxations/s", "cores": 1, "kind": "port", "sample": sample,
-            "extrapolated": True, "measured": [{"nodes": a, "functions": b, "seconds": t, "status": s}
-                                               for a, b, t, s in pts]}
+    scale = ((N * N * F) / (n_l * n_l * f_l)) ** p_exp
+    # pool throughput at the largest measured size
+    w = max(1, min(workers, os.cpu_count() or 1))
+    m, bnds = model_and_bounds(n_l, f_l, w, seed + 1)
+    sts, _, wall, w_used = lp_batch_cpu(m, bnds, workers=w)
+    pool_lps = len(sts) / wall
+    log(f"cpu baseline: {w_used} workers solved {len(sts)} {n_l}x{f_l} node LPs in {wall:.2f}s "
+        f"({pool_lps:.2f} LP/s)")
+    dnf = _dnf_probe(N, F, seed, max(5.0, budget - (time.perf_counter() - t_start)))
+    value = pool_lps / scale
+    sample = ("HiGHS (oracle/solve.py, scipy %s) on the reference formulation (oracle/formulation.py), node LPs "
+              "with %d c-fixings, same generator. Single-thread times %s; fit t ~ (N^2 F)^%.2f over the last %d "
+              "sizes -> %.0f s per %dx%d LP. Pool: %d worker processes solved %d %dx%d LPs in %.2f s = %.2f LP/s; "
+              "value = that rate / %.0f (the fitted per-LP time ratio to %dx%d). At %dx%d itself: %s"
+              % (__import__("scipy").__version__, fix, ", ".join(f"{a}x{b}: {t:.2f}s" for a, b, t, _ in pts),
+                 p_exp, min(3, len(pts)), t_l * scale, N, F, w_used, len(sts), n_l, f_l, wall, pool_lps, scale,
+                 N, F, N, F, dnf.get("note", "finished the model build in %.1f s" % dnf["seconds"])))
+    return {"value": value, "unit": "LP-relaxations/s", "cores": w_used, "kind": "port", "sample": sample,
+            "extrapolated": True, "pool_lp_per_s_at": {"nodes": n_l, "functions": f_l, "value": pool_lps},
+            "dnf_at_bench_size": dnf,
+            "measured": [{"nodes": a, "functions": b, "seconds": t, "status": s} for a, b, t, s in pts]}
+
+
+def bnb_section(a, rank, world, dev):
+    """The product's own branch-and-bound (core/engine/bnb.py, the search SCIP runs inside
+    pywraplp Solve(), solver.py:35-40) on BASELINE config 3's instance (default 256x128, step-1
+    NeptuneMinDelayAndUtilization), time-limited: certified node LPs per second INSIDE the
+    B&B, nodes, incumbent, bound and gap.  With N ranks the search is the sharded one (subtrees per
+    rank, incumbent / termination all-reduces over RCCL: core/engine/comm.TorchComm)."""
+    from core.engine.bnb import BranchAndBound
+    from core.engine.comm import LocalComm, TorchComm
+    from core.engine.lp import LPModel
+    from core.solvers.neptune.neptune_step import NeptuneStep1CPUMinDelayAndUtilization
+    from core.utils import data_to_solver_input
+    from core.utils.synthetic import synthetic_payload
+    N, F = a.bnb_nodes, a.bnb_functions
+    p = synthetic_payload(N, F, seed=a.seed)
+    data = data_to_solver_input(p, with_db=False)
+    alpha = p["solver"]["args"]["alpha"]
+    st1 = NeptuneStep1CPUMinDelayAndUtilization(alpha=alpha, verbose=False)
+    st1.load_data(data)
+    ub = st1.upper_bound()
+    m = LPModel(data, "MinDelayAndUtilization", step=1, alpha=alpha, max_batch=a.batch + 2)
+    comm = TorchComm(device=dev) if world > 1 else LocalComm()
+    bnb = BranchAndBound(m, data.workload_matrix, data.function_memory_matrix, data.node_memory_matrix,
+                         batch=a.batch, tol=a.tol, max_iters=a.max_iters, time_limit=a.bnb_seconds,
+                         upper_bound=ub * (1 + 1e-6) + 1e-6, comm=comm, check_every=a.check_every,
+                         root_max_iters=a.root_max_iters)
+    m.reset_stats()
+    t0 = time.perf_counter()
+    res = bnb.solve()
+    wall = time.perf_counter() - t0
+    if world > 1:
+        wall = comm.max(wall)
+    m.close()
+    inc = res.objective
+    gap = None if inc is None else (inc - res.bound) / max(1.0, abs(inc))
+    return {"workload": f"synthetic_{N}x{F}_step1_MDU_product_bnb", "time_limit_s": a.bnb_seconds,
+            "status": res.status, "wall_s": wall, "nodes": res.nodes, "leaves": res.leaves, "lps": res.lps,
+            "certified_lps": res.certified, "certified_lp_per_s": res.certified / wall, "nodes_per_s": res.nodes / wall,
+            "lp_iterations": res.lp_iterations, "incumbent": inc, "bound": res.bound, "rel_gap": gap,
+            "ranks": world}
 
 
 class NodeStream:
@@ -279,8 +367,10 @@ def main():
         td.all_reduce(sm, op=td.ReduceOp.SUM)
         wall, gmax = float(mx[0]), float(mx[3])
         n_ok, n_it, n_done = int(sm[1]), int(sm[2]), int(sm[4])
+    m.close()
+    # the product's own B&B (every rank takes part: the sharded search when world > 1)
+    bnb = bnb_section(a, rank, world, dev) if a.bnb_seconds > 0 else None
     if rank != 0:
-        m.close()
         if dist:
             td.destroy_process_group()
         return
@@ -298,7 +388,7 @@ def main():
             traffic = t.get("bytes_per_launch")
     cpu = None
     if world == 1 and a.cpu_budget > 0:
-        cpu = cpu_baseline(N, F, a.seed, a.fix, a.cpu_budget)
+        cpu = cpu_baseline(N, F, a.seed, a.fix, a.cpu_budget, a.cpu_workers)
     out = {
         "metric": "LP-relaxations/sec + objective gap vs reference, 512-node×256-function",
         "value": n_ok / wall,
@@ -327,9 +417,9 @@ def main():
                      "kernel": "x_pass", "algorithmic_bytes_per_launch": per_lp * lps_per_launch,
                      "avg_launch_ms": launch_ms, "sampled_launches": st["x_pass_sampled"]},
         "cpu_baseline": cpu,
+        "bnb": bnb,
     }
     print(json.dumps(out), flush=True)
-    m.close()
     if dist:
         td.destroy_process_group()
 

@@ -129,7 +129,9 @@ int nep_lp_advance(void *model, int32_t min_done, int32_t *n_done, int32_t *done
                    double *primal_obj, int32_t *status, int64_t *iters);
 int nep_lp_active(void *model);
 
-/* z_int (host, n_int) and optionally the dense routing x[i][f][j] (host float, N*F*N) of a slot. */
+/* z_int (host, n_int) and optionally the dense routing x[i][f][j] (host float, N*F*N) of a slot.  For a
+ * certified slot (NEP_LP_OPTIMAL) z_int is the certificate's repaired point — the primal solution
+ * whose objective primal_obj is and whose rows the certificate checked — else the PDHG iterate. */
 int nep_lp_get_solution(void *model, int32_t slot, double *z_int, float *x_dense);
 /* aggregated routing rows (host float, R*N) and the row map (row_f, row_src; src = -1: pooled
  * zero-workload sources of function f, each routed identically). */

@@ -15,6 +15,9 @@ class LocalComm:
     def min(self, v):
         return float(v)
 
+    def max(self, v):
+        return float(v)
+
     def sum(self, v):
         return int(v)
 
@@ -40,6 +43,9 @@ class TorchComm:
 
     def min(self, v):
         return float(self._reduce(float(v), self._d.ReduceOp.MIN, self._t.float64))
+
+    def max(self, v):
+        return float(self._reduce(float(v), self._d.ReduceOp.MAX, self._t.float64))
 
     def sum(self, v):
         return int(self._reduce(int(v), self._d.ReduceOp.SUM, self._t.int64))

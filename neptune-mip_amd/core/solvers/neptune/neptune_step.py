@@ -29,7 +29,7 @@ def make_lp(data, variant, step, max_batch, **kw):
 class NeptuneStepBase(Solver):
     VARIANT = None
 
-    def __init__(self, batch=16, node_limit=20000, time_limit=None, lp_tol=1e-7, lp_max_iters=5000, **kwargs):
+    def __init__(self, batch=16, node_limit=20000, time_limit=None, lp_tol=5e-7, lp_max_iters=5000, **kwargs):
         super().__init__(**kwargs)
         self.batch = batch
         self.node_limit = node_limit
@@ -154,8 +154,10 @@ class NeptuneStep1CPUMinDelayAndUtilization(NeptuneStep1CPUMinUtilization):
         md = np.asarray(self.data.max_delay_matrix, np.float64)
         ub = float(self.alpha)
         if W.sum():
-            mwd = sum(W[f, i] * max(d for d in D[i] if d <= md[f])
-                      for f in range(W.shape[0]) for i in range(W.shape[1]))
+            mwd = 0.0                     # objectives.py:36-43, vectorised over the distinct max delays
+            for mdv in np.unique(md):
+                best = np.where(D <= mdv, D, -np.inf).max(axis=1)
+                mwd += float((W[md == mdv] * best[None, :]).sum())
             if mwd > 0:
                 ub += (1 - self.alpha) * float((W * D.max(axis=1)[None, :]).sum()) / mwd
         return ub

@@ -113,13 +113,12 @@ __global__ __launch_bounds__(256) void compact_write(const T *__restrict__ vals,
 enum { SC_DELAY = 0, SC_BAD_CX, SC_BAD_HANDLE, SC_BAD_MEM, SC_BAD_CPU, SC_BAD_NC, SC_NUSED, SC_COST, SC_HANDLE_MAXDEV,
        SC_CPU_MAXEXCESS, NSC };
 
-__global__ __launch_bounds__(256) void score_pass_f(DeviceView v, int slot, double *__restrict__ cpu_fj,
-                                                    double *__restrict__ fpart) {
+__global__ __launch_bounds__(256) void score_pass_f(DeviceView v, int slot, const double *__restrict__ zi,
+                                                    double *__restrict__ cpu_fj, double *__restrict__ fpart) {
   __shared__ double red[4][4];
   const int f = blockIdx.x;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const float *x = v.x + slot * v.sx;
-  const double *zi = v.zi + slot * v.sint;
   const int r0 = v.frow[f], r1 = v.frow[f + 1];
   const double M = v.M, eps = v.eps;
   double bad_cx = 0.0, delay = 0.0;
@@ -173,12 +172,12 @@ __global__ __launch_bounds__(256) void score_pass_f(DeviceView v, int slot, doub
   }
 }
 
-__global__ __launch_bounds__(256) void score_pass_j(DeviceView v, int slot, const double *__restrict__ cpu_fj,
+__global__ __launch_bounds__(256) void score_pass_j(DeviceView v, const double *__restrict__ zi,
+                                                    const double *__restrict__ cpu_fj,
                                                     const double *__restrict__ node_cost, double budget,
                                                     double *__restrict__ jpart) {
   const int j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= v.N) return;
-  const double *zi = v.zi + slot * v.sint;
   const double M = v.M, eps = v.eps;
   double cpu = 0.0, mem = 0.0, sumc = 0.0;
   for (int f = 0; f < v.F; ++f) {
@@ -268,10 +267,10 @@ hipError_t launch_compact_f64(const double *vals, int rows, int cols, int64_t ld
   return hipGetLastError();
 }
 
-hipError_t launch_score_check(const DeviceView &v, int slot, double *cpu_fj, double *fpart, double *jpart,
-                              const double *node_cost, double budget, double *out, hipStream_t s) {
-  hipLaunchKernelGGL(score_pass_f, dim3(v.F), dim3(256), 0, s, v, slot, cpu_fj, fpart);
-  hipLaunchKernelGGL(score_pass_j, dim3((v.N + 255) / 256), dim3(256), 0, s, v, slot, cpu_fj, node_cost, budget, jpart);
+hipError_t launch_score_check(const DeviceView &v, int slot, const double *zi, double *cpu_fj, double *fpart,
+                              double *jpart, const double *node_cost, double budget, double *out, hipStream_t s) {
+  hipLaunchKernelGGL(score_pass_f, dim3(v.F), dim3(256), 0, s, v, slot, zi, cpu_fj, fpart);
+  hipLaunchKernelGGL(score_pass_j, dim3((v.N + 255) / 256), dim3(256), 0, s, v, zi, cpu_fj, node_cost, budget, jpart);
   hipLaunchKernelGGL(score_final, dim3(1), dim3(256), 0, s, v, fpart, jpart, out);
   return hipGetLastError();
 }

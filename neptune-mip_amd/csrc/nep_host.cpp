@@ -38,8 +38,8 @@ hipError_t launch_compact_f32(const float *vals, int rows, int cols, int64_t ld,
 hipError_t launch_compact_f64(const double *vals, int rows, int cols, int64_t ld, double thr, int round3,
                               int32_t *cnt, int32_t *off, int32_t *orow, int32_t *ocol, double *oval, bool count_only,
                               hipStream_t s);
-hipError_t launch_score_check(const DeviceView &v, int slot, double *cpu_fj, double *fpart, double *jpart,
-                              const double *node_cost, double budget, double *out, hipStream_t s);
+hipError_t launch_score_check(const DeviceView &v, int slot, const double *zi, double *cpu_fj, double *fpart,
+                              double *jpart, const double *node_cost, double budget, double *out, hipStream_t s);
 }  // namespace nep
 
 using namespace nep;
@@ -601,6 +601,7 @@ int setup_dense(Model &m, const nep_model_desc &d) {
   if ((rc = dalloc(m, &v.mask, (size_t)B * v.smask))) return rc;
   if ((rc = dalloc(m, &v.zi, (size_t)B * v.sint))) return rc;
   if ((rc = dalloc(m, &v.zia, (size_t)B * v.sint))) return rc;
+  if ((rc = dalloc(m, &v.zr, (size_t)B * v.sint))) return rc;
   if ((rc = dalloc(m, &v.lb, (size_t)B * v.sint))) return rc;
   if ((rc = dalloc(m, &v.ub, (size_t)B * v.sint))) return rc;
   if ((rc = dalloc(m, &v.y, (size_t)B * v.sdual))) return rc;
@@ -1073,6 +1074,16 @@ int solve_batch(Model &m, int B, const int32_t *slots, const double *lbi, const 
 // ---------------------------------------------------------------------------------------------
 // auxiliary device work on finished slots (nep_aux.hip)
 // ---------------------------------------------------------------------------------------------
+// The solution of a slot: the certificate's repaired point when its LP was certified (that point
+// is the one whose objective and feasibility the certificate proved), else the PDHG iterate.
+int solution_z(Model &m, int slot, const double **z) {
+  int32_t st = 0;
+  HIPCHK(hipMemcpyAsync(&st, &m.v.ctrl[slot].status, sizeof(int32_t), hipMemcpyDeviceToHost, m.stream));
+  HIPCHK(hipStreamSynchronize(m.stream));
+  *z = (st == NEP_LP_OPTIMAL ? m.v.zr : m.v.zi) + (size_t)slot * m.v.sint;
+  return NEP_OK;
+}
+
 int ensure_entries(Model &m, int64_t need) {
   if (need <= m.ecap) return NEP_OK;
   int64_t cap = std::max<int64_t>(need, 4096);
@@ -1146,7 +1157,9 @@ int score_check(Model &m, int slot, double *out) {
     m.d_node_cost = const_cast<double *>(p);
   }
   double *cpu_fj = m.d_score, *fpart = cpu_fj + nfj, *jpart = fpart + nf, *dout = jpart + nj;
-  HIPCHK(launch_score_check(m.v, slot, cpu_fj, fpart, jpart, m.d_node_cost, m.node_budget, dout, m.stream));
+  const double *z = nullptr;
+  if ((rc = solution_z(m, slot, &z))) return rc;
+  HIPCHK(launch_score_check(m.v, slot, z, cpu_fj, fpart, jpart, m.d_node_cost, m.node_budget, dout, m.stream));
   double raw[16] = {0};
   HIPCHK(hipMemcpyAsync(raw, dout, 10 * sizeof(double), hipMemcpyDeviceToHost, m.stream));
   HIPCHK(hipStreamSynchronize(m.stream));
@@ -1238,9 +1251,12 @@ int nep_lp_get_solution(void *model, int32_t slot, double *z_int, float *x_dense
   if (!model) return fail(NEP_ERR_ARG, "null model");
   Model &m = *static_cast<Model *>(model);
   if (slot < 0 || slot >= m.max_batch) return fail(NEP_ERR_ARG, "slot out of range");
-  if (z_int)
-    HIPCHK(hipMemcpyAsync(z_int, m.v.zi + (size_t)slot * m.v.sint, m.il.n_int * sizeof(double), hipMemcpyDeviceToHost,
-                          m.stream));
+  if (z_int) {
+    const double *z = nullptr;
+    int rc = solution_z(m, slot, &z);
+    if (rc) return rc;
+    HIPCHK(hipMemcpyAsync(z_int, z, m.il.n_int * sizeof(double), hipMemcpyDeviceToHost, m.stream));
+  }
   if (x_dense) {
     std::vector<float> xb((size_t)m.R * m.NP);
     HIPCHK(hipMemcpyAsync(xb.data(), m.v.x + (size_t)slot * m.v.sx, xb.size() * sizeof(float), hipMemcpyDeviceToHost,
@@ -1329,8 +1345,10 @@ int nep_lp_allocation_entries(void *model, int32_t slot, double threshold, int64
   Model &m = *static_cast<Model *>(model);
   if (slot < 0 || slot >= m.max_batch) return fail(NEP_ERR_ARG, "slot out of range");
   if (m.busy[slot]) return fail(NEP_ERR_STATE, "slot is still iterating");
-  return compact<double>(m, m.v.zi + (size_t)slot * m.v.sint + m.il.oc, m.F, m.N, m.N, threshold, 0, capacity,
-                         n_entries, fn, dst, nullptr);
+  const double *z = nullptr;
+  int rc = solution_z(m, slot, &z);
+  if (rc) return rc;
+  return compact<double>(m, z + m.il.oc, m.F, m.N, m.N, threshold, 0, capacity, n_entries, fn, dst, nullptr);
 }
 
 int nep_lp_score_check(void *model, int32_t slot, double *out) {

@@ -111,6 +111,7 @@ struct DeviceView {
   float *theta;                          // [R] last simplex threshold of each routing row (a start hint)
   uint8_t *mask;
   double *zi, *zia, *lb, *ub;
+  double *zr;                            // [n_int] the certificate's repaired small variables (last check)
   double *y, *ya, *kz, *kza;             // duals, anchor, activity K z of the iterate and of the anchor
   float *kty;
   double *tpart, *bpart, *npart;

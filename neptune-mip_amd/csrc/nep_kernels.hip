@@ -591,11 +591,14 @@ void x_pass(DeviceView v, const int32_t *__restrict__ slots, int first, int plai
       if (v.step2) {
         const double old = -v.lo[dl.oD1 + idx];
         const double mfr = fmax(lb[il.omf + idx], cr - old), mtr = fmax(lb[il.omt + idx], old - cr);
+        v.zr[slot * v.sint + il.omf + idx] = mfr;
+        v.zr[slot * v.sint + il.omt + idx] = mtr;
         a.res = fmax(a.res, fmax(mfr - ub[il.omf + idx], mtr - ub[il.omt + idx]));
         a.pobj += v.cost_int[il.omf + idx] * mfr + v.cost_int[il.omt + idx] * mtr;
       }
       a.res = fmax(a.res, (loc - hic) / v.rownorm[dl.o2 + idx]);
       a.pobj += v.cost_int[il.oc + idx] * cr;
+      v.zr[slot * v.sint + il.oc + idx] = cr;
       sumc_rep += cr;
       double *rp = v.rpart + slot * v.srpart + (int64_t)f * 2 * NP;
       rp[j] = memf * cr;
@@ -755,6 +758,7 @@ __global__ __launch_bounds__(kNodeThreads) void node_pass(DeviceView v, const in
         const double nr = lon > hin ? lon : fmin(fmax(nn, lon), hin);
         a.res = fmax(a.res, lon - hin);
         a.pobj += v.cost_int[il.on + j] * nr;
+        v.zr[slot * v.sint + il.on + j] = nr;
         score_n_rep = v.score_n_coef * nr;
       }
     }
@@ -870,6 +874,8 @@ __global__ __launch_bounds__(256) void scalar_pass(DeviceView v, const int32_t *
     const double dr = fmax(lb[il.od], K - ar);
     res = fmax(res, fmax(lb[il.oa] - A, dr - Dm));
     pobj += v.cost_int[il.oa] * ar + v.cost_int[il.od] * dr;
+    v.zr[slot * v.sint + il.oa] = ar;
+    v.zr[slot * v.sint + il.od] = dr;
     const double score_rep = tot[TS_SCORE] + tot[NTS + BS_SCORE_N_REP];
     res = fmax(res, row_viol(score_rep, v.lo[dl.oS], v.hi[dl.oS]) / v.rownorm[dl.oS]);
   }

@@ -1,0 +1,88 @@
+"""The device-side helpers around a finished node LP (csrc/nep_aux.hip) against host computations on
+the same engine solution:
+  nep_lp_get_flows          flow[f, j] = sum_i x[i, f, j]  (the B&B's branching / rounding input)
+  nep_lp_routing_entries    the wire format of neptune/utils/output.py:23-31 (x > 0.001, np.round(x, 3))
+  nep_lp_allocation_entries output.py:33-39 (c > 0.001)
+  nep_lp_score_check        efttc/utils/objectives.py scorers + constraints_step1.py checkers
+"""
+import numpy as np
+import pytest
+
+from gpu_cases import build_args
+
+pytestmark = pytest.mark.gpu
+CASES = [("payload", 0), ("syn_8x4_s2_r0.1_NeptuneMinDelayAndUtilization", 0), ("syn_10x5_s4_r0.2_NeptuneMinDelay", 0),
+         ("sim5_NeptuneMinUtilization", 0)]
+
+
+def _solved(name, k, fix_seed=3):
+    from core.engine.lp import LPModel
+    data, variant, step, kw = build_args(name, k)
+    m = LPModel(data, variant, step=step, max_batch=3, **kw)
+    F, N = len(data.functions), len(data.nodes)
+    rng = np.random.default_rng(fix_seed)
+    lb = np.full((3, m.n_int), -np.inf)
+    ub = np.full((3, m.n_int), np.inf)
+    for b in (1, 2):                           # a leaf-like node: every c fixed (a feasible rounding)
+        c = np.zeros((F, N))
+        for f in range(F):
+            c[f, rng.integers(0, N)] = 1.0
+        lb[b, :F * N] = ub[b, :F * N] = c.ravel()
+    r = m.solve(np.arange(3), lb, ub, tol=1e-7, max_iters=50000)
+    return m, data, variant, r
+
+
+def _dense(m, data, slot):
+    z, x = m.solution(slot, dense_x=True)
+    return z, x.astype(np.float64)
+
+
+@pytest.mark.parametrize("name,k", CASES)
+def test_flows_entries_and_checks(name, k):
+    m, data, variant, r = _solved(name, k)
+    F, N = len(data.functions), len(data.nodes)
+    try:
+        for slot in range(3):
+            if int(r["status"][slot]) == 2:
+                continue
+            z, x = _dense(m, data, slot)
+            # flows
+            fl = m.flows([slot])[0]
+            ref = x.sum(axis=0)                             # [f, j]
+            assert np.allclose(fl, ref, rtol=1e-6, atol=1e-6)
+            # routing entries == reference wire format of the dense x
+            row, dst, val = m.routing_entries(slot)
+            xb, rf, rs = m.rows(slot)
+            W = np.asarray(data.workload_matrix)
+            got = {}
+            for rr, j, v in zip(row.tolist(), dst.tolist(), val.tolist()):
+                srcs = [rs[rr]] if rs[rr] >= 0 else [i for i in range(N) if W[rf[rr], i] == 0]
+                for i in srcs:
+                    got[(i, int(rf[rr]), j)] = v
+            ii, ff, jj = np.nonzero(x > 0.001)
+            want = {(i, f, j): float(np.round(x[i, f, j], 3)) for i, f, j in zip(ii, ff, jj)}
+            assert got == want
+            # allocation entries
+            fn, dj = m.allocation_entries(slot)
+            cm = z[:F * N].reshape(F, N)
+            assert sorted(zip(fn.tolist(), dj.tolist())) == sorted(zip(*np.nonzero(cm > 0.001)))
+            # scorers / checkers
+            sc = m.score_check(slot)
+            D, cpr = np.asarray(data.node_delay_matrix), np.asarray(data.core_per_req_matrix)
+            delay = float(np.sum(x * D[:, None, :] * W.T[:, :, None]))
+            assert abs(sc["network_delay"] - delay) <= 1e-6 * max(1.0, abs(delay))
+            flow = x.sum(axis=0)
+            cb = cm != 0
+            bad_cx = int(((flow > np.where(cb, 1e6, 0.0)) | (flow + 1e-6 < np.where(cb, 1.0, 0.0))).sum())
+            assert sc["bad_c_x"] == bad_cx
+            cpu = np.einsum("ifj,fi,fj->j", x, W, cpr)
+            assert sc["bad_cpu"] == int((cpu > np.asarray(data.node_cores_matrix) + 1e-6).sum())
+            mem = (np.asarray(data.function_memory_matrix)[:, None] * cb).sum(axis=0)
+            assert sc["bad_memory"] == int((mem > np.asarray(data.node_memory_matrix)).sum())
+            dev = np.abs(x.sum(axis=2) - 1.0)
+            assert sc["bad_handle"] == int((~(dev < 0.1)).sum())
+            if variant != "MinDelay":
+                n = z[F * N:F * N + N]
+                assert sc["nodes_used"] == int((n != 0).sum())
+    finally:
+        m.close()

