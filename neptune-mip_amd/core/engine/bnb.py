@@ -65,6 +65,7 @@ class BnBResult:
         self.unresolved = 0      # leaves still uncertified after their retry
         self.seconds = 0.0
         self.incumbent_slot = None
+        self.polished = False    # the incumbent's LP was re-solved at the polish tolerance
 
     def as_dict(self):
         return {k: getattr(self, k) for k in ("status", "objective", "bound", "nodes", "leaves", "lps", "certified",
@@ -90,7 +91,7 @@ class BranchAndBound:
 
     def __init__(self, lp, workload, fn_mem, node_mem, batch=16, tol=1e-7, gap=1e-6, max_iters=5000,
                  node_limit=20000, time_limit=None, upper_bound=math.inf, flow_tol=1e-4, log=None, comm=None,
-                 warm=True, root_max_iters=200000, check_every=16):
+                 warm=True, root_max_iters=200000, check_every=16, polish_tol=1e-8, polish_iters=20000):
         self.lp = lp
         self.N, self.F = lp.N, lp.F
         L = lp.layout()
@@ -106,6 +107,10 @@ class BranchAndBound:
         self.tol, self.gap, self.max_iters = tol, gap, max_iters
         self.root_max_iters = max(max_iters, root_max_iters)
         self.check_every = check_every
+        # the final incumbent's LP is re-solved (warm, from its own state) at polish_tol, so the
+        # returned routing also meets the reference's absolute checker tolerances
+        # (efttc/utils/constraints_step1.py:68-78: CPU <= cores + 1e-6)
+        self.polish_tol, self.polish_iters = polish_tol, polish_iters
         self.node_limit, self.time_limit = node_limit, time_limit
         self.ub0 = upper_bound
         self.flow_tol = flow_tol
@@ -124,24 +129,59 @@ class BranchAndBound:
         return fx
 
     def _round(self, node, flow):
-        """Heuristic completion of a node: c = fixed value, else 1 where it carries flow; n = any c.
-        Returns (idx, val) arrays fixing every c and n, or None when visibly infeasible."""
+        """Heuristic completion of a node (a leaf fixing every c and n), or None.
+
+        Memory-aware greedy rounding of the node LP's flows: the fixed c stay as fixed; the free
+        (f, j) are opened in decreasing order of the flow f sends to j while node j's memory
+        (C3, constraints_step1.py:18-23) has room and n[j] is not fixed to 0; a function left without
+        an open destination gets the one it sends most flow to that still has room; n[j] = any c[:, j]
+        (a node fixed open gets its best-fitting function).  The leaf's LP then re-optimises x."""
         F, N, c0, c1 = self.F, self.N, self.c0, self.c1
-        c = (flow.ravel() > self.flow_tol).astype(np.float64)
+        fixed = np.full(F * N, -1.0)
         sel = (node.idx >= c0) & (node.idx < c1)
-        c[node.idx[sel] - c0] = node.val[sel]
+        fixed[node.idx[sel] - c0] = node.val[sel]
+        nfix = np.full(N, -1.0)
+        if self.n_range is not None:
+            n0, n1 = self.n_range
+            seln = (node.idx >= n0) & (node.idx < n1)
+            nfix[node.idx[seln] - n0] = node.val[seln]
+        c = np.where(fixed > 0.5, 1.0, 0.0)
         cm = c.reshape(F, N)
-        if (cm.sum(axis=1) < 1).any():
+        used = (self.fn_mem[:, None] * cm).sum(axis=0)
+        room = self.node_mem + 1e-9
+        if (used > room).any():
             return None
-        if ((self.fn_mem[:, None] * cm).sum(axis=0) > self.node_mem + 1e-9).any():
-            return None
+        fl = flow.ravel().astype(np.float64)
+        closed = (fixed >= 0) | (np.repeat(nfix[None, :] == 0.0, F, axis=0).ravel())
+        cand = np.flatnonzero(~closed & (fl > self.flow_tol))
+        for k in cand[np.argsort(-fl[cand], kind="stable")]:
+            f, j = divmod(int(k), N)
+            if used[j] + self.fn_mem[f] <= room[j]:
+                c[k] = 1.0
+                used[j] += self.fn_mem[f]
+        for f in np.flatnonzero(cm.sum(axis=1) < 1):
+            order = np.argsort(-fl[f * N:(f + 1) * N], kind="stable")
+            for j in order:
+                k = f * N + int(j)
+                if not closed[k] and used[j] + self.fn_mem[f] <= room[j]:
+                    c[k] = 1.0
+                    used[j] += self.fn_mem[f]
+                    break
+            else:
+                return None
         idx = [np.arange(c0, c1)]
         val = [c]
         if self.n_range is not None:
-            n0, n1 = self.n_range
             nv = (cm.sum(axis=0) >= 1).astype(np.float64)
-            seln = (node.idx >= n0) & (node.idx < n1)
-            if (nv[node.idx[seln] - n0] != node.val[seln]).any():
+            for j in np.flatnonzero((nfix == 1.0) & (nv == 0.0)):
+                fs = [f for f in np.argsort(self.fn_mem, kind="stable")
+                      if fixed[f * N + j] < 0 and used[j] + self.fn_mem[f] <= room[j]]
+                if not fs:
+                    return None
+                c[fs[0] * N + j] = 1.0
+                used[j] += self.fn_mem[fs[0]]
+                nv[j] = 1.0
+            if ((nfix == 0.0) & (nv == 1.0)).any():
                 return None
             idx.append(np.arange(n0, n1))
             val.append(nv)
@@ -238,6 +278,7 @@ class BranchAndBound:
                 if pobj < inc - self._gap_abs(inc):
                     inc = pobj
                     res.objective = pobj
+                    self.inc_node = node
                     res.z, _ = self.lp.solution(slot, dense_x=False)
                     if self.warm:
                         self.lp.copy_state(slot, self.inc_slot)   # its x is fetched once, at the end
@@ -281,6 +322,26 @@ class BranchAndBound:
         self.free.append(slot)        # most recently finished last: its state survives longest
         return inc
 
+    def _polish(self, res):
+        """Re-solve the incumbent leaf from its own final state at polish_tol; keep the result when
+        it certifies (the value moves by at most the certificate tolerance)."""
+        lp, slot, node = self.lp, res.incumbent_slot, self.inc_node
+        lb = np.full((1, lp.n_int), -np.inf)
+        ub = np.full((1, lp.n_int), np.inf)
+        lb[0, node.idx] = node.val
+        ub[0, node.idx] = node.val
+        st = lp.submit(np.array([slot], np.int32), lb, ub, tol=self.polish_tol, cutoff=math.inf,
+                       max_iters=self.polish_iters, check_every=self.check_every, warm_start=True)
+        if int(st[0]) == LP_INFEASIBLE:
+            return
+        r = lp.advance(1)
+        while lp.active() > 0:
+            r = lp.advance(1)
+        if len(r["slots"]) and int(r["status"][0]) == LP_OPTIMAL:
+            res.objective = float(r["primal_obj"][0])
+            res.z, _ = lp.solution(slot, dense_x=False)
+            res.polished = True
+
     # ---------------------------------------------------------------------------------------
     def solve(self):
         t0 = time.time()
@@ -296,6 +357,7 @@ class BranchAndBound:
         self.seen_leaves = set()
         self.inflight = {}
         self.keep = set()
+        self.inc_node = None
         nwork = lp.max_batch - self.reserved
         self.free = deque(range(nwork))
         self.slot_gen = [0] * lp.max_batch
@@ -357,6 +419,8 @@ class BranchAndBound:
                 node = self.inflight.pop(slot, None)
                 if node is not None and int(r["status"][i]) not in (LP_INFEASIBLE, LP_CUTOFF):
                     open_bounds.append(max(node.bound, float(r["obj"][i])))
+        if res.objective is not None and res.incumbent_slot is not None and self.polish_tol:
+            self._polish(res)
         open_bounds += [h[0] for h in self.heap] + [n.bound for n in self.pending] + [n.bound for n in self.retry]
         open_bounds += self.unresolved_bounds
         res.bound = min(open_bounds + [inc])

@@ -29,8 +29,8 @@ hipError_t launch_scalar_pass(const DeviceView &v, const int32_t *slots, int nsl
 hipError_t launch_node_bounds(const DeviceView &v, const int32_t *slots, int nslots, const double *base_lb,
                               const double *base_ub, const uint8_t *base_mask, const int32_t *off, const int32_t *idx,
                               const double *cl, const double *cu, int max_chg, hipStream_t s);
-hipError_t launch_init_slot(const DeviceView &v, const int32_t *slots, int nslots, bool warm, double eta,
-                            double omega0, hipStream_t s);
+hipError_t launch_init_slot(const DeviceView &v, const int32_t *slots, const int32_t *exact, int nslots, bool warm,
+                            double eta, double omega0, hipStream_t s);
 hipError_t launch_node_flows(const DeviceView &v, const int32_t *slots, int n, float *out, hipStream_t s);
 hipError_t launch_compact_f32(const float *vals, int rows, int cols, int64_t ld, double thr, int round3,
                               int32_t *cnt, int32_t *off, int32_t *orow, int32_t *ocol, double *oval, bool count_only,
@@ -56,6 +56,12 @@ static int fail(int code, const std::string &msg) {
   } while (0)
 
 static const double INF = std::numeric_limits<double>::infinity();
+// NEP_HALPERN=0 (A/B build variant): plain restarted PDHG — every iteration w' = T(w), the anchor is
+// read only on certificate iterations (restart distances)
+#ifndef NEP_HALPERN
+#define NEP_HALPERN 1
+#endif
+static constexpr bool kHalpern = NEP_HALPERN != 0;
 
 namespace {
 
@@ -88,6 +94,8 @@ struct Model {
   std::vector<int> Kr, Kc;
   std::vector<double> Kv, ftot;
   bool x_coef_nonneg = true;   // every x coefficient outside C1/C2 is >= 0 (W, cpr, D >= 0)
+  bool x_cost_free = true;     // no routing entry carries objective cost (step 2; W == 0)
+  int32_t *d_exact = nullptr;  // per submitted node: the box fixes the objective (Ctrl::exact)
   // node presolve as a sparse change of the base box (presolve_setup / presolve_node)
   bool base_ok = false;
   std::vector<double> base_lb, base_ub, base_amin, base_amax;
@@ -279,7 +287,7 @@ int build(Model &m, const nep_model_desc &d) {
   m.rows.resize(m.R);
   for (int r = 0; r < m.R; ++r)
     m.rows[r] = RowInfo{m.row_m[r], m.row_w[r], m.row_wobj[r], m.row_wsc[r], m.row_src[r], m.row_f[r], 0, 0};
-  m.JB = (N + kWave - 1) / kWave;
+  m.JB = (N + kNodeJ - 1) / kNodeJ;   // node-pass workgroups per LP
 
   // integer-variable layout (variables.py order minus x)
   const int FN = F * N;
@@ -429,6 +437,7 @@ int build(Model &m, const nep_model_desc &d) {
   m.Kr = K.r;
   m.Kc = K.c;
   m.Kv = K.v;
+  for (int r = 0; r < m.R; ++r) m.x_cost_free = m.x_cost_free && m.row_wobj[r] == 0.f;
   m.ftot.assign(F, 0.0);
   for (int r = 0; r < m.R; ++r) m.ftot[m.row_f[r]] += m.row_m[r];
   for (size_t k = 0; k < (size_t)N * N && m.x_coef_nonneg; ++k) m.x_coef_nonneg = D[k] >= 0.0;
@@ -618,6 +627,7 @@ int setup_dense(Model &m, const nep_model_desc &d) {
   v.prm = m.d_prm;
   if ((rc = dalloc(m, &m.d_slots, (size_t)B))) return rc;
   if ((rc = dalloc(m, &m.d_new, (size_t)B))) return rc;
+  if ((rc = dalloc(m, &m.d_exact, (size_t)B))) return rc;
   {
     const double *p = nullptr;
     if ((rc = upload(m, &p, m.base_lb))) return rc;
@@ -876,7 +886,7 @@ int submit(Model &m, int n, const int32_t *slots, const double *lbi, const doubl
   m.prm_host[0] = o.tol;
   m.prm_host[1] = o.cutoff;
   HIPCHK(hipMemcpyAsync(m.d_prm, m.prm_host, sizeof(m.prm_host), hipMemcpyHostToDevice, m.stream));
-  std::vector<int32_t> fresh, off(1, 0), ci;
+  std::vector<int32_t> fresh, off(1, 0), ci, exact;
   std::vector<double> cl, cu;
   const size_t ni = (size_t)m.il.n_int;
   int max_chg = 0;
@@ -888,6 +898,16 @@ int submit(Model &m, int n, const int32_t *slots, const double *lbi, const doubl
     if (!ok) continue;
     m.busy[s] = 1;
     fresh.push_back(s);
+    // the box fixes the objective when the routing carries no cost and every c and n is fixed (a
+    // leaf): mf / mt / allocated / deallocated then follow from c at their cheapest (the repair)
+    bool ex = m.x_cost_free;
+    const double *L = lbi ? lbi + (size_t)b * ni : nullptr, *U = ubi ? ubi + (size_t)b * ni : nullptr;
+    const int n_fix_end = m.has_n ? m.il.on + m.N : m.il.oc + m.F * m.N;
+    for (int k = m.il.oc; ex && k < m.il.oc + m.F * m.N; ++k)
+      ex = L && U && std::max(L[k], m.nat_lb[k]) == std::min(U[k], m.nat_ub[k]);
+    for (int k = m.has_n ? m.il.on : n_fix_end; ex && k < n_fix_end; ++k)
+      ex = L && U && std::max(L[k], m.nat_lb[k]) == std::min(U[k], m.nat_ub[k]);
+    exact.push_back(ex ? 1 : 0);
     off.push_back((int32_t)ci.size());
     max_chg = std::max(max_chg, (int)(ci.size() - c0));
   }
@@ -904,7 +924,8 @@ int submit(Model &m, int n, const int32_t *slots, const double *lbi, const doubl
   }
   HIPCHK(launch_node_bounds(v, m.d_new, nf, m.d_base_lb, m.d_base_ub, m.d_base_mask, m.d_chg_off, m.d_chg_idx,
                             m.d_chg_lb, m.d_chg_ub, max_chg, m.stream));
-  HIPCHK(launch_init_slot(v, m.d_new, nf, o.warm_start != 0, m.eta, m.omega0, m.stream));
+  HIPCHK(hipMemcpyAsync(m.d_exact, exact.data(), nf * sizeof(int32_t), hipMemcpyHostToDevice, m.stream));
+  HIPCHK(launch_init_slot(v, m.d_new, m.d_exact, nf, o.warm_start != 0, m.eta, m.omega0, m.stream));
   HIPCHK(launch_x_pass(v, m.d_new, nf, false, true, true, true, 0, m.stream));
   HIPCHK(launch_node_pass(v, m.d_new, nf, false, true, true, true, 0, m.stream));
   HIPCHK(launch_scalar_pass(v, m.d_new, nf, false, true, true, true, 0, o.check_every, m.stream));
@@ -931,7 +952,7 @@ hipError_t block_graph(Model &m, int na, hipGraphExec_t *out) {
     hipError_t le = hipSuccess;
     for (int it = 0; it < ce && le == hipSuccess; ++it) {
       const bool check = it == 0, first = it == 1;
-      const bool plain = ce < 4 || it == 0 || it == ce - 1;
+      const bool plain = !kHalpern || ce < 4 || it == 0 || it == ce - 1;
       le = launch_x_pass(m.v, m.d_slots, na, check, false, first, plain, it, m.stream);
       if (le == hipSuccess) le = launch_node_pass(m.v, m.d_slots, na, check, false, first, plain, it, m.stream);
       if (le == hipSuccess && (m.step2 || check))
@@ -987,7 +1008,7 @@ int advance(Model &m, int min_done, int32_t *n_done, int32_t *done, double *obj,
     }
     for (int it = 0; it < ce && eager; ++it) {
       const bool check = it == 0, first = it == 1;
-      const bool plain = ce < 4 || it == 0 || it == ce - 1;
+      const bool plain = !kHalpern || ce < 4 || it == 0 || it == ce - 1;
       const bool sample = it == sample_it;
       if (sample) HIPCHK(hipEventRecord(m.ev0, m.stream));
       HIPCHK(launch_x_pass(v, m.d_slots, na, check, false, first, plain, it, m.stream));

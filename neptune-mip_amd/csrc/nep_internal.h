@@ -46,6 +46,7 @@ using anchor_t = float;
 constexpr int kWave = 64;
 constexpr int kNodeWaves = 16;           // waves per node-pass workgroup (each sums F/16 functions)
 constexpr int kNodeThreads = kWave * kNodeWaves;
+constexpr int kNodeJ = 16;               // nodes per node-pass workgroup
 
 // one routing row (32 B, one scalar load): pooled-row weight m (1 for a single source), workload
 // w = W[f, src], objective weight wobj (cost of x[r, j] = wobj * D[src, j]), score-row weight wsc
@@ -79,7 +80,8 @@ struct Ctrl {
   double omega_lo, omega_hi;
   int64_t k, k_since_restart, ks_base;   // ks_base: Halpern counter at the block's first iteration
   int64_t max_iters;                     // this LP's iteration limit (nep_lp_opts of its submit)
-  int32_t status, active, restart_pending, pad;
+  int32_t status, active, restart_pending;
+  int32_t exact;                         // 1: the node box fixes the objective (see scalar_pass)
 };
 
 // row-family offsets inside y / kz / rho / lo / hi

@@ -176,51 +176,43 @@ __device__ __forceinline__ float4 ld4(const float *p) { return *reinterpret_cast
 // the routing-state streams (x, anchor): read and written once per iteration, so non-temporal
 // (NEP_NT): they then do not push the delay rows D[src, :] — re-read by every row of a function
 // and by every LP slot — out of the XCD's L2
-__device__ __forceinline__ f32x4 ld_x4(const float *p) {
-#if NEP_NT
-  return __builtin_nontemporal_load(reinterpret_cast<const f32x4 *>(p));
-#else
+// `nt` is chosen per launch by the host (launch_x_tw): only when the iterating slots' routing state
+// exceeds what the 256 MiB Infinity Cache can keep between iterations — a lone root LP (55 MB of x +
+// anchor at 512x256) streams from the Infinity Cache with default-policy loads, 32 slots (1.8 GB)
+// cannot.
+__device__ __forceinline__ f32x4 ld_x4(const float *p, bool nt) {
+  if (NEP_NT && nt) return __builtin_nontemporal_load(reinterpret_cast<const f32x4 *>(p));
   return *reinterpret_cast<const f32x4 *>(p);
-#endif
 }
-__device__ __forceinline__ void st_x4(float *p, f32x4 v) {
-#if NEP_NT
-  __builtin_nontemporal_store(v, reinterpret_cast<f32x4 *>(p));
-#else
-  *reinterpret_cast<f32x4 *>(p) = v;
-#endif
+__device__ __forceinline__ void st_x4(float *p, f32x4 v, bool nt) {
+  if (NEP_NT && nt) __builtin_nontemporal_store(v, reinterpret_cast<f32x4 *>(p));
+  else *reinterpret_cast<f32x4 *>(p) = v;
 }
-__device__ __forceinline__ anc4 ld_a4(const anchor_t *p) {
-#if NEP_NT
-  return __builtin_nontemporal_load(reinterpret_cast<const anc4 *>(p));
-#else
+__device__ __forceinline__ anc4 ld_a4(const anchor_t *p, bool nt) {
+  if (NEP_NT && nt) return __builtin_nontemporal_load(reinterpret_cast<const anc4 *>(p));
   return *reinterpret_cast<const anc4 *>(p);
-#endif
 }
-__device__ __forceinline__ void st_a4(anchor_t *p, anc4 v) {
-#if NEP_NT
-  __builtin_nontemporal_store(v, reinterpret_cast<anc4 *>(p));
-#else
-  *reinterpret_cast<anc4 *>(p) = v;
-#endif
+__device__ __forceinline__ void st_a4(anchor_t *p, anc4 v, bool nt) {
+  if (NEP_NT && nt) __builtin_nontemporal_store(v, reinterpret_cast<anc4 *>(p));
+  else *reinterpret_cast<anc4 *>(p) = v;
 }
 
 // one routing row's operands: x̄ row, delay row D[src, :] (if the row has delay-weighted
 // coefficients) and the anchor row (if needed)
 template <int CPL>
 __device__ __forceinline__ void load_row(const float *__restrict__ xrow, const float *__restrict__ drow,
-                                         const anchor_t *__restrict__ arow, bool nd, bool na, int lane, int NP,
-                                         float (&xo)[4 * CPL], float (&dout)[4 * CPL], float (&ao)[4 * CPL]) {
+                                         const anchor_t *__restrict__ arow, bool nd, bool na, bool nt, int lane,
+                                         int NP, float (&xo)[4 * CPL], float (&dout)[4 * CPL], float (&ao)[4 * CPL]) {
 #pragma unroll
   for (int q = 0; q < CPL; ++q) {
     const int j0 = 4 * (lane + kWave * q);
     f32x4 a = {0.f, 0.f, 0.f, 0.f}, an = a;
     float4 d = make_float4(0.f, 0.f, 0.f, 0.f);
     if (j0 < NP) {
-      a = ld_x4(xrow + j0);
+      a = ld_x4(xrow + j0, nt);
       if (nd) d = ld4(drow + j0);
       if (na) {
-        const anc4 h = ld_a4(arow + j0);
+        const anc4 h = ld_a4(arow + j0, nt);
         an = f32x4{(float)h.x, (float)h.y, (float)h.z, (float)h.w};
       }
     }
@@ -251,7 +243,8 @@ __device__ __forceinline__ void load_row(const float *__restrict__ xrow, const f
 // certificate iterations (fp64 Lagrangian terms, 143 VGPRs) run at 3 waves per SIMD.
 template <int CPL, bool CHECK, bool INIT, int TW>
 __global__ __launch_bounds__(kWave * TW) __attribute__((amdgpu_waves_per_eu(CHECK ? 2 : (TW == 16 ? 4 : 6), 8)))
-void x_pass(DeviceView v, const int32_t *__restrict__ slots, int first, int plain, int it, int nslots) {
+void x_pass(DeviceView v, const int32_t *__restrict__ slots, int first, int plain, int it, int nslots, int nt_i) {
+  const bool nt = nt_i != 0;
   constexpr int E = 4 * CPL;
   extern __shared__ __attribute__((aligned(16))) float lds[];   // [2][TW][NP] accumulators + [2][NP] constants
   __shared__ double lds_s[TW][NTS + NBS];
@@ -341,7 +334,7 @@ void x_pass(DeviceView v, const int32_t *__restrict__ slots, int first, int plai
     // (0.575 vs 0.591 ms per launch before the LDS accumulators; other waves hide the latency)
     float xc[E], dc[E], ac[E];
     load_row<CPL>(x + (int64_t)r * NP, v.D + (int64_t)(ri.src < 0 ? 0 : ri.src) * NP, xa + (int64_t)r * NP, nd,
-                  need_anchor, lane, NP, xc, dc, ac);
+                  need_anchor, nt, lane, NP, xc, dc, ac);
     const float m = ri.m, w = ri.w, wobj = ri.wobj, wsc = ri.wsc;
     float kx[E], cy5[E];
 #pragma unroll
@@ -468,10 +461,10 @@ void x_pass(DeviceView v, const int32_t *__restrict__ slots, int first, int plai
           const int e = 4 * q + t;
           o[t] = halp ? lam * (2.f * xn[e] - xc[e]) + (1.f - lam) * xav[e] : xn[e];
         }
-        st_x4(xrow + j0, f32x4{o[0], o[1], o[2], o[3]});
+        st_x4(xrow + j0, f32x4{o[0], o[1], o[2], o[3]}, nt);
         if (restart)
           st_a4(arow + j0, anc4{(anchor_t)xav[4 * q], (anchor_t)xav[4 * q + 1], (anchor_t)xav[4 * q + 2],
-                                (anchor_t)xav[4 * q + 3]});
+                                (anchor_t)xav[4 * q + 3]}, nt);
       }
     }
     float sc = 0.f;
@@ -596,7 +589,7 @@ void x_pass(DeviceView v, const int32_t *__restrict__ slots, int first, int plai
         a.res = fmax(a.res, fmax(mfr - ub[il.omf + idx], mtr - ub[il.omt + idx]));
         a.pobj += v.cost_int[il.omf + idx] * mfr + v.cost_int[il.omt + idx] * mtr;
       }
-      a.res = fmax(a.res, (loc - hic) / v.rownorm[dl.o2 + idx]);
+      a.res = fmax(a.res, loc - hic);   // absolute: a fixed-open (f, j) needs flow >= c - eps
       a.pobj += v.cost_int[il.oc + idx] * cr;
       v.zr[slot * v.sint + il.oc + idx] = cr;
       sumc_rep += cr;
@@ -673,52 +666,61 @@ __device__ __forceinline__ void write_bpart(double *bp, const SmallAcc &a, doubl
 template <bool CHECK, bool INIT>
 __global__ __launch_bounds__(kNodeThreads) void node_pass(DeviceView v, const int32_t *__restrict__ slots, int first,
                                                           int plain, int it) {
-  __shared__ double red[kNodeWaves][5][kWave];
+  // kNodeJ nodes per workgroup (so a lone LP still spreads its F x 3 x N shares over N / kNodeJ
+  // workgroups): thread t sums the shares of node t % kNodeJ over function group t / kNodeJ
+  constexpr int NG = kNodeThreads / kNodeJ;
+  __shared__ double red[5][NG][kNodeJ];
   const int jb = blockIdx.x;
   const int slot = slots[blockIdx.y];
   Ctrl *ctrl = v.ctrl + slot;
   if (!ctrl->active) return;
   const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x >> 6;
-  const int j = jb * kWave + lane;
-  const bool valid = j < v.N;
   const int NP = v.NP, F = v.F;
   {
-    const int per = (F + kNodeWaves - 1) / kNodeWaves;
-    const int f0 = wave * per, f1 = min(F, f0 + per);
+    const int jj = threadIdx.x % kNodeJ, g = threadIdx.x / kNodeJ;
+    const int jl = jb * kNodeJ + jj;
+    const int per = (F + NG - 1) / NG;
+    const int f0 = g * per, f1 = min(F, f0 + per);
     double memc = 0.0, sumc = 0.0, U = 0.0, memr = 0.0, sumr = 0.0;
-    if (valid) {
+    if (jl < v.N) {
       const double *np_ = v.npart + slot * v.snpart;
-#pragma unroll 4
       for (int f = f0; f < f1; ++f) {
         const double *p = np_ + (int64_t)f * 3 * NP;
-        memc += p[j];
-        sumc += p[NP + j];
-        U += p[2 * NP + j];
+        memc += p[jl];
+        sumc += p[NP + jl];
+        U += p[2 * NP + jl];
       }
       if (CHECK) {
         const double *rp = v.rpart + slot * v.srpart;
         for (int f = f0; f < f1; ++f) {
-          memr += rp[(int64_t)f * 2 * NP + j];
-          sumr += rp[(int64_t)f * 2 * NP + NP + j];
+          memr += rp[(int64_t)f * 2 * NP + jl];
+          sumr += rp[(int64_t)f * 2 * NP + NP + jl];
         }
       }
     }
-    red[wave][0][lane] = memc;
-    red[wave][1][lane] = sumc;
-    red[wave][2][lane] = U;
-    red[wave][3][lane] = memr;
-    red[wave][4][lane] = sumr;
+    red[0][g][jj] = memc;
+    red[1][g][jj] = sumc;
+    red[2][g][jj] = U;
+    red[3][g][jj] = memr;
+    red[4][g][jj] = sumr;
   }
   __syncthreads();
   if (wave != 0) return;
+  // wave 0: lane (< kNodeJ) = node; fixed-order sums over the function groups
+  const int j = jb * kNodeJ + lane;
+  const bool valid = lane < kNodeJ && j < v.N;
   double memc = 0.0, sumc = 0.0, U = 0.0, memr = 0.0, sumr = 0.0;
-#pragma unroll
-  for (int wv = 0; wv < kNodeWaves; ++wv) {
-    memc += red[wv][0][lane];
-    sumc += red[wv][1][lane];
-    U += red[wv][2][lane];
-    memr += red[wv][3][lane];
-    sumr += red[wv][4][lane];
+  if (lane < kNodeJ) {
+#pragma unroll 8
+    for (int g = 0; g < NG; ++g) {
+      memc += red[0][g][lane];
+      sumc += red[1][g][lane];
+      U += red[2][g][lane];
+      if (CHECK) {
+        memr += red[3][g][lane];
+        sumr += red[4][g][lane];
+      }
+    }
   }
   const DualLayout &dl = v.dl;
   const IntLayout &il = v.il;
@@ -881,12 +883,24 @@ __global__ __launch_bounds__(256) void scalar_pass(DeviceView v, const int32_t *
   }
   const double lagr = a.lagr;
   const double gap = pobj - lagr;
+  const double tol = v.prm[0], cutoff = v.prm[1];
   ctrl->pobj = pobj;
+  if (ctrl->exact && isfinite(pobj) && res <= tol) {
+    // The node box fixes every variable that carries cost (a leaf of a model whose routing has no
+    // cost: step 2, or W == 0): every feasible point has the repaired point's objective, so a
+    // feasible repaired point IS an LP optimum and its objective the LP value.
+    ctrl->lagr = pobj;
+    ctrl->best_lagr = fmax(ctrl->best_lagr, pobj);
+    ctrl->pres = res;
+    ctrl->gap = 0.0;
+    ctrl->status = 0;
+    ctrl->active = 0;
+    return;
+  }
   ctrl->lagr = lagr;
   if (lagr > ctrl->best_lagr) ctrl->best_lagr = lagr;
   ctrl->pres = res;
   ctrl->gap = gap;
-  const double tol = v.prm[0], cutoff = v.prm[1];
   if (isfinite(lagr) && res <= tol && gap <= tol * fmax(1.0, fabs(lagr))) {
     ctrl->status = 0; ctrl->active = 0; return;
   }
@@ -922,7 +936,8 @@ __global__ __launch_bounds__(256) void scalar_pass(DeviceView v, const int32_t *
 }
 
 // cold / warm initialisation of a slot (x̄ ← 0 for cold; the init passes project it)
-__global__ void init_slot(DeviceView v, const int32_t *__restrict__ slots, int warm, double eta, double omega0) {
+__global__ void init_slot(DeviceView v, const int32_t *__restrict__ slots, const int32_t *__restrict__ exact, int warm,
+                          double eta, double omega0) {
   const int slot = slots[blockIdx.y];
   Ctrl *ctrl = v.ctrl + slot;
   const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -956,6 +971,7 @@ __global__ void init_slot(DeviceView v, const int32_t *__restrict__ slots, int w
     ctrl->sigma = eta * ctrl->omega;
     ctrl->status = 1;
     ctrl->active = 1;
+    ctrl->exact = exact[blockIdx.y];
     ctrl->max_iters = v.max_iters;
     ctrl->restart_pending = 1;
     ctrl->best_lagr = -INFINITY;
@@ -1008,10 +1024,12 @@ static hipError_t launch_x_tw(const DeviceView &v, const int32_t *slots, int nsl
   const size_t lds = (size_t)(2 * TW + 2) * v.NP * sizeof(float) +
                     (check ? (size_t)2 * TW * v.NP * sizeof(float) + 2 * v.NP * sizeof(double) : 0);
   const int fi = first ? 1 : 0, pl = plain ? 1 : 0;
-  if (init) hipLaunchKernelGGL((x_pass<CPL, false, true, TW>), grid, block, lds, s, v, slots, fi, pl, it, nslots);
+  // non-temporal routing streams only when the iterating slots' x + anchor exceed ~160 MB (see ld_x4)
+  const int nt = (double)nslots * 2.0 * (double)v.sx * sizeof(float) > 160e6 ? 1 : 0;
+  if (init) hipLaunchKernelGGL((x_pass<CPL, false, true, TW>), grid, block, lds, s, v, slots, fi, pl, it, nslots, nt);
   else if (check)
-    hipLaunchKernelGGL((x_pass<CPL, true, false, TW>), grid, block, lds, s, v, slots, fi, pl, it, nslots);
-  else hipLaunchKernelGGL((x_pass<CPL, false, false, TW>), grid, block, lds, s, v, slots, fi, pl, it, nslots);
+    hipLaunchKernelGGL((x_pass<CPL, true, false, TW>), grid, block, lds, s, v, slots, fi, pl, it, nslots, nt);
+  else hipLaunchKernelGGL((x_pass<CPL, false, false, TW>), grid, block, lds, s, v, slots, fi, pl, it, nslots, nt);
   return hipGetLastError();
 }
 
@@ -1053,7 +1071,7 @@ hipError_t launch_x_pass(const DeviceView &v, const int32_t *slots, int nslots, 
 hipError_t launch_node_pass(const DeviceView &v, const int32_t *slots, int nslots, bool check, bool init, bool first,
                             bool plain, int it, hipStream_t s) {
   const int fi = first ? 1 : 0, pl = plain ? 1 : 0;
-  dim3 grid(v.JB, nslots), block(kNodeThreads);
+  dim3 grid(v.JB, nslots), block(kNodeThreads);   // JB = ceil(N / kNodeJ)
   if (init) hipLaunchKernelGGL((node_pass<false, true>), grid, block, 0, s, v, slots, fi, pl, it);
   else if (check) hipLaunchKernelGGL((node_pass<true, false>), grid, block, 0, s, v, slots, fi, pl, it);
   else hipLaunchKernelGGL((node_pass<false, false>), grid, block, 0, s, v, slots, fi, pl, it);
@@ -1084,10 +1102,10 @@ hipError_t launch_node_bounds(const DeviceView &v, const int32_t *slots, int nsl
   return hipGetLastError();
 }
 
-hipError_t launch_init_slot(const DeviceView &v, const int32_t *slots, int nslots, bool warm, double eta,
-                            double omega0, hipStream_t s) {
+hipError_t launch_init_slot(const DeviceView &v, const int32_t *slots, const int32_t *exact, int nslots, bool warm,
+                            double eta, double omega0, hipStream_t s) {
   dim3 grid(256, nslots), block(256);
-  hipLaunchKernelGGL(init_slot, grid, block, 0, s, v, slots, warm ? 1 : 0, eta, omega0);
+  hipLaunchKernelGGL(init_slot, grid, block, 0, s, v, slots, exact, warm ? 1 : 0, eta, omega0);
   return hipGetLastError();
 }
 

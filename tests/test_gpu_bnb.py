@@ -1,0 +1,89 @@
+"""The product's streaming branch-and-bound (core/engine/bnb.py) on the MI355X engine at BASELINE
+config 2/3 sizes, time-limited: it must return a feasible placement whose objective it reports
+correctly, a valid bound, and device-side helpers (flows, scorer/checker) consistent with it.  And
+the NeptuneWithEFTTC* flows (EF-TTC step 1 + the NEPTUNE step-2 MIP on the GPU) reproduce the
+reference's recorded scores (tests/golden/efttc.json)."""
+import json
+import math
+import os
+
+import numpy as np
+import pytest
+
+from golden_util import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+
+def _mdu_objective(data, alpha, x, z):
+    """objectives.py:30-53 on a placement (dense x[i,f,j], z = c[F*N] + n[N])."""
+    W, D = np.asarray(data.workload_matrix, float), np.asarray(data.node_delay_matrix, float)
+    md = np.asarray(data.max_delay_matrix, float)
+    F, N = W.shape
+    obj = alpha / N * float(np.sum(z[F * N:F * N + N]))
+    if W.sum():
+        mwd = 0.0
+        for mdv in np.unique(md):
+            best = np.where(D <= mdv, D, -np.inf).max(axis=1)
+            mwd += float((W[md == mdv] * best[None, :]).sum())
+        obj += (1 - alpha) / mwd * float(np.sum(x * D[:, None, :] * W.T[:, :, None]))
+    return obj
+
+
+@pytest.mark.parametrize("n,f,seconds", [(64, 32, 25.0), (256, 128, 40.0)])
+def test_product_bnb_time_limited(n, f, seconds):
+    from core.engine.bnb import INFEASIBLE, BranchAndBound
+    from core.engine.lp import LPModel
+    from core.solvers.efttc import scoring
+    from core.solvers.neptune.neptune_step import NeptuneStep1CPUMinDelayAndUtilization
+    from core.utils import data_to_solver_input
+    from core.utils.synthetic import synthetic_payload
+    p = synthetic_payload(n, f, seed=0)
+    data = data_to_solver_input(p, with_db=False)
+    st1 = NeptuneStep1CPUMinDelayAndUtilization(alpha=0.5, verbose=False)
+    st1.load_data(data)
+    ub = st1.upper_bound()
+    m = LPModel(data, "MinDelayAndUtilization", step=1, alpha=0.5, max_batch=34)
+    try:
+        res = BranchAndBound(m, data.workload_matrix, data.function_memory_matrix, data.node_memory_matrix,
+                             batch=32, tol=5e-7, time_limit=seconds, upper_bound=ub * (1 + 1e-6) + 1e-6).solve()
+    finally:
+        m.close()
+    print(res.as_dict())
+    assert res.status != INFEASIBLE and res.objective is not None, res.as_dict()
+    assert res.certified > 0 and res.nodes > 0
+    assert res.bound <= res.objective + 1e-9
+    x, z = np.asarray(res.x, np.float64), np.asarray(res.z, np.float64)
+    c = z[:f * n].reshape(f, n)
+    assert np.all((np.abs(c) < 1e-9) | (np.abs(c - 1) < 1e-9)), "incumbent c not integral"
+    # the incumbent's objective, recomputed on the host, is the reported one
+    assert abs(_mdu_objective(data, 0.5, x, z) - res.objective) <= 1e-6 * max(1.0, abs(res.objective))
+    # and it is feasible by the reference's own checkers (efttc/utils/constraints_step1.py)
+    assert scoring.cpu_usage_ok(data, x)
+    mem = (np.asarray(data.function_memory_matrix)[:, None] * (c > 0.5)).sum(axis=0)
+    assert np.all(mem <= np.asarray(data.node_memory_matrix) + 1e-9)
+    assert np.all(np.abs(x.sum(axis=2) - 1.0) < 1e-4)
+
+
+with open(os.path.join(GOLDEN, "efttc.json")) as fh:
+    E = json.load(fh)
+WITH = sorted(k for k in E if k.split("|")[1].startswith("NeptuneWithEFTTC") and "error" not in E[k]
+              and k.split("|")[0] in ("payload", "testpy", "sim0_NeptuneMinDelay", "sim3_NeptuneMinUtilization",
+                                      "syn_4x3_s0_r0.5_NeptuneMinDelayAndUtilization"))
+
+
+@pytest.mark.parametrize("key", WITH)
+def test_neptune_with_efttc_flow_on_gpu(key):
+    import core.solvers as S
+    from core.utils import data_to_solver_input
+    name, stype = key.split("|")
+    with open(os.path.join(GOLDEN, "inputs", name + ".json")) as fh:
+        p = json.load(fh)
+    data = data_to_solver_input(p, workload_coeff=p.get("workload_coeff", 1), with_db=False)
+    solver = S.SOLVERS[stype](**p["solver"].get("args", {}))
+    solver.load_data(data)
+    solver.solve()
+    score = solver.score()
+    ref = E[key]["response"]["score"]
+    assert math.isclose(score["step1"], ref["step1"], rel_tol=1e-9, abs_tol=1e-9), (score, ref)
+    assert abs(score["step2"] - ref["step2"]) <= 1e-6 * max(1.0, abs(ref["step2"])), (score, ref)
