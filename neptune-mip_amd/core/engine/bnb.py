@@ -69,7 +69,7 @@ class BnBResult:
 
     def as_dict(self):
         return {k: getattr(self, k) for k in ("status", "objective", "bound", "nodes", "leaves", "lps", "certified",
-                                              "lp_iterations", "unresolved", "seconds")}
+                                              "lp_iterations", "unresolved", "seconds", "polished")}
 
 
 class _Node:

@@ -9,6 +9,7 @@
 #include <climits>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <limits>
 #include <memory>
@@ -565,6 +566,9 @@ int setup_device(Model &m, int max_batch, void *stream) {
   v.M = m.M; v.eps = m.eps; v.sigma4 = m.sigma4; v.cost_n = m.cost_n; v.score_n_coef = m.score_n_coef;
   v.w_dis = m.w_dis;
   v.dl = m.dl; v.il = m.il;
+  v.rs_suff = 0.2; v.rs_nec = 0.9; v.rs_art = 0.36; v.omega_smooth = 0.5;   // necessary 0.9: DESIGN.md §4
+  if (const char *e = std::getenv("NEP_RESTART")) std::sscanf(e, "%lf,%lf,%lf", &v.rs_suff, &v.rs_nec, &v.rs_art);
+  if (const char *e = std::getenv("NEP_OMEGA_SMOOTH")) v.omega_smooth = std::atof(e);
   int rc;
   if ((rc = upload(m, &v.rows, m.rows))) return rc;
   if ((rc = upload(m, &v.frow, m.frow))) return rc;

@@ -125,6 +125,10 @@ struct DeviceView {
   // passed by value would stay frozen at capture time.
   const double *prm;
   double warm_omega_floor;               // warm starts: primal weight kept >= this x the parent's (0: off)
+  // restart rule on the fixed-point residual (sufficient / necessary / artificial, PDLP's 0.2 / 0.8 /
+  // 0.36; necessary 0.9 here, measured) and the primal-weight smoothing (0.5); NEP_RESTART /
+  // NEP_OMEGA_SMOOTH override them
+  double rs_suff, rs_nec, rs_art, omega_smooth;
   int64_t max_iters;
 };
 

@@ -912,14 +912,14 @@ __global__ __launch_bounds__(256) void scalar_pass(DeviceView v, const int32_t *
   const double w = ctrl->omega;
   const double fpr = sqrt(w * a.mvz + a.mvy / w);
   if (ctrl->last_restart_fpr < 0) ctrl->last_restart_fpr = fpr;
-  const bool restart = (fpr <= 0.2 * ctrl->last_restart_fpr) ||
-                       (fpr <= 0.8 * ctrl->last_restart_fpr && fpr > ctrl->prev_fpr) ||
-                       (ctrl->k_since_restart >= 0.36 * ctrl->k);
+  const bool restart = (fpr <= v.rs_suff * ctrl->last_restart_fpr) ||
+                       (fpr <= v.rs_nec * ctrl->last_restart_fpr && fpr > ctrl->prev_fpr) ||
+                       (ctrl->k_since_restart >= v.rs_art * ctrl->k);
   ctrl->prev_fpr = fpr;
   if (restart) {
     const double dz = sqrt(a.dsz), dy = sqrt(a.dsy);
     if (dz > 1e-10 && dy > 1e-10) {
-      double nw = exp(0.5 * log(dy / dz) + 0.5 * log(w));
+      double nw = exp(v.omega_smooth * log(dy / dz) + (1.0 - v.omega_smooth) * log(w));
       nw = fmin(fmax(nw, ctrl->omega_lo), ctrl->omega_hi);
       ctrl->omega = nw;
       ctrl->tau = ctrl->eta / nw;

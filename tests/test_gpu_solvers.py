@@ -1,7 +1,9 @@
 """GPU twin of tests/test_bnb_cpu.py: the drop-in NEPTUNE solver classes (core/solvers) run the
 two-step flow on the MI355X engine — batched PDHG node LPs, warm-started from their parents
 (core/engine/bnb.py) — and must reproduce the reference flow's responses recorded in the golden
-fixtures: both scores, and the placement where the reference optimum is unique."""
+fixtures: both scores, and — where the reference optimum is unique — the whole wire format
+(allocations; routing sources, and for functions with one open destination — where the routing is
+forced — every destination and rounded value)."""
 import pytest
 
 from golden_util import golden, payload
@@ -35,5 +37,16 @@ def test_solver_flow_on_gpu(name):
     assert _close(score["step2"], ref["score"]["step2"]), (score, ref["score"])
     done = [m for m in G[name]["models"] if m["status"] == 0]
     if done and done[-1].get("mip_tied") is False:
+        # unique optimum: the whole wire format — allocations, and every routing entry's source,
+        # function, destination and rounded value (output.py:23-39) within 1e-3
         assert c == ref["cpu_allocations"]
-        assert set(x) == set(ref["cpu_routing_rules"])
+        rr = ref["cpu_routing_rules"]
+        assert set(x) == set(rr)
+        for src, fns in rr.items():
+            assert set(x[src]) == set(fns), (src, x[src], fns)
+            for fn, dsts in fns.items():
+                if len(ref["cpu_allocations"].get(fn, {})) != 1:
+                    continue     # several open destinations: the routing may have tied optima
+                assert set(x[src][fn]) == set(dsts), (src, fn, x[src][fn], dsts)
+                for dst, val in dsts.items():
+                    assert abs(x[src][fn][dst] - val) <= 1e-3, (src, fn, dst, x[src][fn][dst], val)
