@@ -29,7 +29,7 @@ source aggregation.  `achieved` = those bytes x the LPs one sampled launch carri
 HIP-event duration on the engine's own stream, averaged over one steady-state launch per
 64-iteration block (nep_get_stats).  `traffic` is read from profiles/traffic.json (separate
 rocprofv3 --pmc passes, tools/traffic.py) when it was measured on this exact
-workload, else null.
+workload (else null), per LP-iteration and scaled to the LPs of the average sampled launch.
 
 CPU baseline.  The oracle (HiGHS on the reference's formulation restated as one CSR, oracle/)
 timed on rank 0's host, bounded by `--cpu-budget` seconds (see `cpu_baseline`).
@@ -380,12 +380,16 @@ def main():
     lps_per_launch = st["x_pass_lp_iters"] / max(1, st["x_pass_sampled"])
     achieved = per_lp * lps_per_launch / (launch_ms * 1e-3) / 1e9 if launch_ms > 0 else 0.0
     workload = workload_name(a)
-    traffic = None
+    traffic = traffic_ratio = None
     if os.path.exists(a.traffic):
         with open(a.traffic) as fh:
             t = json.load(fh)
         if t.get("workload") == workload:
-            traffic = t.get("bytes_per_launch")
+            # measured per LP-iteration (PMC passes at t["lps_per_launch"] slots), scaled to the LPs
+            # of this run's average sampled launch so it compares with `achieved`'s bytes
+            per_lp_iter = t["bytes_per_launch"] / max(1, t.get("lps_per_launch", 1))
+            traffic = per_lp_iter * lps_per_launch
+            traffic_ratio = per_lp_iter / per_lp
     cpu = None
     if world == 1 and a.cpu_budget > 0:
         cpu = cpu_baseline(N, F, a.seed, a.fix, a.cpu_budget, a.cpu_workers)
@@ -413,7 +417,7 @@ def main():
                "slot_utilisation_rank0": util,
                "root_obj": root_obj, "root_iters": root_iters},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_over_algorithmic": traffic_ratio,
                      "kernel": "x_pass", "algorithmic_bytes_per_launch": per_lp * lps_per_launch,
                      "avg_launch_ms": launch_ms, "sampled_launches": st["x_pass_sampled"]},
         "cpu_baseline": cpu,

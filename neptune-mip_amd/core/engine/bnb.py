@@ -91,7 +91,8 @@ class BranchAndBound:
 
     def __init__(self, lp, workload, fn_mem, node_mem, batch=16, tol=1e-7, gap=1e-6, max_iters=5000,
                  node_limit=20000, time_limit=None, upper_bound=math.inf, flow_tol=1e-4, log=None, comm=None,
-                 warm=True, root_max_iters=200000, check_every=16, polish_tol=1e-8, polish_iters=20000):
+                 warm=True, root_max_iters=200000, check_every=16, polish_tol=1e-8, polish_iters=20000,
+                 seed_leaves=None, prune=None):
         self.lp = lp
         self.N, self.F = lp.N, lp.F
         L = lp.layout()
@@ -111,6 +112,10 @@ class BranchAndBound:
         # returned routing also meets the reference's absolute checker tolerances
         # (efttc/utils/constraints_step1.py:68-78: CPU <= cores + 1e-6)
         self.polish_tol, self.polish_iters = polish_tol, polish_iters
+        # seed_leaves: [(idx, val)] placements queued as leaves after the root (primal starts);
+        # prune(idx, val) -> True: the node's fixings admit no integral solution (model-specific cut)
+        self.seed_leaves = list(seed_leaves or [])
+        self.prune = prune
         self.node_limit, self.time_limit = node_limit, time_limit
         self.ub0 = upper_bound
         self.flow_tol = flow_tol
@@ -128,14 +133,17 @@ class BranchAndBound:
         fx[node.idx] = True
         return fx
 
-    def _round(self, node, flow):
+    def _round(self, node, flow, zc=None):
         """Heuristic completion of a node (a leaf fixing every c and n), or None.
 
-        Memory-aware greedy rounding of the node LP's flows: the fixed c stay as fixed; the free
-        (f, j) are opened in decreasing order of the flow f sends to j while node j's memory
-        (C3, constraints_step1.py:18-23) has room and n[j] is not fixed to 0; a function left without
-        an open destination gets the one it sends most flow to that still has room; n[j] = any c[:, j]
-        (a node fixed open gets its best-fitting function).  The leaf's LP then re-optimises x."""
+        Memory-aware greedy rounding of the node LP: the fixed c stay as fixed; the free c the LP
+        holds at >= 1/2 (zc, the LP's c) are opened first, largest first, then the free (f, j) in
+        decreasing order of the flow f sends to j, while node j's memory (C3,
+        constraints_step1.py:18-23) has room and n[j] is not fixed to 0; a function left without an
+        open destination gets the one with the largest LP c, then flow, that still has room;
+        n[j] = any c[:, j] (a node fixed open gets its best-fitting function).  The leaf's LP then
+        re-optimises x.  (Opening the LP's near-integral c first is what keeps step 2's placement
+        next to the old allocation: its LP c sits at old wherever no flow forces a move.)"""
         F, N, c0, c1 = self.F, self.N, self.c0, self.c1
         fixed = np.full(F * N, -1.0)
         sel = (node.idx >= c0) & (node.idx < c1)
@@ -153,14 +161,21 @@ class BranchAndBound:
             return None
         fl = flow.ravel().astype(np.float64)
         closed = (fixed >= 0) | (np.repeat(nfix[None, :] == 0.0, F, axis=0).ravel())
-        cand = np.flatnonzero(~closed & (fl > self.flow_tol))
+        zc = np.zeros(F * N) if zc is None else np.asarray(zc, np.float64).ravel()
+        half = np.flatnonzero(~closed & (zc >= 0.5))
+        for k in half[np.argsort(-zc[half], kind="stable")]:
+            f, j = divmod(int(k), N)
+            if used[j] + self.fn_mem[f] <= room[j]:
+                c[k] = 1.0
+                used[j] += self.fn_mem[f]
+        cand = np.flatnonzero(~closed & (c < 0.5) & (fl > self.flow_tol))
         for k in cand[np.argsort(-fl[cand], kind="stable")]:
             f, j = divmod(int(k), N)
             if used[j] + self.fn_mem[f] <= room[j]:
                 c[k] = 1.0
                 used[j] += self.fn_mem[f]
         for f in np.flatnonzero(cm.sum(axis=1) < 1):
-            order = np.argsort(-fl[f * N:(f + 1) * N], kind="stable")
+            order = np.lexsort((-fl[f * N:(f + 1) * N], -zc[f * N:(f + 1) * N]))
             for j in order:
                 k = f * N + int(j)
                 if not closed[k] and used[j] + self.fn_mem[f] <= room[j]:
@@ -268,6 +283,14 @@ class BranchAndBound:
             if self.warm and st not in (LP_INFEASIBLE, LP_CUTOFF):
                 self.lp.copy_state(slot, self.root_slot)   # every later node can start from the root
             self.root_ready = True
+            me0 = (slot, self.slot_gen[slot])
+            for idx, val in self.seed_leaves:
+                if self.prune is None or not self.prune(idx, val):
+                    key = np.packbits(np.asarray(val) > 0.5).tobytes()
+                    if key not in self.seen_leaves:
+                        self.seen_leaves.add(key)
+                        self.pending.append(_Node(-math.inf, np.asarray(idx), np.asarray(val, np.float64), LEAF,
+                                                  me0, 1))
         if st in (LP_INFEASIBLE, LP_CUTOFF):
             self.free.append(slot)
             return inc
@@ -305,7 +328,8 @@ class BranchAndBound:
         res.nodes += 1
         flow = self.lp.flows([slot])[0]
         me = (slot, self.slot_gen[slot])
-        leaf = self._round(node, flow)
+        z, _ = self.lp.solution(slot, dense_x=False)
+        leaf = self._round(node, flow, z[self.c0:self.c1])
         if leaf is not None:
             key = np.packbits(leaf[1] > 0.5).tobytes()
             if key not in self.seen_leaves:
@@ -316,6 +340,8 @@ class BranchAndBound:
             for v in (1.0, 0.0):
                 idx = np.append(node.idx, var)
                 val = np.append(node.val, v)
+                if self.prune is not None and self.prune(idx, val):
+                    continue
                 kind = LEAF if len(idx) >= self._nb else NODE
                 heapq.heappush(self.heap, (bound, -(node.depth + 1), next(self.seq),
                                            _Node(bound, idx, val, kind, me, node.depth + 1)))
@@ -350,7 +376,9 @@ class BranchAndBound:
         comm = self.comm
         inc = math.inf
         self.seq = itertools.count()
-        self.heap = [(-math.inf, 0, next(self.seq), _Node(-math.inf, np.zeros(0, np.int64), np.zeros(0), NODE, None, 0))]
+        root = _Node(-math.inf, np.zeros(0, np.int64), np.zeros(0), NODE, None, 0)
+        self.heap = [] if (self.prune is not None and self.prune(root.idx, root.val)) else \
+            [(-math.inf, 0, next(self.seq), root)]
         self.pending = deque()       # rounding leaves
         self.retry = deque()         # uncertified leaves, re-solved once with the root budget
         self.unresolved_bounds = []

@@ -63,6 +63,14 @@ class NeptuneStepBase(Solver):
     def upper_bound(self):
         return math.inf
 
+    def seed_leaves(self, layout):
+        """Placements to try as leaves right after the root (a B&B primal start); none by default."""
+        return []
+
+    def integer_prune(self):
+        """A node test valid for integral solutions only (a B&B cut), or None."""
+        return None
+
     def solve(self):
         self.init_objective()
         data = self.data
@@ -76,7 +84,8 @@ class NeptuneStepBase(Solver):
                                  batch=self.batch, tol=self.lp_tol, max_iters=self.lp_max_iters,
                                  node_limit=self.node_limit,
                                  time_limit=self.time_limit,
-                                 upper_bound=ub * (1 + 1e-6) + 1e-6 if math.isfinite(ub) else ub, log=self.log)
+                                 upper_bound=ub * (1 + 1e-6) + 1e-6 if math.isfinite(ub) else ub, log=self.log,
+                                 seed_leaves=self.seed_leaves(model.layout()), prune=self.integer_prune())
             res = bnb.solve()
             layout = model.layout()
         finally:
@@ -189,6 +198,48 @@ class NeptuneStep2Base(NeptuneStepBase):
         # allocated / deallocated <= 0
         FN = len(self.data.nodes) * len(self.data.functions)
         return float(FN) * FN
+
+    def seed_leaves(self, layout):
+        """Step 2's natural primal starts (neptune.py:18-30): the step-1 placement (it meets the
+        score row by construction) and the old allocation (no moves)."""
+        d = self.data
+        F, N = len(d.functions), len(d.nodes)
+        c0, c1 = layout["c"]
+        cands = []
+        prev = getattr(d, "prev_c", None)
+        if prev is not None and np.size(prev) == F * N:
+            cands.append((np.asarray(prev, np.float64).reshape(F, N) > 0.5).astype(np.float64))
+        old = np.asarray(d.old_allocations_matrix, np.float64).reshape(F, N)
+        cands.append((old > 0.5).astype(np.float64))
+        out = []
+        for c in cands:
+            if (c.sum(axis=1) < 1).any():
+                continue
+            idx, val = [np.arange(c0, c1)], [c.ravel()]
+            if layout.get("n") is not None:
+                n0, n1 = layout["n"]
+                idx.append(np.arange(n0, n1))
+                val.append((c.sum(axis=0) >= 1).astype(np.float64))
+            out.append((np.concatenate(idx), np.concatenate(val)))
+        return out
+
+    def integer_prune(self):
+        """Delete mode (constraints_step2.py:36-44 with D3) needs sum c <= sum old; an integral
+        placement opens at least one destination per function (C2 with C4: every function's
+        requests flow somewhere, and c >= flow / M > 0 makes c = 1 there).  So a node whose
+        functions need more openings than sum old allows holds no integral solution."""
+        if self.mode != "delete":
+            return None
+        d = self.data
+        F, N = len(d.functions), len(d.nodes)
+        sum_old = float(np.asarray(d.old_allocations_matrix, np.float64).sum())
+
+        def prune(idx, val):
+            ones = np.zeros(F)
+            sel = (idx < F * N) & (val > 0.5)          # c occupies z_int[0 : F*N] (neptune_lp.h)
+            np.add.at(ones, idx[sel] // N, 1.0)
+            return float(np.maximum(ones, 1.0).sum()) > sum_old + 1e-9
+        return prune
 
     def results(self):
         # neptune_step2.py:43-51: no side effects on data (the prints are logs only)
