@@ -92,7 +92,7 @@ class BranchAndBound:
     def __init__(self, lp, workload, fn_mem, node_mem, batch=16, tol=1e-7, gap=1e-6, max_iters=5000,
                  node_limit=20000, time_limit=None, upper_bound=math.inf, flow_tol=1e-4, log=None, comm=None,
                  warm=True, root_max_iters=200000, check_every=16, polish_tol=1e-8, polish_iters=20000,
-                 seed_leaves=None, prune=None):
+                 seed_leaves=None, integer_bound=None):
         self.lp = lp
         self.N, self.F = lp.N, lp.F
         L = lp.layout()
@@ -113,9 +113,10 @@ class BranchAndBound:
         # (efttc/utils/constraints_step1.py:68-78: CPU <= cores + 1e-6)
         self.polish_tol, self.polish_iters = polish_tol, polish_iters
         # seed_leaves: [(idx, val)] placements queued as leaves after the root (primal starts);
-        # prune(idx, val) -> True: the node's fixings admit no integral solution (model-specific cut)
+        # integer_bound(idx, val): a model-specific lower bound valid for every integral completion of
+        # a node's fixings (+inf: none); a node's bound is the larger of it and its parent LP's
         self.seed_leaves = list(seed_leaves or [])
-        self.prune = prune
+        self.integer_bound = integer_bound
         self.node_limit, self.time_limit = node_limit, time_limit
         self.ub0 = upper_bound
         self.flow_tol = flow_tol
@@ -128,12 +129,15 @@ class BranchAndBound:
     def _gap_abs(self, inc):
         return self.gap * max(1.0, abs(inc)) if math.isfinite(inc) else 0.0
 
+    def _ibound(self, idx, val):
+        return -math.inf if self.integer_bound is None else float(self.integer_bound(idx, val))
+
     def _fixed(self, node):
         fx = np.zeros(self.lp.n_int, bool)
         fx[node.idx] = True
         return fx
 
-    def _round(self, node, flow, zc=None):
+    def _round(self, node, flow, zc=None, by_flow=True):
         """Heuristic completion of a node (a leaf fixing every c and n), or None.
 
         Memory-aware greedy rounding of the node LP: the fixed c stay as fixed; the free c the LP
@@ -143,7 +147,9 @@ class BranchAndBound:
         open destination gets the one with the largest LP c, then flow, that still has room;
         n[j] = any c[:, j] (a node fixed open gets its best-fitting function).  The leaf's LP then
         re-optimises x.  (Opening the LP's near-integral c first is what keeps step 2's placement
-        next to the old allocation: its LP c sits at old wherever no flow forces a move.)"""
+        next to the old allocation: its LP c sits at old wherever no flow forces a move.)
+        by_flow=False skips the flow pass: the fewest openings the LP's c allows (a leaf whose x
+        must then fit the CPU rows with those openings only)."""
         F, N, c0, c1 = self.F, self.N, self.c0, self.c1
         fixed = np.full(F * N, -1.0)
         sel = (node.idx >= c0) & (node.idx < c1)
@@ -168,7 +174,7 @@ class BranchAndBound:
             if used[j] + self.fn_mem[f] <= room[j]:
                 c[k] = 1.0
                 used[j] += self.fn_mem[f]
-        cand = np.flatnonzero(~closed & (c < 0.5) & (fl > self.flow_tol))
+        cand = np.flatnonzero(~closed & (c < 0.5) & (fl > self.flow_tol)) if by_flow else np.zeros(0, np.int64)
         for k in cand[np.argsort(-fl[cand], kind="stable")]:
             f, j = divmod(int(k), N)
             if used[j] + self.fn_mem[f] <= room[j]:
@@ -285,12 +291,13 @@ class BranchAndBound:
             self.root_ready = True
             me0 = (slot, self.slot_gen[slot])
             for idx, val in self.seed_leaves:
-                if self.prune is None or not self.prune(idx, val):
-                    key = np.packbits(np.asarray(val) > 0.5).tobytes()
+                idx, val = np.asarray(idx), np.asarray(val, np.float64)
+                lb = self._ibound(idx, val)
+                if lb < math.inf:
+                    key = np.packbits(val > 0.5).tobytes()
                     if key not in self.seen_leaves:
                         self.seen_leaves.add(key)
-                        self.pending.append(_Node(-math.inf, np.asarray(idx), np.asarray(val, np.float64), LEAF,
-                                                  me0, 1))
+                        self.pending.append(_Node(lb, idx, val, LEAF, me0, 1))
         if st in (LP_INFEASIBLE, LP_CUTOFF):
             self.free.append(slot)
             return inc
@@ -329,22 +336,26 @@ class BranchAndBound:
         flow = self.lp.flows([slot])[0]
         me = (slot, self.slot_gen[slot])
         z, _ = self.lp.solution(slot, dense_x=False)
-        leaf = self._round(node, flow, z[self.c0:self.c1])
-        if leaf is not None:
-            key = np.packbits(leaf[1] > 0.5).tobytes()
-            if key not in self.seen_leaves:
-                self.seen_leaves.add(key)
-                self.pending.append(_Node(bound, leaf[0], leaf[1], LEAF, me, node.depth + 1))
+        for by_flow in (False, True):
+            leaf = self._round(node, flow, z[self.c0:self.c1], by_flow)
+            if leaf is not None:
+                key = np.packbits(leaf[1] > 0.5).tobytes()
+                if key not in self.seen_leaves:
+                    self.seen_leaves.add(key)
+                    lb = max(bound, self._ibound(*leaf))
+                    if lb < inc - self._gap_abs(inc):
+                        self.pending.append(_Node(lb, leaf[0], leaf[1], LEAF, me, node.depth + 1))
         var = self._branch_var(node, flow, slot)
         if var is not None:
             for v in (1.0, 0.0):
                 idx = np.append(node.idx, var)
                 val = np.append(node.val, v)
-                if self.prune is not None and self.prune(idx, val):
+                cb = max(bound, self._ibound(idx, val))
+                if cb >= inc - self._gap_abs(inc):
                     continue
                 kind = LEAF if len(idx) >= self._nb else NODE
-                heapq.heappush(self.heap, (bound, -(node.depth + 1), next(self.seq),
-                                           _Node(bound, idx, val, kind, me, node.depth + 1)))
+                heapq.heappush(self.heap, (cb, -(node.depth + 1), next(self.seq),
+                                           _Node(cb, idx, val, kind, me, node.depth + 1)))
         self.free.append(slot)        # most recently finished last: its state survives longest
         return inc
 
@@ -376,9 +387,9 @@ class BranchAndBound:
         comm = self.comm
         inc = math.inf
         self.seq = itertools.count()
-        root = _Node(-math.inf, np.zeros(0, np.int64), np.zeros(0), NODE, None, 0)
-        self.heap = [] if (self.prune is not None and self.prune(root.idx, root.val)) else \
-            [(-math.inf, 0, next(self.seq), root)]
+        rb = self._ibound(np.zeros(0, np.int64), np.zeros(0))
+        root = _Node(rb, np.zeros(0, np.int64), np.zeros(0), NODE, None, 0)
+        self.heap = [] if rb == math.inf else [(rb, 0, next(self.seq), root)]
         self.pending = deque()       # rounding leaves
         self.retry = deque()         # uncertified leaves, re-solved once with the root budget
         self.unresolved_bounds = []
@@ -422,6 +433,8 @@ class BranchAndBound:
                     node = self.retry.popleft()
                 elif self.pending:
                     node = self.pending.popleft()
+                    if node.bound >= inc - self._gap_abs(inc):
+                        continue
                 else:
                     _, _, _, node = heapq.heappop(self.heap)
                     if node.bound >= inc - self._gap_abs(inc):

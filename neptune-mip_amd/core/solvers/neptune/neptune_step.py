@@ -67,8 +67,9 @@ class NeptuneStepBase(Solver):
         """Placements to try as leaves right after the root (a B&B primal start); none by default."""
         return []
 
-    def integer_prune(self):
-        """A node test valid for integral solutions only (a B&B cut), or None."""
+    def integer_bound(self):
+        """bound(idx, val): a lower bound on the objective of every integral completion of a node's
+        fixings (+inf: none exists), or None."""
         return None
 
     def solve(self):
@@ -85,7 +86,7 @@ class NeptuneStepBase(Solver):
                                  node_limit=self.node_limit,
                                  time_limit=self.time_limit,
                                  upper_bound=ub * (1 + 1e-6) + 1e-6 if math.isfinite(ub) else ub, log=self.log,
-                                 seed_leaves=self.seed_leaves(model.layout()), prune=self.integer_prune())
+                                 seed_leaves=self.seed_leaves(model.layout()), integer_bound=self.integer_bound())
             res = bnb.solve()
             layout = model.layout()
         finally:
@@ -223,23 +224,45 @@ class NeptuneStep2Base(NeptuneStepBase):
             out.append((np.concatenate(idx), np.concatenate(val)))
         return out
 
-    def integer_prune(self):
-        """Delete mode (constraints_step2.py:36-44 with D3) needs sum c <= sum old; an integral
-        placement opens at least one destination per function (C2 with C4: every function's
-        requests flow somewhere, and c >= flow / M > 0 makes c = 1 there).  So a node whose
-        functions need more openings than sum old allows holds no integral solution."""
-        if self.mode != "delete":
-            return None
+    def integer_bound(self):
+        """The step-2 objective over integral placements, bounded from the node's c fixings.
+
+        With c binary, A = #(c=1, old=0) additions, R = #(c=0, old=1) removals and O = sum old,
+        minimize_disruption (objectives.py:55-63, w = F*N) under constrain_migrations
+        (constraints_step2.py:19-33) is w(A+R) + (w-1) allocated + (w+1) deallocated with
+          create (:47-54): sum c >= O and the optimum A + (2w-1) R,
+          delete (:36-44): sum c <= O and the optimum (2w+1) A - R.
+        Every function needs an open destination (constraints_step1.py:27-35 with :5-15: its rows
+        route somewhere and c >= flow / M), so A is at least the fixed additions plus one per
+        function that no fixed-1 c and no free old c can cover.  The bound is the closed form at
+        those least A, R (largest R for delete), +inf when the sum-c condition cannot hold."""
         d = self.data
         F, N = len(d.functions), len(d.nodes)
-        sum_old = float(np.asarray(d.old_allocations_matrix, np.float64).sum())
+        FN = F * N
+        w = float(FN)
+        old = (np.asarray(d.old_allocations_matrix, np.float64).reshape(FN) > 0.5)
+        O = float(old.sum())
+        create = self.mode == "create"
 
-        def prune(idx, val):
-            ones = np.zeros(F)
-            sel = (idx < F * N) & (val > 0.5)          # c occupies z_int[0 : F*N] (neptune_lp.h)
-            np.add.at(ones, idx[sel] // N, 1.0)
-            return float(np.maximum(ones, 1.0).sum()) > sum_old + 1e-9
-        return prune
+        def bound(idx, val):
+            fx = np.full(FN, -1.0)
+            sel = idx < FN                                    # c occupies z_int[0 : F*N] (neptune_lp.h)
+            fx[idx[sel]] = val[sel]
+            one, zero = fx > 0.5, (fx >= 0) & (fx < 0.5)
+            add_fixed = float((one & ~old).sum())
+            rem_fixed = float((zero & old).sum())
+            covered = (one | (old & ~zero)).reshape(F, N).any(axis=1)
+            A = add_fixed + float((~covered).sum())
+            if create:
+                if FN - float(zero.sum()) < O:
+                    return math.inf
+                return A + (2 * w - 1) * rem_fixed
+            ones_f = one.reshape(F, N).sum(axis=1)
+            if float(np.maximum(ones_f, 1.0).sum()) > O + 1e-9:
+                return math.inf
+            R_max = O - float((one & old).sum())
+            return (2 * w + 1) * A - R_max
+        return bound
 
     def results(self):
         # neptune_step2.py:43-51: no side effects on data (the prints are logs only)

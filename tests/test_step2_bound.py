@@ -1,0 +1,76 @@
+"""The step-2 integral bound (core/solvers/neptune/neptune_step.py NeptuneStep2Base.integer_bound)
+against brute force on the reference formulation: for every binary c that covers each function
+(constraints_step1.py:5-35), minimize_disruption (objectives.py:55-63) is minimised over the integer
+moved_from / moved_to / allocated / deallocated (variables.py:29-33, constraints_step2.py:5-54) by
+enumeration.  The bound must never exceed the best completion of a node's fixings, must equal it on
+complete fixings, and must be +inf exactly when no completion exists."""
+import itertools
+import math
+import types
+
+import numpy as np
+import pytest
+
+
+def _objective(c, old, mode):
+    """min over the integer step-2 variables for a fixed binary c (None: infeasible)."""
+    w = old.size
+    A = int(((c == 1) & (old == 0)).sum())
+    R = int(((c == 0) & (old == 1)).sum())
+    O, C = int(old.sum()), int(c.sum())
+    best = None
+    for al in range(-w, 1):
+        if al > O - C:
+            continue
+        for de in range(-w, 1):
+            if de > C - O:
+                continue
+            if mode == "delete" and de + al + O - C < 0:
+                continue
+            if mode == "create" and de + al - O + C < 0:
+                continue
+            v = w * (A + R) + (w - 1) * al + (w + 1) * de
+            best = v if best is None else min(best, v)
+    return best
+
+
+def _solver(F, N, old, mode):
+    from core.solvers.neptune.neptune_step import NeptuneStep2Base
+    s = NeptuneStep2Base.__new__(NeptuneStep2Base)
+    s.mode = mode
+    s.data = types.SimpleNamespace(functions=list(range(F)), nodes=list(range(N)),
+                                   old_allocations_matrix=old.reshape(F, N).astype(float))
+    return s.integer_bound()
+
+
+@pytest.mark.parametrize("mode", ["delete", "create"])
+@pytest.mark.parametrize("seed", range(6))
+def test_step2_integer_bound_brute_force(mode, seed):
+    rng = np.random.default_rng(seed)
+    F, N = 2, 3
+    FN = F * N
+    old = (rng.random(FN) < 0.4).astype(int)
+    bound = _solver(F, N, old, mode)
+    values = {}
+    for bits in itertools.product((0, 1), repeat=FN):
+        c = np.array(bits)
+        if (c.reshape(F, N).sum(axis=1) < 1).any():
+            continue
+        values[bits] = _objective(c, old, mode)
+    # random partial fixings, plus the empty and every complete one
+    fixings = [np.zeros(0, np.int64)] + [rng.permutation(FN)[:k] for k in range(1, FN) for _ in range(4)]
+    for idx in fixings:
+        for vals in itertools.product((0, 1), repeat=len(idx)):
+            val = np.array(vals, float)
+            comp = [v for bits, v in values.items() if v is not None
+                    and all(bits[i] == int(x) for i, x in zip(idx, val))]
+            b = bound(np.asarray(idx, np.int64), val)
+            if not comp:
+                continue                      # a bound may stay finite without a completion
+            assert b <= min(comp) + 1e-9, (idx, val, b, min(comp))
+    for bits, v in values.items():
+        b = bound(np.arange(FN), np.array(bits, float))
+        if v is None:
+            assert b == math.inf, (bits, b)
+        else:
+            assert b == v, (bits, b, v)
