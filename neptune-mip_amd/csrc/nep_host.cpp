@@ -25,6 +25,7 @@ hipError_t launch_x_pass(const DeviceView &v, const int32_t *slots, int nslots, 
                          bool plain, int it, hipStream_t s);
 hipError_t launch_node_pass(const DeviceView &v, const int32_t *slots, int nslots, bool check, bool init, bool first,
                             bool plain, int it, hipStream_t s);
+hipError_t launch_dblock_pass(const DeviceView &v, const int32_t *slots, int nslots, hipStream_t s);
 hipError_t launch_scalar_pass(const DeviceView &v, const int32_t *slots, int nslots, bool check, bool init,
                               bool first, bool plain, int it, int block_len, hipStream_t s);
 hipError_t launch_node_bounds(const DeviceView &v, const int32_t *slots, int nslots, const double *base_lb,
@@ -957,7 +958,8 @@ hipError_t block_graph(Model &m, int na, hipGraphExec_t *out) {
     for (int it = 0; it < ce && le == hipSuccess; ++it) {
       const bool check = it == 0, first = it == 1;
       const bool plain = !kHalpern || ce < 4 || it == 0 || it == ce - 1;
-      le = launch_x_pass(m.v, m.d_slots, na, check, false, first, plain, it, m.stream);
+      if (check && m.step2) le = launch_dblock_pass(m.v, m.d_slots, na, m.stream);
+      if (le == hipSuccess) le = launch_x_pass(m.v, m.d_slots, na, check, false, first, plain, it, m.stream);
       if (le == hipSuccess) le = launch_node_pass(m.v, m.d_slots, na, check, false, first, plain, it, m.stream);
       if (le == hipSuccess && (m.step2 || check))
         le = launch_scalar_pass(m.v, m.d_slots, na, check, false, first, plain, it, ce, m.stream);
@@ -1014,6 +1016,7 @@ int advance(Model &m, int min_done, int32_t *n_done, int32_t *done, double *obj,
       const bool check = it == 0, first = it == 1;
       const bool plain = !kHalpern || ce < 4 || it == 0 || it == ce - 1;
       const bool sample = it == sample_it;
+      if (check && m.step2) HIPCHK(launch_dblock_pass(v, m.d_slots, na, m.stream));
       if (sample) HIPCHK(hipEventRecord(m.ev0, m.stream));
       HIPCHK(launch_x_pass(v, m.d_slots, na, check, false, first, plain, it, m.stream));
       if (sample) HIPCHK(hipEventRecord(m.ev1, m.stream));

@@ -68,8 +68,12 @@ enum {
   BS_MOVE_Z, BS_MOVE_Y, BS_DIST_Z, BS_DIST_Y,
   BS_SUMC_REP,       // certificate: sum over (f,j) of the repaired c (step-2 rows D3/D4)
   BS_SCORE_N_REP,    // certificate: score-row n part of the repaired n
-  NBS
+  BS_LAGR_D,         // step 2: the disruption block's share of the Lagrangian (c, moved, a, d; D1-D4)
+  BS_TLO, BS_THI,    // step 2: sum over (f,j) of the node box of c (the range of sum c)
+  BS_LK0,            // step 2: the disruption block kept exact, one sum per price lambda_k of sum c
+  NBS = BS_LK0 + 6   //   (kNLam candidates; DESIGN.md §4 "Disruption block")
 };
+constexpr int kNLam = 6;
 // BS_POBJ / BS_RES carry, on certificate iterations, the objective of the REPAIRED small variables and
 // the max violation of the rows at the repaired point (DESIGN.md §4 "Certificate").
 

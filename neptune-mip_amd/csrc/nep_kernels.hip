@@ -94,7 +94,44 @@ __device__ __forceinline__ double row_viol(double a, double lo, double hi) {
 
 struct SmallAcc {
   double lagr = 0, pobj = 0, res = 0, mvz = 0, mvy = 0, dsz = 0, dsy = 0;
+  double lagrD = 0;   // Lagrangian terms of the step-2 disruption block (dblk calls)
 };
+
+// ---------------------------------------------------------------------------------------------
+// Step-2 disruption block kept exact in the bound (DESIGN.md §4 "Disruption block").  The rows
+// D1/D2 (moved_from/to vs c and old), D3a/D3b/D4 (allocated / deallocated vs sum c) carry duals
+// against costs F*N, F*N +- 1: fp32-level relative noise on them moves the plain Lagrangian by ~1e-5
+// (tools/dblock_probe.py), more than the 1e-6 certificate allows.  Instead of dualising them, the
+// bound minimises the block exactly: sum c is relaxed to a free T priced by lambda, each (f, j) takes
+// min over (c, mf, mt) of (r' - lambda) c + cmf mf + cmt mt on its box and D1/D2 (a piecewise-linear
+// function of c: its minimum is at an end or a kink), and G(lambda) = min over (a, d, T) of
+// ca a + cd d + lambda T on the boxes and D3a/D3b/D4 (a 3-variable LP: the best vertex).  For every
+// lambda that is a valid lower bound; kNLam candidates are evaluated in the same pass: the PDHG's own
+// price of sum c and the slopes +-ca, +-cd, 0 that the optimal price takes unless a D3 cap binds.
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ void dblock_lambdas(const DeviceView &v, const double *y, double (&lam)[kNLam]) {
+  const double ca = v.cost_int[v.il.oa], cd = v.cost_int[v.il.od];
+  lam[0] = -y[v.dl.oD3a] + y[v.dl.oD3b] + v.sigma4 * y[v.dl.oD4];
+  lam[1] = -cd;
+  lam[2] = ca;
+  lam[3] = -ca;
+  lam[4] = cd;
+  lam[5] = 0.0;
+}
+
+// min over c of (r - lam) c + cmf max(lmf, c - old) + cmt max(lmt, old - c), c in [clo, chi]
+__device__ __forceinline__ double dblock_item(double r, double lam, double old, double cmf, double lmf, double cmt,
+                                              double lmt, double clo, double chi) {
+  if (clo > chi) return INFINITY;
+  const double pts[4] = {clo, chi, fmin(fmax(old + lmf, clo), chi), fmin(fmax(old - lmt, clo), chi)};
+  double best = INFINITY;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const double c = pts[q];
+    best = fmin(best, (r - lam) * c + cmf * fmax(lmf, c - old) + cmt * fmax(lmt, old - c));
+  }
+  return best;
+}
 
 // Dual half-step of one row.  Returns the new *iterate* y'; `act` is the row activity at the T
 // output (K·[x̂, ẑ]).  On a Halpern iteration y' = λ(2ŷ − y) + (1 − λ)y_anchor and the iterate's
@@ -102,7 +139,7 @@ struct SmallAcc {
 template <bool CHECK, bool INIT>
 __device__ __forceinline__ double dual_step(const DeviceView &v, double *y, double *ya, double *kz, double *kza,
                                             int row, double act, double yold, double sigma, bool copy_anchor,
-                                            bool halp, double lam, SmallAcc &a) {
+                                            bool halp, double lam, SmallAcc &a, bool dblk = false) {
   const double lo = v.lo[row], hi = v.hi[row];
   const double kold = kz[row];
   double yanc, kanc;
@@ -136,7 +173,7 @@ __device__ __forceinline__ double dual_step(const DeviceView &v, double *y, doub
     y[row] = ynew;
   }
   kz[row] = knew;
-  if (CHECK) a.lagr += row_lagr(yold, lo, hi);
+  if (CHECK) (dblk ? a.lagrD : a.lagr) += row_lagr(yold, lo, hi);
   return ynew;
 }
 
@@ -145,7 +182,7 @@ __device__ __forceinline__ double dual_step(const DeviceView &v, double *y, doub
 template <bool CHECK>
 __device__ __forceinline__ double primal_step(const DeviceView &v, double *zi, double *zia, const double *lb,
                                               const double *ub, int k, double rc, double tau, bool copy_anchor,
-                                              bool halp, double lam, SmallAcc &a) {
+                                              bool halp, double lam, SmallAcc &a, bool dblk = false) {
   const double old = zi[k];
   if (copy_anchor) zia[k] = old;
   const double zanc = copy_anchor ? old : zia[k];
@@ -157,7 +194,7 @@ __device__ __forceinline__ double primal_step(const DeviceView &v, double *zi, d
   if (CHECK) {
     const double u = (nz - zanc) / g;
     a.dsz += u * u;
-    a.lagr += rc > 0 ? lb[k] * rc : ub[k] * rc;
+    (dblk ? a.lagrD : a.lagr) += rc > 0 ? lb[k] * rc : ub[k] * rc;
   }
   return nz;
 }
@@ -554,18 +591,18 @@ void x_pass(DeviceView v, const int32_t *__restrict__ slots, int first, int plai
       kty_c += -yd1 + yd2 - yD3a + yD3b + v.sigma4 * yD4;
     }
     const double cn = primal_step<CHECK>(v, zi, zia, lb, ub, il.oc + idx, v.cost_int[il.oc + idx] - kty_c, taud,
-                                         copy_anchor, halp, lamd, a);
+                                         copy_anchor, halp, lamd, a, v.step2);
     const double y1n = dual_step<CHECK, INIT>(v, y, ya, kz, kza, dl.o1 + idx, S - v.M * cn, y1, sigma, copy_anchor,
                                               halp, lamd, a);
     const double y2n = dual_step<CHECK, INIT>(v, y, ya, kz, kza, dl.o2 + idx, S - cn, y2, sigma, copy_anchor, halp,
                                               lamd, a);
     if (v.step2) {
       const double mfn = primal_step<CHECK>(v, zi, zia, lb, ub, il.omf + idx, v.cost_int[il.omf + idx] - yd1, taud,
-                                            copy_anchor, halp, lamd, a);
+                                            copy_anchor, halp, lamd, a, true);
       const double mtn = primal_step<CHECK>(v, zi, zia, lb, ub, il.omt + idx, v.cost_int[il.omt + idx] - yd2, taud,
-                                            copy_anchor, halp, lamd, a);
-      dual_step<CHECK, INIT>(v, y, ya, kz, kza, dl.oD1 + idx, mfn - cn, yd1, sigma, copy_anchor, halp, lamd, a);
-      dual_step<CHECK, INIT>(v, y, ya, kz, kza, dl.oD2 + idx, mtn + cn, yd2, sigma, copy_anchor, halp, lamd, a);
+                                            copy_anchor, halp, lamd, a, true);
+      dual_step<CHECK, INIT>(v, y, ya, kz, kza, dl.oD1 + idx, mfn - cn, yd1, sigma, copy_anchor, halp, lamd, a, true);
+      dual_step<CHECK, INIT>(v, y, ya, kz, kza, dl.oD2 + idx, mtn + cn, yd2, sigma, copy_anchor, halp, lamd, a, true);
     }
     kty[(int64_t)f * NP + j] = (float)(y1n + y2n);
     np_[j] = memf * cn;
@@ -619,8 +656,10 @@ void x_pass(DeviceView v, const int32_t *__restrict__ slots, int first, int plai
   vals[NTS + BS_DIST_Y] = a.dsy;
   vals[NTS + BS_SUMC_REP] = sumc_rep;
   vals[NTS + BS_SCORE_N_REP] = 0.0;
+  vals[NTS + BS_LAGR_D] = a.lagrD;
+  constexpr int NW = NTS + BS_TLO;   // the fields from BS_TLO on are dblock_pass's
 #pragma unroll
-  for (int k = 0; k < NTS + NBS; ++k) {
+  for (int k = 0; k < NW; ++k) {
     const bool needed = INIT || CHECK || k == TS_SCORE || k == NTS + BS_SUMC_NEW;
     double t = 0.0;
     if (needed) t = (k == NTS + BS_RES) ? wave_max_d(vals[k]) : wave_sum_d(vals[k]);
@@ -628,7 +667,7 @@ void x_pass(DeviceView v, const int32_t *__restrict__ slots, int first, int plai
   }
   __syncthreads();
   const int k = threadIdx.x;
-  if (k < NTS + NBS) {
+  if (k < NW) {
     double t = 0.0;
 #pragma unroll
     for (int wv = 0; wv < TW; ++wv) t = (k == NTS + BS_RES) ? fmax(t, lds_s[wv][k]) : t + lds_s[wv][k];
@@ -651,6 +690,10 @@ __device__ __forceinline__ void write_bpart(double *bp, const SmallAcc &a, doubl
   vals[BS_MOVE_Y] = a.mvy;
   vals[BS_DIST_Z] = a.dsz;
   vals[BS_DIST_Y] = a.dsy;
+  vals[BS_LAGR_D] = a.lagrD;
+  vals[BS_TLO] = vals[BS_THI] = 0.0;
+#pragma unroll
+  for (int q = 0; q < kNLam; ++q) vals[BS_LK0 + q] = 0.0;
 #pragma unroll
   for (int k = 0; k < NBS; ++k) {
     const double t = (k == BS_RES) ? wave_max_d(vals[k]) : wave_sum_d(vals[k]);
@@ -769,6 +812,55 @@ __global__ __launch_bounds__(kNodeThreads) void node_pass(DeviceView v, const in
 }
 
 // ---------------------------------------------------------------------------------------------
+// dblock_pass (step-2 certificate iterations, launched BEFORE that iteration's x_pass so that it
+// reads the same duals y the rest of the bound uses): per (f, slot), the disruption-block terms of
+// the exact bound for each candidate price (dblock_item), and f's share of the node box of sum c.
+// Writes bpart[f][BS_TLO ..]; x_pass leaves those fields alone.
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void dblock_pass(DeviceView v, const int32_t *__restrict__ slots) {
+  __shared__ double red[4][2 + kNLam];
+  const int f = blockIdx.x;
+  const int slot = slots[blockIdx.y];
+  const Ctrl *ctrl = v.ctrl + slot;
+  if (!ctrl->active) return;
+  const DualLayout &dl = v.dl;
+  const IntLayout &il = v.il;
+  const int N = v.N;
+  const double *y = v.y + slot * v.sdual;
+  const double *lb = v.lb + slot * v.sint, *ub = v.ub + slot * v.sint;
+  double lamk[kNLam], acc[2 + kNLam];
+  dblock_lambdas(v, y, lamk);
+#pragma unroll
+  for (int q = 0; q < 2 + kNLam; ++q) acc[q] = 0.0;
+  const double memf = v.mem_f[f];
+  for (int j = threadIdx.x; j < N; j += 256) {
+    const int idx = f * N + j;
+    double kty_c = -v.M * y[dl.o1 + idx] - y[dl.o2 + idx] + memf * y[dl.o3 + j];
+    if (v.has_n) kty_c += y[dl.o6 + j] + y[dl.o7 + j];
+    const double r = v.cost_int[il.oc + idx] - kty_c;   // c's reduced cost without the D rows
+    const double old = -v.lo[dl.oD1 + idx];
+    const double lmf = lb[il.omf + idx], lmt = lb[il.omt + idx];
+    const double clo = fmax(lb[il.oc + idx], old - ub[il.omt + idx]);
+    const double chi = fmin(ub[il.oc + idx], old + ub[il.omf + idx]);
+    const double cmf = v.cost_int[il.omf + idx], cmt = v.cost_int[il.omt + idx];
+    acc[0] += lb[il.oc + idx];
+    acc[1] += ub[il.oc + idx];
+#pragma unroll
+    for (int q = 0; q < kNLam; ++q) acc[2 + q] += dblock_item(r, lamk[q], old, cmf, lmf, cmt, lmt, clo, chi);
+  }
+  const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int q = 0; q < 2 + kNLam; ++q) {
+    const double t = wave_sum_d(acc[q]);
+    if (lane == 0) red[wave][q] = t;
+  }
+  __syncthreads();
+  const int q = threadIdx.x;
+  if (q < 2 + kNLam)
+    v.bpart[slot * v.sbpart + (int64_t)f * NBS + BS_TLO + q] = red[0][q] + red[1][q] + red[2][q] + red[3][q];
+}
+
+// ---------------------------------------------------------------------------------------------
 // scalar_pass: one workgroup per slot.  Step-2 scalar rows (D3a, D3b, D4, score) and the
 // integer-bounded a / d variables; at check iterations the certificate (primal objective,
 // Lagrangian bound, residuals), status, restarts and the primal-weight update.
@@ -806,6 +898,70 @@ __global__ __launch_bounds__(256) void scalar_pass(DeviceView v, const int32_t *
     if (tid == 0) tot[k] = red[0];
     __syncthreads();
   }
+  // step-2 certificate: G(lambda_q) = min over (a, d, T) of ca a + cd d + lambda_q T on the boxes and
+  // the rows D3a/D3b/D4, by its vertices (3 of at most 12 half-spaces g . (a, d, T) >= h: 220
+  // triples, one per thread).  A vertex is accepted within 1e-9 of every half-space: accepting a
+  // slightly infeasible one can only lower the minimum, so the bound stays valid.
+  __shared__ double gmin[kNLam][256];
+  if (CHECK && v.step2) {
+    const DualLayout &dl = v.dl;
+    const IntLayout &il = v.il;
+    const double *lbs = v.lb + slot * v.sint, *ubs = v.ub + slot * v.sint;
+    double lamk[kNLam];
+    dblock_lambdas(v, v.y + slot * v.sdual, lamk);
+    double hg[12][3], hh[12];
+    int nh = 0;
+    auto add = [&](double ga, double gd, double gt, double h) {
+      if (!isfinite(h)) return;
+      hg[nh][0] = ga; hg[nh][1] = gd; hg[nh][2] = gt; hh[nh] = h; ++nh;
+    };
+    add(1, 0, 0, lbs[il.oa]);  add(-1, 0, 0, -ubs[il.oa]);
+    add(0, 1, 0, lbs[il.od]);  add(0, -1, 0, -ubs[il.od]);
+    add(0, 0, 1, tot[NTS + BS_TLO]);  add(0, 0, -1, -tot[NTS + BS_THI]);
+    const int rws[3] = {dl.oD3a, dl.oD3b, dl.oD4};
+    const double rg[3][3] = {{-1, 0, -1}, {0, -1, 1}, {1, 1, v.sigma4}};
+    for (int q = 0; q < 3; ++q) {
+      add(rg[q][0], rg[q][1], rg[q][2], v.lo[rws[q]]);
+      add(-rg[q][0], -rg[q][1], -rg[q][2], -v.hi[rws[q]]);
+    }
+    const double ca = v.cost_int[il.oa], cd = v.cost_int[il.od];
+    double best[kNLam];
+#pragma unroll
+    for (int q = 0; q < kNLam; ++q) best[q] = INFINITY;
+    int t = 0;
+    for (int i0 = 0; i0 < nh; ++i0)
+      for (int i1 = i0 + 1; i1 < nh; ++i1)
+        for (int i2 = i1 + 1; i2 < nh; ++i2, ++t) {
+          if ((t & 255) != tid) continue;
+          const double *g0 = hg[i0], *g1 = hg[i1], *g2 = hg[i2];
+          const double det = g0[0] * (g1[1] * g2[2] - g1[2] * g2[1]) - g0[1] * (g1[0] * g2[2] - g1[2] * g2[0]) +
+                             g0[2] * (g1[0] * g2[1] - g1[1] * g2[0]);
+          if (fabs(det) < 1e-12) continue;
+          const double h0 = hh[i0], h1 = hh[i1], h2 = hh[i2];
+          const double va = (h0 * (g1[1] * g2[2] - g1[2] * g2[1]) - g0[1] * (h1 * g2[2] - g1[2] * h2) +
+                             g0[2] * (h1 * g2[1] - g1[1] * h2)) / det;
+          const double vd = (g0[0] * (h1 * g2[2] - g1[2] * h2) - h0 * (g1[0] * g2[2] - g1[2] * g2[0]) +
+                             g0[2] * (g1[0] * h2 - h1 * g2[0])) / det;
+          const double vt = (g0[0] * (g1[1] * h2 - h1 * g2[1]) - g0[1] * (g1[0] * h2 - h1 * g2[0]) +
+                             h0 * (g1[0] * g2[1] - g1[1] * g2[0])) / det;
+          bool ok = true;
+          for (int e = 0; e < nh; ++e)
+            ok = ok && (hg[e][0] * va + hg[e][1] * vd + hg[e][2] * vt >= hh[e] - 1e-9 * (1.0 + fabs(hh[e])));
+          if (!ok) continue;
+#pragma unroll
+          for (int q = 0; q < kNLam; ++q) best[q] = fmin(best[q], ca * va + cd * vd + lamk[q] * vt);
+        }
+#pragma unroll
+    for (int q = 0; q < kNLam; ++q) gmin[q][tid] = best[q];
+    __syncthreads();
+    for (int s2 = 128; s2 > 0; s2 >>= 1) {
+      if (tid < s2) {
+#pragma unroll
+        for (int q = 0; q < kNLam; ++q) gmin[q][tid] = fmin(gmin[q][tid], gmin[q][tid + s2]);
+      }
+      __syncthreads();
+    }
+  }
   if (tid != 0) return;
 
   const DualLayout &dl = v.dl;
@@ -826,6 +982,7 @@ __global__ __launch_bounds__(256) void scalar_pass(DeviceView v, const int32_t *
   a.mvy = tot[NTS + BS_MOVE_Y];
   a.dsz = tot[TS_DIST] + tot[NTS + BS_DIST_Z];
   a.dsy = tot[NTS + BS_DIST_Y];
+  a.lagrD = tot[NTS + BS_LAGR_D];
 
   if (v.step2) {
     const double sumc = tot[NTS + BS_SUMC_NEW];
@@ -833,13 +990,13 @@ __global__ __launch_bounds__(256) void scalar_pass(DeviceView v, const int32_t *
     const double yD3a = y[dl.oD3a], yD3b = y[dl.oD3b], yD4 = y[dl.oD4], yS = y[dl.oS];
     // allocated (a): D3a coef -1, D4 coef +1 ; deallocated (d): D3b coef -1, D4 coef +1
     const double an = primal_step<CHECK>(v, zi, zia, lb, ub, il.oa, v.cost_int[il.oa] - (-yD3a + yD4), tau,
-                                         copy_anchor, halp, lam, a);
+                                         copy_anchor, halp, lam, a, true);
     const double dn = primal_step<CHECK>(v, zi, zia, lb, ub, il.od, v.cost_int[il.od] - (-yD3b + yD4), tau,
-                                         copy_anchor, halp, lam, a);
-    dual_step<CHECK, INIT>(v, y, ya, kz, kza, dl.oD3a, -sumc - an, yD3a, sigma, copy_anchor, halp, lam, a);
-    dual_step<CHECK, INIT>(v, y, ya, kz, kza, dl.oD3b, sumc - dn, yD3b, sigma, copy_anchor, halp, lam, a);
+                                         copy_anchor, halp, lam, a, true);
+    dual_step<CHECK, INIT>(v, y, ya, kz, kza, dl.oD3a, -sumc - an, yD3a, sigma, copy_anchor, halp, lam, a, true);
+    dual_step<CHECK, INIT>(v, y, ya, kz, kza, dl.oD3b, sumc - dn, yD3b, sigma, copy_anchor, halp, lam, a, true);
     dual_step<CHECK, INIT>(v, y, ya, kz, kza, dl.oD4, dn + an + v.sigma4 * sumc, yD4, sigma, copy_anchor, halp, lam,
-                           a);
+                           a, true);
     dual_step<CHECK, INIT>(v, y, ya, kz, kza, dl.oS, score, yS, sigma, copy_anchor, halp, lam, a);
     float *kty = v.kty + slot * v.skty;
     kty[(int64_t)v.F * v.NP + v.NP] = (float)y[dl.oS];
@@ -881,7 +1038,14 @@ __global__ __launch_bounds__(256) void scalar_pass(DeviceView v, const int32_t *
     const double score_rep = tot[TS_SCORE] + tot[NTS + BS_SCORE_N_REP];
     res = fmax(res, row_viol(score_rep, v.lo[dl.oS], v.hi[dl.oS]) / v.rownorm[dl.oS]);
   }
-  const double lagr = a.lagr;
+  // the Lagrangian with every row dualised, or (step 2) the disruption block kept exact at the best
+  // of the candidate prices (both are valid bounds)
+  double lagr = a.lagr + a.lagrD;
+  if (v.step2) {
+#pragma unroll
+    for (int q = 0; q < kNLam; ++q)
+      if (isfinite(gmin[q][0])) lagr = fmax(lagr, a.lagr + tot[NTS + BS_LK0 + q] + gmin[q][0]);
+  }
   const double gap = pobj - lagr;
   const double tol = v.prm[0], cutoff = v.prm[1];
   ctrl->pobj = pobj;
@@ -1075,6 +1239,11 @@ hipError_t launch_node_pass(const DeviceView &v, const int32_t *slots, int nslot
   if (init) hipLaunchKernelGGL((node_pass<false, true>), grid, block, 0, s, v, slots, fi, pl, it);
   else if (check) hipLaunchKernelGGL((node_pass<true, false>), grid, block, 0, s, v, slots, fi, pl, it);
   else hipLaunchKernelGGL((node_pass<false, false>), grid, block, 0, s, v, slots, fi, pl, it);
+  return hipGetLastError();
+}
+
+hipError_t launch_dblock_pass(const DeviceView &v, const int32_t *slots, int nslots, hipStream_t s) {
+  hipLaunchKernelGGL(dblock_pass, dim3(v.F, nslots), dim3(256), 0, s, v, slots);
   return hipGetLastError();
 }
 
