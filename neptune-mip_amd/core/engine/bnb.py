@@ -92,7 +92,7 @@ class BranchAndBound:
     def __init__(self, lp, workload, fn_mem, node_mem, batch=16, tol=1e-7, gap=1e-6, max_iters=5000,
                  node_limit=20000, time_limit=None, upper_bound=math.inf, flow_tol=1e-4, log=None, comm=None,
                  warm=True, root_max_iters=200000, check_every=16, polish_tol=1e-8, polish_iters=20000,
-                 seed_leaves=None, integer_bound=None):
+                 seed_leaves=None, integer_bound=None, improve=None):
         self.lp = lp
         self.N, self.F = lp.N, lp.F
         L = lp.layout()
@@ -117,6 +117,8 @@ class BranchAndBound:
         # a node's fixings (+inf: none); a node's bound is the larger of it and its parent LP's
         self.seed_leaves = list(seed_leaves or [])
         self.integer_bound = integer_bound
+        # improve(idx, val, value) -> [(idx, val)]: neighbour leaves of each new incumbent (local search)
+        self.improve = improve
         self.node_limit, self.time_limit = node_limit, time_limit
         self.ub0 = upper_bound
         self.flow_tol = flow_tol
@@ -321,6 +323,15 @@ class BranchAndBound:
                         self.keep.add(slot)
                     self.lp.set_params(self.tol, min(inc, self.ub0))
                     self.log(f"incumbent {pobj:.10g} (lps {res.lps}, nodes {res.nodes})")
+                    if self.improve is not None:
+                        for idx, val in self.improve(node.idx, node.val, pobj):
+                            key = np.packbits(np.asarray(val) > 0.5).tobytes()
+                            if key not in self.seen_leaves:
+                                self.seen_leaves.add(key)
+                                # a neighbour is no descendant of this leaf: its bound is its own
+                                self.pending.appendleft(_Node(self._ibound(idx, val), idx,
+                                                              np.asarray(val, np.float64), LEAF, (slot, self.slot_gen[slot]),
+                                                              node.depth))
             elif node.kind == LEAF:
                 self.retry.append(_Node(bound, node.idx, node.val, RETRY, (slot, self.slot_gen[slot]), node.depth))
             else:

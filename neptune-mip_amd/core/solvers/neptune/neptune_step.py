@@ -72,6 +72,11 @@ class NeptuneStepBase(Solver):
         fixings (+inf: none exists), or None."""
         return None
 
+    def improve(self, layout):
+        """improve(idx, val, value) -> [(idx, val)]: neighbour placements of a new incumbent leaf
+        worth solving (a local-search heuristic), or None."""
+        return None
+
     def solve(self):
         self.init_objective()
         data = self.data
@@ -86,7 +91,8 @@ class NeptuneStepBase(Solver):
                                  node_limit=self.node_limit,
                                  time_limit=self.time_limit,
                                  upper_bound=ub * (1 + 1e-6) + 1e-6 if math.isfinite(ub) else ub, log=self.log,
-                                 seed_leaves=self.seed_leaves(model.layout()), integer_bound=self.integer_bound())
+                                 seed_leaves=self.seed_leaves(model.layout()), integer_bound=self.integer_bound(),
+                                 improve=self.improve(model.layout()))
             res = bnb.solve()
             layout = model.layout()
         finally:
@@ -263,6 +269,63 @@ class NeptuneStep2Base(NeptuneStepBase):
             R_max = O - float((one & old).sum())
             return (2 * w + 1) * A - R_max
         return bound
+
+    def improve(self, layout, top=4):
+        """Node relocation around a new incumbent: exchange the placement columns of two nodes
+        (c[:, ju] <-> c[:, jt], n alike), for every node ju the incumbent uses and every other node jt.
+        The step-2 objective depends on c only (integer_bound's closed form in A, R), so every
+        exchange is priced exactly from column counts (A(p, o) = p . (1 - o), R(p, o) = (1 - p) . o,
+        one F x N by N x F product each); sum c is unchanged (D3/D4 hold as before), memory (C3,
+        constraints_step1.py:18-23) is checked, and the `top` cheapest exchanges below the incumbent
+        are returned as leaves (their LPs re-check routing and the remaining rows).  E.g. the Alibaba
+        MDU case: step 1 puts every function on one node, step 2 must keep one node (score row) and
+        the optimum is the node holding most of the old allocation."""
+        d = self.data
+        F, N = len(d.functions), len(d.nodes)
+        FN = F * N
+        old = (np.asarray(d.old_allocations_matrix, np.float64).reshape(F, N) > 0.5).astype(np.float64)
+        mem_f = np.asarray(d.function_memory_matrix, np.float64).reshape(F)
+        node_mem = np.asarray(d.node_memory_matrix, np.float64).reshape(N)
+        w = float(FN)
+        ka, kr = (1.0, 2 * w - 1) if self.mode == "create" else (2 * w + 1, -1.0)
+        has_n = layout.get("n") is not None
+
+        def neighbours(idx, val, value):
+            c = np.zeros(FN)
+            sel = idx < FN
+            c[idx[sel]] = val[sel]
+            P = (c.reshape(F, N) > 0.5).astype(np.float64)
+            Acol = (P * (1 - old)).sum(axis=0)                 # additions per node
+            Rcol = ((1 - P) * old).sum(axis=0)                 # removals per node
+            Across = P.T @ (1 - old)                           # [a, b]: column a's pattern on node b
+            Rcross = (1 - P).T @ old
+            used = np.flatnonzero(P.sum(axis=0) > 0)
+            if used.size == 0:
+                return []
+            memcol = mem_f @ P                                 # memory of each column's pattern
+            dA = Across[used, :] + Across[:, used].T - Acol[used][:, None] - Acol[None, :]
+            dR = Rcross[used, :] + Rcross[:, used].T - Rcol[used][:, None] - Rcol[None, :]
+            delta = ka * dA + kr * dR                          # objective change of exchanging (ju, jt)
+            ok = (memcol[used][:, None] <= node_mem[None, :] + 1e-9) & (memcol[None, :] <= node_mem[used][:, None] + 1e-9)
+            ok &= used[:, None] != np.arange(N)[None, :]
+            delta = np.where(ok, delta, np.inf)
+            order = np.argsort(delta, axis=None, kind="stable")[:top]
+            out = []
+            for k in order:
+                if not delta.flat[k] < -0.5:                     # integral objective: improve by >= 1
+                    break
+                u, t = divmod(int(k), N)
+                ju = int(used[u])
+                Q = P.copy()
+                Q[:, [ju, t]] = Q[:, [t, ju]]
+                ids, vs = [np.arange(FN)], [Q.ravel()]
+                if has_n:
+                    n0, n1 = layout["n"]
+                    ids.append(np.arange(n0, n1))
+                    vs.append((Q.sum(axis=0) > 0).astype(np.float64))
+                out.append((np.concatenate(ids), np.concatenate(vs)))
+            return out
+        return neighbours
 
     def results(self):
         # neptune_step2.py:43-51: no side effects on data (the prints are logs only)

@@ -74,3 +74,56 @@ def test_step2_integer_bound_brute_force(mode, seed):
             assert b == math.inf, (bits, b)
         else:
             assert b == v, (bits, b, v)
+
+
+@pytest.mark.parametrize("mode", ["delete", "create"])
+@pytest.mark.parametrize("seed", range(4))
+def test_step2_relocation_prices_exactly(mode, seed):
+    """NeptuneStep2Base.improve: every neighbour it returns is a column exchange of the incumbent,
+    fits memory, and its objective (the exact closed form, integer_bound on a complete fixing) is
+    below the incumbent's; and it finds the best exchange (brute force over all pairs)."""
+    from core.solvers.neptune.neptune_step import NeptuneStep2Base
+    rng = np.random.default_rng(seed)
+    F, N = 3, 5
+    FN = F * N
+    old = (rng.random((F, N)) < 0.35).astype(float)
+    s = NeptuneStep2Base.__new__(NeptuneStep2Base)
+    s.mode = mode
+    s.data = types.SimpleNamespace(functions=list(range(F)), nodes=list(range(N)), old_allocations_matrix=old,
+                                   function_memory_matrix=rng.integers(1, 4, F).astype(float),
+                                   node_memory_matrix=rng.integers(3, 9, N).astype(float))
+    bound = s.integer_bound()
+    layout = {"c": (0, FN), "n": (FN + 4, FN + 4 + N)}
+    imp = s.improve(layout, top=FN * N)
+    for trial in range(20):
+        P = (rng.random((F, N)) < 0.3).astype(float)
+        P[np.arange(F), rng.integers(0, N, F)] = 1.0
+        value = bound(np.arange(FN), P.ravel())
+        if not np.isfinite(value) or (s.data.function_memory_matrix @ P > s.data.node_memory_matrix).any():
+            continue                      # an incumbent is feasible
+        idx = np.concatenate([np.arange(FN), np.arange(FN + 4, FN + 4 + N)])
+        val = np.concatenate([P.ravel(), (P.sum(axis=0) > 0).astype(float)])
+        got = imp(idx, val, value)
+        mem = s.data.function_memory_matrix
+        best = value
+        for ju in range(N):
+            for jt in range(N):
+                if ju == jt or P[:, ju].sum() == 0:
+                    continue
+                Q = P.copy()
+                Q[:, [ju, jt]] = Q[:, [jt, ju]]
+                if (mem @ Q > s.data.node_memory_matrix + 1e-9).any():
+                    continue
+                best = min(best, bound(np.arange(FN), Q.ravel()))
+        vals = []
+        for gi, gv in got:
+            Q = gv[:FN].reshape(F, N)
+            assert sorted(map(tuple, Q.T.tolist())) == sorted(map(tuple, P.T.tolist()))   # an exchange
+            assert (mem @ Q <= s.data.node_memory_matrix + 1e-9).all()
+            assert np.array_equal(gv[FN:], (Q.sum(axis=0) > 0).astype(float))
+            vals.append(bound(np.arange(FN), Q.ravel()))
+            assert vals[-1] < value
+        if best < value - 0.5:
+            assert vals and min(vals) == best, (vals, best, value)
+        else:
+            assert not got
