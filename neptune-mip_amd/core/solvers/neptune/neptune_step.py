@@ -67,7 +67,7 @@ class NeptuneStepBase(Solver):
         """Placements to try as leaves right after the root (a B&B primal start); none by default."""
         return []
 
-    def integer_bound(self):
+    def integer_bound(self, layout=None):
         """bound(idx, val): a lower bound on the objective of every integral completion of a node's
         fixings (+inf: none exists), or None."""
         return None
@@ -91,7 +91,7 @@ class NeptuneStepBase(Solver):
                                  node_limit=self.node_limit,
                                  time_limit=self.time_limit,
                                  upper_bound=ub * (1 + 1e-6) + 1e-6 if math.isfinite(ub) else ub, log=self.log,
-                                 seed_leaves=self.seed_leaves(model.layout()), integer_bound=self.integer_bound(),
+                                 seed_leaves=self.seed_leaves(model.layout()), integer_bound=self.integer_bound(model.layout()),
                                  improve=self.improve(model.layout()))
             res = bnb.solve()
             layout = model.layout()
@@ -230,8 +230,21 @@ class NeptuneStep2Base(NeptuneStepBase):
             out.append((np.concatenate(idx), np.concatenate(val)))
         return out
 
-    def integer_bound(self):
-        """The step-2 objective over integral placements, bounded from the node's c fixings.
+    def node_cap(self):
+        """The most nodes an integral step-2 placement can open (n binary, n = 1 wherever c = 1 by
+        C6/C7), from the step-2 rows on n: MinUtilization's sum n <= max_score * soften
+        (constraints_step2.py:71-73); MinDelayAndUtilization's score row (:76-88), whose x terms are
+        >= 0, gives alpha / N * sum n <= max_score * soften.  inf when nothing caps it."""
+        if self.VARIANT not in ("MinUtilization", "MinDelayAndUtilization"):
+            return math.inf
+        d = self.data
+        ms = float(getattr(d, "max_score", 0.0) or 0.0) * self.soften_step1_sol
+        if self.VARIANT == "MinUtilization":
+            return ms
+        return ms * len(d.nodes) / self.alpha if self.alpha > 0 else math.inf
+
+    def integer_bound(self, layout=None):
+        """The step-2 objective over integral placements, bounded from the node's c (and n) fixings.
 
         With c binary, A = #(c=1, old=0) additions, R = #(c=0, old=1) removals and O = sum old,
         minimize_disruption (objectives.py:55-63, w = F*N) under constrain_migrations
@@ -241,7 +254,9 @@ class NeptuneStep2Base(NeptuneStepBase):
         Every function needs an open destination (constraints_step1.py:27-35 with :5-15: its rows
         route somewhere and c >= flow / M), so A is at least the fixed additions plus one per
         function that no fixed-1 c and no free old c can cover.  The bound is the closed form at
-        those least A, R (largest R for delete), +inf when the sum-c condition cannot hold."""
+        those least A, R (largest R for delete), +inf when the sum-c condition cannot hold.
+        With at most K nodes open (node_cap), the old allocations kept sit on at most K nodes:
+        R >= O - (the most keepable old entries on K nodes that include every node the fixings open)."""
         d = self.data
         F, N = len(d.functions), len(d.nodes)
         FN = F * N
@@ -249,6 +264,9 @@ class NeptuneStep2Base(NeptuneStepBase):
         old = (np.asarray(d.old_allocations_matrix, np.float64).reshape(FN) > 0.5)
         O = float(old.sum())
         create = self.mode == "create"
+        K = self.node_cap()
+        Kint = math.floor(K + 1e-9) if math.isfinite(K) else None
+        nr = None if layout is None else layout.get("n")
 
         def bound(idx, val):
             fx = np.full(FN, -1.0)
@@ -259,10 +277,25 @@ class NeptuneStep2Base(NeptuneStepBase):
             rem_fixed = float((zero & old).sum())
             covered = (one | (old & ~zero)).reshape(F, N).any(axis=1)
             A = add_fixed + float((~covered).sum())
+            R_lb = rem_fixed
+            if Kint is not None:
+                nf = np.full(N, -1.0)
+                if nr is not None:
+                    seln = (idx >= nr[0]) & (idx < nr[1])
+                    nf[idx[seln] - nr[0]] = val[seln]
+                opened = (nf > 0.5) | one.reshape(F, N).any(axis=0)
+                closed = (nf >= 0) & (nf < 0.5)
+                if (opened & closed).any() or opened.sum() > Kint:
+                    return math.inf
+                keep = ((old & ~zero).reshape(F, N).sum(axis=0)).astype(np.float64)
+                keep[closed] = 0.0
+                free = np.sort(keep[~opened & ~closed])[::-1]
+                best = float(keep[opened].sum()) + float(free[:max(0, Kint - int(opened.sum()))].sum())
+                R_lb = max(R_lb, O - best)
             if create:
                 if FN - float(zero.sum()) < O:
                     return math.inf
-                return A + (2 * w - 1) * rem_fixed
+                return A + (2 * w - 1) * R_lb
             ones_f = one.reshape(F, N).sum(axis=1)
             if float(np.maximum(ones_f, 1.0).sum()) > O + 1e-9:
                 return math.inf

@@ -127,3 +127,42 @@ def test_step2_relocation_prices_exactly(mode, seed):
             assert vals and min(vals) == best, (vals, best, value)
         else:
             assert not got
+
+
+@pytest.mark.parametrize("mode", ["delete", "create"])
+@pytest.mark.parametrize("seed", range(4))
+def test_step2_integer_bound_with_node_cap(mode, seed):
+    """MinUtilization step 2: at most K = max_score * soften nodes open (constraints_step2.py:71-73).
+    Brute force over binary c (n = any c per node, n fixings respected): the bound never exceeds the
+    best completion of a node's c / n fixings and is +inf when no completion exists."""
+    from core.solvers.neptune.neptune_step import NeptuneStep2MinUtilization
+    rng = np.random.default_rng(100 + seed)
+    F, N = 2, 4
+    FN = F * N
+    old = (rng.random(FN) < 0.45).astype(int)
+    s = NeptuneStep2MinUtilization.__new__(NeptuneStep2MinUtilization)
+    s.mode, s.soften_step1_sol = mode, 1.0
+    K = int(rng.integers(1, 3))
+    s.data = types.SimpleNamespace(functions=list(range(F)), nodes=list(range(N)), max_score=K + 0.3,
+                                   old_allocations_matrix=old.reshape(F, N).astype(float))
+    n0 = 3 * FN + 2
+    bound = s.integer_bound({"c": (0, FN), "n": (n0, n0 + N)})
+    values = {}
+    for bits in itertools.product((0, 1), repeat=FN):
+        c = np.array(bits)
+        opened = c.reshape(F, N).any(axis=0)
+        if (c.reshape(F, N).sum(axis=1) < 1).any() or opened.sum() > K:
+            continue
+        values[bits] = (_objective(c, old, mode), opened)
+    for _ in range(60):
+        k = int(rng.integers(0, FN))
+        ci = rng.permutation(FN)[:k]
+        cv = rng.integers(0, 2, k).astype(float)
+        kn = int(rng.integers(0, 3))
+        ni = rng.permutation(N)[:kn]
+        nv = rng.integers(0, 2, kn).astype(float)
+        comp = [v for bits, (v, op) in values.items() if v is not None
+                and all(bits[i] == int(x) for i, x in zip(ci, cv)) and all(op[j] == bool(x) for j, x in zip(ni, nv))]
+        b = bound(np.concatenate([ci, n0 + ni]).astype(np.int64), np.concatenate([cv, nv]))
+        if comp:
+            assert b <= min(comp) + 1e-9, (ci, cv, ni, nv, b, min(comp))
