@@ -68,6 +68,9 @@ def parse(argv=None):
     ap.add_argument("--root-max-iters", type=int, default=400000)
     ap.add_argument("--check-every", type=int, default=16, help="PDHG iterations per certificate check (node LPs)")
     ap.add_argument("--root-check-every", type=int, default=64)
+    ap.add_argument("--root-gap-tol", type=float, default=0.0,
+                    help="after the root certifies at --tol, continue it (warm, same slot) until its objective gap "
+                         "is below this: the children warm-start from a well-converged root (0 = off)")
     ap.add_argument("--cold", action="store_true", help="cold-start every node LP")
     ap.add_argument("--cpu-budget", type=float, default=25.0, help="seconds for the CPU baseline (0 = skip)")
     ap.add_argument("--cpu-workers", type=int, default=16,
@@ -322,6 +325,17 @@ def main():
         f"({time.perf_counter() - t_root:.2f}s)")
     if root_status != LP_OPTIMAL:
         raise RuntimeError(f"root LP not certified: status {root_status} after {root_iters} iterations")
+    root_polish = None
+    if a.root_gap_tol > 0:
+        # the children's starting point: the root's state continued to a tighter objective gap (the
+        # certified root value above stands; the polished state is kept whether or not it certifies)
+        t_pol = time.perf_counter()
+        rp = m.solve([root], tol=a.tol, gap_tol=a.root_gap_tol, max_iters=a.root_max_iters,
+                     check_every=a.root_check_every, warm_start=True, warm_omega_floor=-1.0)
+        root_polish = {"gap_tol": a.root_gap_tol, "status": int(rp["status"][0]), "iters": int(rp["iters"][0]),
+                       "obj": float(rp["obj"][0]), "seconds": time.perf_counter() - t_pol}
+        log(f"rank {rank}: root polish to gap {a.root_gap_tol:g}: status {root_polish['status']} after "
+            f"{root_polish['iters']} iterations ({root_polish['seconds']:.2f}s)")
 
     stream = NodeStream(m, root, a, rank)
 
@@ -415,7 +429,7 @@ def main():
         "lp": {"certified": n_ok, "completed": n_done, "iterations": n_it,
                "mean_iters": n_it / max(1, n_done), "iters_p50_p90_max": iq,
                "slot_utilisation_rank0": util,
-               "root_obj": root_obj, "root_iters": root_iters},
+               "root_obj": root_obj, "root_iters": root_iters, "root_polish": root_polish},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_over_algorithmic": traffic_ratio,
                      "kernel": "x_pass", "algorithmic_bytes_per_launch": per_lp * lps_per_launch,

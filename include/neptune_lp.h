@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define NEP_API_VERSION 4
+#define NEP_API_VERSION 5
 
 /* variants: neptune.py:41-66 (NeptuneMinDelay / MinUtilization / MinDelayAndUtilization) */
 enum { NEP_MIN_DELAY = 0, NEP_MIN_UTILIZATION = 1, NEP_MIN_DELAY_AND_UTILIZATION = 2 };
@@ -81,6 +81,8 @@ typedef struct {
   int32_t warm_start;          /* 1: continue from the slot's current state (after nep_lp_copy_state) */
   double warm_omega_floor;     /* warm starts: the primal weight stays >= this x the parent's
                                   (0: default 2; < 0: no floor) */
+  double gap_tol;              /* API 5: certified objective gap (relative, as tol); 0: = tol.  A tighter
+                                  gap for an LP whose state warm-starts others (a B&B root) */
 } nep_lp_opts;
 
 typedef struct {

@@ -114,7 +114,7 @@ struct Model {
   DeviceView v{};
   std::vector<void *> allocs;
   double *d_prm = nullptr;      // {tol, cutoff} of the LPs in flight (DeviceView::prm)
-  double prm_host[2] = {0, 0};
+  double prm_host[3] = {0, 0, 0};   // tol, cutoff, gap tol of the LPs in flight
   int32_t *d_slots = nullptr;   // the slots currently iterating (mirror of `act`)
   int32_t *d_new = nullptr;     // slots being initialised by nep_lp_submit
   double *d_base_lb = nullptr, *d_base_ub = nullptr;
@@ -570,6 +570,8 @@ int setup_device(Model &m, int max_batch, void *stream) {
   v.rs_suff = 0.2; v.rs_nec = 0.9; v.rs_art = 0.36; v.omega_smooth = 0.5;   // necessary 0.9: DESIGN.md §4
   if (const char *e = std::getenv("NEP_RESTART")) std::sscanf(e, "%lf,%lf,%lf", &v.rs_suff, &v.rs_nec, &v.rs_art);
   if (const char *e = std::getenv("NEP_OMEGA_SMOOTH")) v.omega_smooth = std::atof(e);
+  v.warm_omega_cap = 0.0;
+  if (const char *e = std::getenv("NEP_WARM_OMEGA_CAP")) v.warm_omega_cap = std::atof(e);
   int rc;
   if ((rc = upload(m, &v.rows, m.rows))) return rc;
   if ((rc = upload(m, &v.frow, m.frow))) return rc;
@@ -611,6 +613,8 @@ int setup_dense(Model &m, const nep_model_desc &d) {
   v.srpart = (int64_t)F * 2 * NP;
   if ((rc = dalloc(m, &v.x, (size_t)B * v.sx))) return rc;
   if ((rc = dalloc(m, &v.xa, (size_t)B * v.sx))) return rc;
+  if ((rc = dalloc(m, &v.acnt, (size_t)B * m.R))) return rc;
+  if ((rc = dalloc(m, &v.aent, (size_t)B * m.R * kAnchorK))) return rc;
   if ((rc = dalloc(m, &v.theta, (size_t)B * m.R))) return rc;
   if ((rc = dalloc(m, &v.mask, (size_t)B * v.smask))) return rc;
   if ((rc = dalloc(m, &v.zi, (size_t)B * v.sint))) return rc;
@@ -628,7 +632,7 @@ int setup_dense(Model &m, const nep_model_desc &d) {
   if ((rc = dalloc(m, &v.npart, (size_t)B * v.snpart))) return rc;
   if ((rc = dalloc(m, &v.rpart, (size_t)B * v.srpart))) return rc;
   if ((rc = dalloc(m, &v.ctrl, (size_t)B))) return rc;
-  if ((rc = dalloc(m, &m.d_prm, 2))) return rc;
+  if ((rc = dalloc(m, &m.d_prm, 3))) return rc;
   v.prm = m.d_prm;
   if ((rc = dalloc(m, &m.d_slots, (size_t)B))) return rc;
   if ((rc = dalloc(m, &m.d_new, (size_t)B))) return rc;
@@ -649,7 +653,8 @@ int setup_dense(Model &m, const nep_model_desc &d) {
   if ((rc = dalloc(m, &m.d_chg_ub, (size_t)B * v.sint))) return rc;
   HIPCHK(hipMemsetAsync(v.ctrl, 0, sizeof(Ctrl) * B, m.stream));
   HIPCHK(hipMemsetAsync(v.x, 0, sizeof(float) * B * v.sx, m.stream));
-  HIPCHK(hipMemsetAsync(v.xa, 0, sizeof(anchor_t) * B * v.sx, m.stream));
+  HIPCHK(hipMemsetAsync(v.xa, 0, sizeof(float) * B * v.sx, m.stream));
+  HIPCHK(hipMemsetAsync(v.acnt, 0, sizeof(int32_t) * B * m.R, m.stream));
   HIPCHK(hipMemsetAsync(v.theta, 0xFF, sizeof(float) * B * m.R, m.stream));   // NaN: no hint
   HIPCHK(hipMemsetAsync(v.zi, 0, sizeof(double) * B * v.sint, m.stream));
   HIPCHK(hipMemsetAsync(v.y, 0, sizeof(double) * B * v.sdual, m.stream));
@@ -865,7 +870,9 @@ nep_lp_opts resolve_opts(const nep_lp_opts *opts) {
     if (opts->check_every > 0) o.check_every = opts->check_every;
     o.warm_start = opts->warm_start;
     if (opts->warm_omega_floor != 0) o.warm_omega_floor = opts->warm_omega_floor < 0 ? 0.0 : opts->warm_omega_floor;
+    o.gap_tol = opts->gap_tol;
   }
+  if (!(o.gap_tol > 0)) o.gap_tol = o.tol;
   return o;
 }
 
@@ -890,6 +897,7 @@ int submit(Model &m, int n, const int32_t *slots, const double *lbi, const doubl
   // tol / cutoff of every LP in flight: device memory, read by the (graph-replayed) blocks
   m.prm_host[0] = o.tol;
   m.prm_host[1] = o.cutoff;
+  m.prm_host[2] = o.gap_tol;
   HIPCHK(hipMemcpyAsync(m.d_prm, m.prm_host, sizeof(m.prm_host), hipMemcpyHostToDevice, m.stream));
   std::vector<int32_t> fresh, off(1, 0), ci, exact;
   std::vector<double> cl, cu;
@@ -1347,6 +1355,7 @@ int nep_lp_set_params(void *model, double tol, double cutoff) {
   m.run.cutoff = cutoff;
   m.prm_host[0] = m.run.tol;
   m.prm_host[1] = m.run.cutoff;
+  m.prm_host[2] = m.run.gap_tol;
   HIPCHK(hipMemcpyAsync(m.d_prm, m.prm_host, sizeof(m.prm_host), hipMemcpyHostToDevice, m.stream));
   HIPCHK(hipStreamSynchronize(m.stream));
   return NEP_OK;

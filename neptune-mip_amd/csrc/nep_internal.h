@@ -6,7 +6,9 @@
 //   x     [R][NP] f32   routing rows x̄[r, j]; row r = (function f, source i) or the pooled
 //                       zero-workload sources of f (exact aggregation); the rows of
 //                       one function are consecutive (frow[f] .. frow[f+1])
-//   xa    [R][NP] f32   restart anchor of x (anchor_t: f16 when NEP_ANCHOR_F16=1)
+//   xa    [R][NP] f32   restart anchor of x, dense form (only rows whose anchor has > kAnchorK nonzeros)
+//   acnt  [R] i32       anchor nonzeros of each row (kAnchorDense: the row's anchor is dense in xa)
+//   aent  [R][kAnchorK] (j, value) pairs of the anchor rows held sparse
 //   mask  [F][NP] u8    destination j allowed for function f at this node (c_ub[f,j] > 0)
 //   zi    [n_int] f64   small primal: c, (mf, mt, a, d), n        + anchor zia, bounds lb/ub
 //   y     [n_dual] f64  duals of the dualised rows   + anchor ya, activity kz (iterate) / kza (anchor)
@@ -24,24 +26,28 @@
 // Build-time variants (A/B-measured on the MI355X):
 //   NEP_NT          1: the routing-state streams (x, anchor) use non-temporal loads/stores, so the
 //                      once-per-iteration stream does not evict the delay matrix D from the XCD's L2
-//   NEP_ANCHOR_F16  1: the Halpern anchor rows are stored in fp16.  Measured (512x256 bench, r02a):
-//                      certified node LPs fell from 374/384 to 70/384 — the anchor's rounding (5e-4
-//                      relative) re-enters every restart cycle as an O(dist(anchor, fixed set)/k) term,
-//                      so the iterates stall far above the 1e-6 certificate.  Off by default.
+//   NEP_SPARSE_ANCHOR 1: anchor rows with <= kAnchorK nonzeros are kept as (j, value) pairs (exact
+//                      fp32 values: the same anchor, fewer bytes).  0: always dense.
+// (An fp16 anchor was measured in round 2 and rejected: certified node LPs fell from 374/384 to
+// 70/384 — its rounding re-enters every restart cycle, so the iterates stall above 1e-6.)
 #ifndef NEP_NT
 #define NEP_NT 1
 #endif
-#ifndef NEP_ANCHOR_F16
-#define NEP_ANCHOR_F16 0
+#ifndef NEP_SPARSE_ANCHOR
+#define NEP_SPARSE_ANCHOR 1
 #endif
 
 namespace nep {
 
-#if NEP_ANCHOR_F16
-using anchor_t = _Float16;
-#else
-using anchor_t = float;
-#endif
+// The Halpern anchor is always a point on the routing simplexes (it is set right after a plain
+// PDHG step, or from the initial projection), so its rows are sparse: a row keeps up to kAnchorK
+// (destination, value) pairs, 8 B each, instead of NP floats.
+constexpr int kAnchorK = 16;
+constexpr int kAnchorDense = kAnchorK + 1;
+struct AnchorEnt {
+  int32_t j;
+  float v;
+};
 
 constexpr int kWave = 64;
 constexpr int kNodeWaves = 16;           // waves per node-pass workgroup (each sums F/16 functions)
@@ -113,7 +119,9 @@ struct DeviceView {
   const double *gam, *rho, *lo, *hi, *rownorm, *cost_int, *mem_f;
   // per slot (base pointers; slot stride below)
   float *x;
-  anchor_t *xa;
+  float *xa;
+  int32_t *acnt;                         // [R] anchor nonzeros per row (kAnchorDense: dense in xa)
+  AnchorEnt *aent;                       // [R][kAnchorK] sparse anchor rows
   float *theta;                          // [R] last simplex threshold of each routing row (a start hint)
   uint8_t *mask;
   double *zi, *zia, *lb, *ub;
@@ -124,11 +132,12 @@ struct DeviceView {
   double *rpart;                         // [F][2][NP] certificate: repaired c shares of the node rows (mem, c)
   Ctrl *ctrl;
   int64_t sx, smask, sint, sdual, skty, stpart, sbpart, snpart, srpart;   // per-slot strides (elements)
-  // check/solve parameters.  tol / cutoff live in device memory (prm[0] / prm[1], written by every
+  // check/solve parameters.  tol / cutoff / gap tol live in device memory (prm[0..2], written by every
   // nep_lp_submit) because the iteration blocks are replayed from captured HIP graphs: a value
   // passed by value would stay frozen at capture time.
   const double *prm;
   double warm_omega_floor;               // warm starts: primal weight kept >= this x the parent's (0: off)
+  double warm_omega_cap;                 // warm starts: primal weight kept <= this x the parent's (0: off; NEP_WARM_OMEGA_CAP)
   // restart rule on the fixed-point residual (sufficient / necessary / artificial, PDLP's 0.2 / 0.8 /
   // 0.36; necessary 0.9 here, measured) and the primal-weight smoothing (0.5); NEP_RESTART /
   // NEP_OMEGA_SMOOTH override them

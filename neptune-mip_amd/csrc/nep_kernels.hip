@@ -133,15 +133,49 @@ __device__ __forceinline__ double dblock_item(double r, double lam, double old, 
   return best;
 }
 
+// Operands of one dual row / one small variable, loaded ahead of their update (node_pass issues
+// every load of its rows at kernel start, so they overlap the partial sums instead of forming a
+// load -> store -> load chain through possibly aliasing pointers).
+struct DPre {
+  double y, lo, hi, rho, kz, ya, kza;
+};
+struct ZPre {
+  double z, za, lb, ub, gam, cost;
+};
+template <bool INIT>
+__device__ __forceinline__ DPre dual_pre(const DeviceView &v, const double *y, const double *ya, const double *kz,
+                                         const double *kza, int row, bool copy_anchor) {
+  DPre p;
+  p.y = y[row];
+  p.lo = v.lo[row];
+  p.hi = v.hi[row];
+  p.rho = v.rho[row];
+  p.kz = kz[row];
+  p.ya = (INIT || copy_anchor) ? 0.0 : ya[row];
+  p.kza = (INIT || copy_anchor) ? 0.0 : kza[row];
+  return p;
+}
+__device__ __forceinline__ ZPre primal_pre(const DeviceView &v, const double *zi, const double *zia, const double *lb,
+                                           const double *ub, int k, bool copy_anchor) {
+  ZPre p;
+  p.z = zi[k];
+  p.za = copy_anchor ? 0.0 : zia[k];
+  p.lb = lb[k];
+  p.ub = ub[k];
+  p.gam = v.gam[k];
+  p.cost = v.cost_int[k];
+  return p;
+}
+
 // Dual half-step of one row.  Returns the new *iterate* y'; `act` is the row activity at the T
 // output (K·[x̂, ẑ]).  On a Halpern iteration y' = λ(2ŷ − y) + (1 − λ)y_anchor and the iterate's
 // activity kz follows the same combination.
 template <bool CHECK, bool INIT>
-__device__ __forceinline__ double dual_step(const DeviceView &v, double *y, double *ya, double *kz, double *kza,
-                                            int row, double act, double yold, double sigma, bool copy_anchor,
-                                            bool halp, double lam, SmallAcc &a, bool dblk = false) {
-  const double lo = v.lo[row], hi = v.hi[row];
-  const double kold = kz[row];
+__device__ __forceinline__ double dual_step_p(double *y, double *ya, double *kz, double *kza, int row, double act,
+                                              const DPre &p, double sigma, bool copy_anchor, bool halp, double lam,
+                                              SmallAcc &a, bool dblk = false) {
+  const double lo = p.lo, hi = p.hi, yold = p.y;
+  const double kold = p.kz;
   double yanc, kanc;
   if (INIT) {
     yanc = yold;
@@ -150,8 +184,8 @@ __device__ __forceinline__ double dual_step(const DeviceView &v, double *y, doub
     yanc = yold;
     kanc = kold;
   } else {
-    yanc = ya[row];
-    kanc = kza[row];
+    yanc = p.ya;
+    kanc = p.kza;
   }
   if (copy_anchor) {
     ya[row] = yanc;
@@ -159,7 +193,7 @@ __device__ __forceinline__ double dual_step(const DeviceView &v, double *y, doub
   }
   double ynew = yold, knew = act;
   if (!INIT) {
-    const double rr = v.rho[row];
+    const double rr = p.rho;
     const double yT = dual_prox(yold, sigma * rr * rr, 2.0 * act - kold, lo, hi);
     const double t = (yT - yold) / rr;
     a.mvy += t * t;
@@ -176,27 +210,42 @@ __device__ __forceinline__ double dual_step(const DeviceView &v, double *y, doub
   if (CHECK) (dblk ? a.lagrD : a.lagr) += row_lagr(yold, lo, hi);
   return ynew;
 }
+template <bool CHECK, bool INIT>
+__device__ __forceinline__ double dual_step(const DeviceView &v, double *y, double *ya, double *kz, double *kza,
+                                            int row, double act, double yold, double sigma, bool copy_anchor,
+                                            bool halp, double lam, SmallAcc &a, bool dblk = false) {
+  DPre p = dual_pre<INIT>(v, y, ya, kz, kza, row, copy_anchor);
+  p.y = yold;
+  return dual_step_p<CHECK, INIT>(y, ya, kz, kza, row, act, p, sigma, copy_anchor, halp, lam, a, dblk);
+}
 
 // Primal half-step of one small variable.  Stores the new iterate, returns the T output ẑ (the
-// value every row activity and the certificate use).
+// value every row activity and the certificate use).  rc = cost - Kᵀy.
 template <bool CHECK>
-__device__ __forceinline__ double primal_step(const DeviceView &v, double *zi, double *zia, const double *lb,
-                                              const double *ub, int k, double rc, double tau, bool copy_anchor,
-                                              bool halp, double lam, SmallAcc &a, bool dblk = false) {
-  const double old = zi[k];
+__device__ __forceinline__ double primal_step_p(double *zi, double *zia, int k, double rc, const ZPre &p, double tau,
+                                                bool copy_anchor, bool halp, double lam, SmallAcc &a,
+                                                bool dblk = false) {
+  const double old = p.z;
   if (copy_anchor) zia[k] = old;
-  const double zanc = copy_anchor ? old : zia[k];
-  const double g = v.gam[k];
-  const double nz = fmin(fmax(old - tau * g * g * rc, lb[k]), ub[k]);
+  const double zanc = copy_anchor ? old : p.za;
+  const double g = p.gam;
+  const double nz = fmin(fmax(old - tau * g * g * rc, p.lb), p.ub);
   zi[k] = halp ? lam * (2.0 * nz - old) + (1.0 - lam) * zanc : nz;
   const double t = (nz - old) / g;
   a.mvz += t * t;
   if (CHECK) {
     const double u = (nz - zanc) / g;
     a.dsz += u * u;
-    (dblk ? a.lagrD : a.lagr) += rc > 0 ? lb[k] * rc : ub[k] * rc;
+    (dblk ? a.lagrD : a.lagr) += rc > 0 ? p.lb * rc : p.ub * rc;
   }
   return nz;
+}
+template <bool CHECK>
+__device__ __forceinline__ double primal_step(const DeviceView &v, double *zi, double *zia, const double *lb,
+                                              const double *ub, int k, double rc, double tau, bool copy_anchor,
+                                              bool halp, double lam, SmallAcc &a, bool dblk = false) {
+  const ZPre p = primal_pre(v, zi, zia, lb, ub, k, copy_anchor);
+  return primal_step_p<CHECK>(zi, zia, k, rc, p, tau, copy_anchor, halp, lam, a, dblk);
 }
 
 // Halpern weight of the current iteration for a slot (1 on plain iterations: w' = T(w))
@@ -207,7 +256,6 @@ __device__ __forceinline__ double halpern_lambda(const Ctrl *ctrl, bool halp, in
 }
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
-typedef anchor_t anc4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ float4 ld4(const float *p) { return *reinterpret_cast<const float4 *>(p); }
 // the routing-state streams (x, anchor): read and written once per iteration, so non-temporal
@@ -225,20 +273,12 @@ __device__ __forceinline__ void st_x4(float *p, f32x4 v, bool nt) {
   if (NEP_NT && nt) __builtin_nontemporal_store(v, reinterpret_cast<f32x4 *>(p));
   else *reinterpret_cast<f32x4 *>(p) = v;
 }
-__device__ __forceinline__ anc4 ld_a4(const anchor_t *p, bool nt) {
-  if (NEP_NT && nt) return __builtin_nontemporal_load(reinterpret_cast<const anc4 *>(p));
-  return *reinterpret_cast<const anc4 *>(p);
-}
-__device__ __forceinline__ void st_a4(anchor_t *p, anc4 v, bool nt) {
-  if (NEP_NT && nt) __builtin_nontemporal_store(v, reinterpret_cast<anc4 *>(p));
-  else *reinterpret_cast<anc4 *>(p) = v;
-}
 
 // one routing row's operands: x̄ row, delay row D[src, :] (if the row has delay-weighted
-// coefficients) and the anchor row (if needed)
+// coefficients) and the dense anchor row (if needed and the row's anchor is held dense)
 template <int CPL>
 __device__ __forceinline__ void load_row(const float *__restrict__ xrow, const float *__restrict__ drow,
-                                         const anchor_t *__restrict__ arow, bool nd, bool na, bool nt, int lane,
+                                         const float *__restrict__ arow, bool nd, bool na, bool nt, int lane,
                                          int NP, float (&xo)[4 * CPL], float (&dout)[4 * CPL], float (&ao)[4 * CPL]) {
 #pragma unroll
   for (int q = 0; q < CPL; ++q) {
@@ -248,10 +288,7 @@ __device__ __forceinline__ void load_row(const float *__restrict__ xrow, const f
     if (j0 < NP) {
       a = ld_x4(xrow + j0, nt);
       if (nd) d = ld4(drow + j0);
-      if (na) {
-        const anc4 h = ld_a4(arow + j0, nt);
-        an = f32x4{(float)h.x, (float)h.y, (float)h.z, (float)h.w};
-      }
+      if (na) an = ld_x4(arow + j0, nt);
     }
     xo[4 * q] = a.x; xo[4 * q + 1] = a.y; xo[4 * q + 2] = a.z; xo[4 * q + 3] = a.w;
     dout[4 * q] = d.x; dout[4 * q + 1] = d.y; dout[4 * q + 2] = d.z; dout[4 * q + 3] = d.w;
@@ -278,9 +315,12 @@ __device__ __forceinline__ void load_row(const float *__restrict__ xrow, const f
 // measured at 512x256 / ~14 LPs per launch: 0.382 ms per launch vs 0.402 at the compiler's own 86
 // VGPRs (5 waves) and 0.428 when forced to 8 waves (64 VGPRs + 68 B/lane of spills).  The
 // certificate iterations (fp64 Lagrangian terms, 143 VGPRs) run at 3 waves per SIMD.
-template <int CPL, bool CHECK, bool INIT, int TW>
+// FIRST: the block's first iteration, the only one (with INIT) where a restart decided at the
+// certificate iteration takes effect and the anchor is rewritten; the steady-state variant carries
+// no restart code (fewer registers live).
+template <int CPL, bool CHECK, bool INIT, bool FIRST, int TW>
 __global__ __launch_bounds__(kWave * TW) __attribute__((amdgpu_waves_per_eu(CHECK ? 2 : (TW == 16 ? 4 : 6), 8)))
-void x_pass(DeviceView v, const int32_t *__restrict__ slots, int first, int plain, int it, int nslots, int nt_i) {
+void x_pass(DeviceView v, const int32_t *__restrict__ slots, int plain, int it, int nslots, int nt_i) {
   const bool nt = nt_i != 0;
   constexpr int E = 4 * CPL;
   extern __shared__ __attribute__((aligned(16))) float lds[];   // [2][TW][NP] accumulators + [2][NP] constants
@@ -299,7 +339,7 @@ void x_pass(DeviceView v, const int32_t *__restrict__ slots, int first, int plai
   if (!ctrl->active) return;
   const int NP = v.NP, F = v.F, N = v.N;
   const float tau = INIT ? 0.f : (float)ctrl->tau;
-  const bool restart = INIT || (first && ctrl->restart_pending);
+  const bool restart = INIT || (FIRST && ctrl->restart_pending);
   const bool halp = !INIT && !plain;
   const double lamd = halpern_lambda(ctrl, halp, it);
   const float lam = (float)lamd;
@@ -308,7 +348,9 @@ void x_pass(DeviceView v, const int32_t *__restrict__ slots, int first, int plai
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int r0 = v.frow[f], nrows = v.frow[f + 1] - r0;
   float *__restrict__ x = v.x + slot * v.sx;
-  anchor_t *__restrict__ xa = v.xa + slot * v.sx;
+  float *__restrict__ xa = v.xa + slot * v.sx;
+  int32_t *__restrict__ acnt = v.acnt + (int64_t)slot * v.R;
+  AnchorEnt *__restrict__ aent = v.aent + ((int64_t)slot * v.R) * kAnchorK;
   float *__restrict__ th_row = v.theta + (int64_t)slot * v.R;   // per-row simplex thresholds (hints)
   const uint8_t *__restrict__ mask = v.mask + slot * v.smask + (int64_t)f * NP;
   float *__restrict__ kty = v.kty + slot * v.skty;
@@ -370,8 +412,23 @@ void x_pass(DeviceView v, const int32_t *__restrict__ slots, int first, int plai
     // no software prefetch of the next row: the registers it costs are worth more as occupancy
     // (0.575 vs 0.591 ms per launch before the LDS accumulators; other waves hide the latency)
     float xc[E], dc[E], ac[E];
+    // anchor row: kept sparse (<= kAnchorK (j, value) pairs, lanes 0..cnt-1 load one each) or dense
+    int acn = 0;
+    if (need_anchor) acn = NEP_SPARSE_ANCHOR ? __builtin_amdgcn_readfirstlane(acnt[r]) : kAnchorDense;
     load_row<CPL>(x + (int64_t)r * NP, v.D + (int64_t)(ri.src < 0 ? 0 : ri.src) * NP, xa + (int64_t)r * NP, nd,
-                  need_anchor, nt, lane, NP, xc, dc, ac);
+                  need_anchor && acn > kAnchorK, nt, lane, NP, xc, dc, ac);
+    if (need_anchor && acn <= kAnchorK) {
+      AnchorEnt ae{0, 0.f};
+      if (lane < acn) ae = aent[(int64_t)r * kAnchorK + lane];
+      // scatter the pairs into the lanes that own their destinations (ac is zero from load_row)
+      for (int k = 0; k < acn; ++k) {
+        const int jk = __builtin_amdgcn_readlane(ae.j, k);
+        const float vk = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ae.v), k));
+#pragma unroll
+        for (int e = 0; e < E; ++e)
+          if (4 * (lane + kWave * (e / 4)) + (e & 3) == jk) ac[e] = vk;
+      }
+    }
     const float m = ri.m, w = ri.w, wobj = ri.wobj, wsc = ri.wsc;
     float kx[E], cy5[E];
 #pragma unroll
@@ -487,7 +544,6 @@ void x_pass(DeviceView v, const int32_t *__restrict__ slots, int first, int plai
       s_dist += dd;
     }
     float *xrow = x + (int64_t)r * NP;
-    anchor_t *arow = xa + (int64_t)r * NP;
 #pragma unroll
     for (int q = 0; q < CPL; ++q) {
       const int j0 = 4 * (lane + kWave * q);
@@ -499,10 +555,37 @@ void x_pass(DeviceView v, const int32_t *__restrict__ slots, int first, int plai
           o[t] = halp ? lam * (2.f * xn[e] - xc[e]) + (1.f - lam) * xav[e] : xn[e];
         }
         st_x4(xrow + j0, f32x4{o[0], o[1], o[2], o[3]}, nt);
-        if (restart)
-          st_a4(arow + j0, anc4{(anchor_t)xav[4 * q], (anchor_t)xav[4 * q + 1], (anchor_t)xav[4 * q + 2],
-                                (anchor_t)xav[4 * q + 3]}, nt);
       }
+    }
+    if (restart) {
+      // new anchor = xav: compacted to (j, value) pairs when it has <= kAnchorK nonzeros (a point on
+      // the simplex usually has a handful), else written dense.  Same values either way.
+      int tot = 0;
+#pragma unroll
+      for (int e = 0; e < E; ++e) tot += __popcll(__ballot(4 * (lane + kWave * (e / 4)) < NP && xav[e] != 0.f));
+      if (NEP_SPARSE_ANCHOR && tot <= kAnchorK) {
+        int base = 0;
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          const bool nz = 4 * (lane + kWave * (e / 4)) < NP && xav[e] != 0.f;
+          const uint64_t b = __ballot(nz);
+          if (nz) {
+            const int pos = base + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32),
+                                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
+            aent[(int64_t)r * kAnchorK + pos] = AnchorEnt{4 * (lane + kWave * (e / 4)) + (e & 3), xav[e]};
+          }
+          base += __popcll(b);
+        }
+      } else {
+        tot = kAnchorDense;
+        float *arow = xa + (int64_t)r * NP;
+#pragma unroll
+        for (int q = 0; q < CPL; ++q) {
+          const int j0 = 4 * (lane + kWave * q);
+          if (j0 < NP) st_x4(arow + j0, f32x4{xav[4 * q], xav[4 * q + 1], xav[4 * q + 2], xav[4 * q + 3]}, nt);
+        }
+      }
+      if (lane == 0) acnt[r] = tot;
     }
     float sc = 0.f;
 #pragma unroll
@@ -719,6 +802,33 @@ __global__ __launch_bounds__(kNodeThreads) void node_pass(DeviceView v, const in
   if (!ctrl->active) return;
   const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x >> 6;
   const int NP = v.NP, F = v.F;
+  const DualLayout &dl = v.dl;
+  const IntLayout &il = v.il;
+  const bool copy_anchor = INIT || (first && ctrl->restart_pending);
+  double *zi = v.zi + slot * v.sint, *zia = v.zia + slot * v.sint;
+  const double *lb = v.lb + slot * v.sint, *ub = v.ub + slot * v.sint;
+  double *y = v.y + slot * v.sdual, *ya = v.ya + slot * v.sdual, *kz = v.kz + slot * v.sdual;
+  double *kza = v.kza + slot * v.sdual;
+  // wave 0, lane (< kNodeJ) = node: issue every load of the node's rows now, ahead of the partial sums
+  const int j = jb * kNodeJ + lane;
+  const bool valid = wave == 0 && lane < kNodeJ && j < v.N;
+  DPre p3{}, p5{}, p6{}, p7{};
+  ZPre pn{};
+  double yS = 0.0, nrm3 = 1.0, nrm5 = 1.0;
+  if (valid) {
+    p3 = dual_pre<INIT>(v, y, ya, kz, kza, dl.o3 + j, copy_anchor);
+    p5 = dual_pre<INIT>(v, y, ya, kz, kza, dl.o5 + j, copy_anchor);
+    if (v.has_n) {
+      p6 = dual_pre<INIT>(v, y, ya, kz, kza, dl.o6 + j, copy_anchor);
+      p7 = dual_pre<INIT>(v, y, ya, kz, kza, dl.o7 + j, copy_anchor);
+      pn = primal_pre(v, zi, zia, lb, ub, il.on + j, copy_anchor);
+      if (v.step2) yS = y[dl.oS];
+    }
+    if (CHECK) {
+      nrm3 = v.rownorm[dl.o3 + j];
+      nrm5 = v.rownorm[dl.o5 + j];
+    }
+  }
   {
     const int jj = threadIdx.x % kNodeJ, g = threadIdx.x / kNodeJ;
     const int jl = jb * kNodeJ + jj;
@@ -749,9 +859,7 @@ __global__ __launch_bounds__(kNodeThreads) void node_pass(DeviceView v, const in
   }
   __syncthreads();
   if (wave != 0) return;
-  // wave 0: lane (< kNodeJ) = node; fixed-order sums over the function groups
-  const int j = jb * kNodeJ + lane;
-  const bool valid = lane < kNodeJ && j < v.N;
+  // wave 0: fixed-order sums over the function groups
   double memc = 0.0, sumc = 0.0, U = 0.0, memr = 0.0, sumr = 0.0;
   if (lane < kNodeJ) {
 #pragma unroll 8
@@ -765,44 +873,33 @@ __global__ __launch_bounds__(kNodeThreads) void node_pass(DeviceView v, const in
       }
     }
   }
-  const DualLayout &dl = v.dl;
-  const IntLayout &il = v.il;
   const double tau = INIT ? 0.0 : ctrl->tau, sigma = ctrl->sigma;
-  const bool copy_anchor = INIT || (first && ctrl->restart_pending);
   const bool halp = !INIT && !plain;
   const double lam = halpern_lambda(ctrl, halp, it);
-  double *zi = v.zi + slot * v.sint, *zia = v.zia + slot * v.sint;
-  const double *lb = v.lb + slot * v.sint, *ub = v.ub + slot * v.sint;
-  double *y = v.y + slot * v.sdual, *ya = v.ya + slot * v.sdual, *kz = v.kz + slot * v.sdual;
-  double *kza = v.kza + slot * v.sdual;
   float *kty = v.kty + slot * v.skty;
   SmallAcc a;
   double score_n = 0.0, score_n_rep = 0.0;
   if (valid && CHECK) {
     // certificate point (see x_pass): C3 at the repaired c, C5 (x only)
-    a.res = fmax(a.res, row_viol(memr, v.lo[dl.o3 + j], v.hi[dl.o3 + j]) / v.rownorm[dl.o3 + j]);
-    a.res = fmax(a.res, row_viol(U, v.lo[dl.o5 + j], v.hi[dl.o5 + j]) / v.rownorm[dl.o5 + j]);
+    a.res = fmax(a.res, row_viol(memr, p3.lo, p3.hi) / nrm3);
+    a.res = fmax(a.res, row_viol(U, p5.lo, p5.hi) / nrm5);
   }
   if (valid) {
-    dual_step<CHECK, INIT>(v, y, ya, kz, kza, dl.o3 + j, memc, y[dl.o3 + j], sigma, copy_anchor, halp, lam, a);
-    const double y5n = dual_step<CHECK, INIT>(v, y, ya, kz, kza, dl.o5 + j, U, y[dl.o5 + j], sigma, copy_anchor, halp,
-                                              lam, a);
+    dual_step_p<CHECK, INIT>(y, ya, kz, kza, dl.o3 + j, memc, p3, sigma, copy_anchor, halp, lam, a);
+    const double y5n = dual_step_p<CHECK, INIT>(y, ya, kz, kza, dl.o5 + j, U, p5, sigma, copy_anchor, halp, lam, a);
     kty[(int64_t)F * NP + j] = (float)y5n;
     if (v.has_n) {
-      const double y6 = y[dl.o6 + j], y7 = y[dl.o7 + j];
-      const double yS = v.step2 ? y[dl.oS] : 0.0;
-      const double kty_n = -v.M * y6 - y7 + v.score_n_coef * yS;
-      const double nn = primal_step<CHECK>(v, zi, zia, lb, ub, il.on + j, v.cost_int[il.on + j] - kty_n, tau,
-                                           copy_anchor, halp, lam, a);
-      dual_step<CHECK, INIT>(v, y, ya, kz, kza, dl.o6 + j, sumc - v.M * nn, y6, sigma, copy_anchor, halp, lam, a);
-      dual_step<CHECK, INIT>(v, y, ya, kz, kza, dl.o7 + j, sumc - nn, y7, sigma, copy_anchor, halp, lam, a);
+      const double kty_n = -v.M * p6.y - p7.y + v.score_n_coef * yS;
+      const double nn = primal_step_p<CHECK>(zi, zia, il.on + j, pn.cost - kty_n, pn, tau, copy_anchor, halp, lam, a);
+      dual_step_p<CHECK, INIT>(y, ya, kz, kza, dl.o6 + j, sumc - v.M * nn, p6, sigma, copy_anchor, halp, lam, a);
+      dual_step_p<CHECK, INIT>(y, ya, kz, kza, dl.o7 + j, sumc - nn, p7, sigma, copy_anchor, halp, lam, a);
       score_n = v.score_n_coef * nn;
       if (CHECK) {
         // repaired n: the T output clamped into [sum c / M, sum c + eps] (C6/C7 at the repaired c)
-        const double lon = fmax(lb[il.on + j], sumr / v.M), hin = fmin(ub[il.on + j], sumr + v.eps);
+        const double lon = fmax(pn.lb, sumr / v.M), hin = fmin(pn.ub, sumr + v.eps);
         const double nr = lon > hin ? lon : fmin(fmax(nn, lon), hin);
         a.res = fmax(a.res, lon - hin);
-        a.pobj += v.cost_int[il.on + j] * nr;
+        a.pobj += pn.cost * nr;
         v.zr[slot * v.sint + il.on + j] = nr;
         score_n_rep = v.score_n_coef * nr;
       }
@@ -868,36 +965,38 @@ __global__ __launch_bounds__(256) void dblock_pass(DeviceView v, const int32_t *
 template <bool CHECK, bool INIT>
 __global__ __launch_bounds__(256) void scalar_pass(DeviceView v, const int32_t *__restrict__ slots, int first,
                                                    int plain, int it, int block_len) {
-  __shared__ double red[256];
   __shared__ double tot[NTS + NBS];
   const int slot = slots[blockIdx.x];
   Ctrl *ctrl = v.ctrl + slot;
   if (!ctrl->active) return;
   const int tid = threadIdx.x;
+  const int lane = tid & (kWave - 1), wave = tid >> 6;
   const double *tp = v.tpart + slot * v.stpart;
   const double *bp = v.bpart + slot * v.sbpart;
   const int nb = v.F + v.JB;
-  // deterministic block reductions (fixed order per thread, fixed tree)
-  for (int k = 0; k < NTS + NBS; ++k) {
+  // deterministic reductions of the partials (fixed per-lane order, fixed wave tree): the fields are
+  // dealt over the 4 waves, one wave reduces a field alone (no block-wide tree per field).  Plain
+  // step-2 iterations need only the fields of the step-2 rows (sum c, the score row).
+  for (int k = wave; k < NTS + NBS; k += 4) {
+    const bool needed = CHECK || INIT || k == TS_SCORE || k == NTS + BS_SUMC_NEW || k == NTS + BS_SCORE_N;
+    if (!needed) {
+      if (lane == 0) tot[k] = 0.0;
+      continue;
+    }
     const bool is_max = (k == NTS + BS_RES);
     double acc = 0.0;
     if (k < NTS) {
-      for (int t = tid; t < v.F; t += 256) acc += tp[(int64_t)t * NTS + k];
+      for (int t = lane; t < v.F; t += kWave) acc += tp[(int64_t)t * NTS + k];
     } else {
-      for (int t = tid; t < nb; t += 256) {
+      for (int t = lane; t < nb; t += kWave) {
         const double u = bp[(int64_t)t * NBS + (k - NTS)];
         acc = is_max ? fmax(acc, u) : acc + u;
       }
     }
-    red[tid] = acc;
-    __syncthreads();
-    for (int s = 128; s > 0; s >>= 1) {
-      if (tid < s) red[tid] = is_max ? fmax(red[tid], red[tid + s]) : red[tid] + red[tid + s];
-      __syncthreads();
-    }
-    if (tid == 0) tot[k] = red[0];
-    __syncthreads();
+    acc = is_max ? wave_max_d(acc) : wave_sum_d(acc);
+    if (lane == 0) tot[k] = acc;
   }
+  __syncthreads();
   // step-2 certificate: G(lambda_q) = min over (a, d, T) of ca a + cd d + lambda_q T on the boxes and
   // the rows D3a/D3b/D4, by its vertices (3 of at most 12 half-spaces g . (a, d, T) >= h: 220
   // triples, one per thread).  A vertex is accepted within 1e-9 of every half-space: accepting a
@@ -1047,7 +1146,7 @@ __global__ __launch_bounds__(256) void scalar_pass(DeviceView v, const int32_t *
       if (isfinite(gmin[q][0])) lagr = fmax(lagr, a.lagr + tot[NTS + BS_LK0 + q] + gmin[q][0]);
   }
   const double gap = pobj - lagr;
-  const double tol = v.prm[0], cutoff = v.prm[1];
+  const double tol = v.prm[0], cutoff = v.prm[1], gap_tol = v.prm[2];
   ctrl->pobj = pobj;
   if (ctrl->exact && isfinite(pobj) && res <= tol) {
     // The node box fixes every variable that carries cost (a leaf of a model whose routing has no
@@ -1065,7 +1164,7 @@ __global__ __launch_bounds__(256) void scalar_pass(DeviceView v, const int32_t *
   if (lagr > ctrl->best_lagr) ctrl->best_lagr = lagr;
   ctrl->pres = res;
   ctrl->gap = gap;
-  if (isfinite(lagr) && res <= tol && gap <= tol * fmax(1.0, fabs(lagr))) {
+  if (isfinite(lagr) && res <= tol && gap <= gap_tol * fmax(1.0, fabs(lagr))) {
     ctrl->status = 0; ctrl->active = 0; return;
   }
   if (ctrl->best_lagr > cutoff) { ctrl->status = 3; ctrl->active = 0; return; }
@@ -1131,6 +1230,7 @@ __global__ void init_slot(DeviceView v, const int32_t *__restrict__ slots, const
     // the 512x256 bench children: 81/96 certified within 20k iterations without a floor, 95/96 with
     // floor 2, 62k iterations in all instead of 304k; tools/floor_probe.py).
     if (warm && v.warm_omega_floor > 0) ctrl->omega_lo = fmin(ctrl->omega * v.warm_omega_floor, ctrl->omega_hi);
+    if (warm && v.warm_omega_cap > 0) ctrl->omega_hi = fmax(ctrl->omega * v.warm_omega_cap, ctrl->omega_lo);
     ctrl->tau = eta / ctrl->omega;
     ctrl->sigma = eta * ctrl->omega;
     ctrl->status = 1;
@@ -1187,13 +1287,15 @@ static hipError_t launch_x_tw(const DeviceView &v, const int32_t *slots, int nsl
   dim3 grid(8 * ((v.F * nslots + 7) / 8)), block(kWave * TW);
   const size_t lds = (size_t)(2 * TW + 2) * v.NP * sizeof(float) +
                     (check ? (size_t)2 * TW * v.NP * sizeof(float) + 2 * v.NP * sizeof(double) : 0);
-  const int fi = first ? 1 : 0, pl = plain ? 1 : 0;
+  const int pl = plain ? 1 : 0;
   // non-temporal routing streams only when the iterating slots' x + anchor exceed ~160 MB (see ld_x4)
   const int nt = (double)nslots * 2.0 * (double)v.sx * sizeof(float) > 160e6 ? 1 : 0;
-  if (init) hipLaunchKernelGGL((x_pass<CPL, false, true, TW>), grid, block, lds, s, v, slots, fi, pl, it, nslots, nt);
+  if (init) hipLaunchKernelGGL((x_pass<CPL, false, true, false, TW>), grid, block, lds, s, v, slots, pl, it, nslots, nt);
   else if (check)
-    hipLaunchKernelGGL((x_pass<CPL, true, false, TW>), grid, block, lds, s, v, slots, fi, pl, it, nslots, nt);
-  else hipLaunchKernelGGL((x_pass<CPL, false, false, TW>), grid, block, lds, s, v, slots, fi, pl, it, nslots, nt);
+    hipLaunchKernelGGL((x_pass<CPL, true, false, false, TW>), grid, block, lds, s, v, slots, pl, it, nslots, nt);
+  else if (first)
+    hipLaunchKernelGGL((x_pass<CPL, false, false, true, TW>), grid, block, lds, s, v, slots, pl, it, nslots, nt);
+  else hipLaunchKernelGGL((x_pass<CPL, false, false, false, TW>), grid, block, lds, s, v, slots, pl, it, nslots, nt);
   return hipGetLastError();
 }
 
