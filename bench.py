@@ -389,7 +389,10 @@ def main():
             td.destroy_process_group()
         return
 
-    per_lp = 8.0 * P                                     # x read + write, fp32
+    # algorithmic bytes of one PDHG iteration of one LP: SURVEY.md §8(d) B_iter = 4 (2P + 2FN + 2N + 2m),
+    # x read + write, c and n read + write, duals read + write (fp32 units), P = R x N routing entries
+    # after exact aggregation, m = the dualised rows (nep_model_info.bytes_per_iter)
+    per_lp = float(m.info.bytes_per_iter)
     launch_ms = st["x_pass_ms"] / max(1, st["x_pass_sampled"])
     lps_per_launch = st["x_pass_lp_iters"] / max(1, st["x_pass_sampled"])
     achieved = per_lp * lps_per_launch / (launch_ms * 1e-3) / 1e9 if launch_ms > 0 else 0.0
@@ -433,6 +436,8 @@ def main():
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_over_algorithmic": traffic_ratio,
                      "kernel": "x_pass", "algorithmic_bytes_per_launch": per_lp * lps_per_launch,
+                     "algorithmic_bytes_per_lp_iter": per_lp,
+                     "algorithmic_formula": "SURVEY.md 8(d) B_iter = 4(2P + 2FN + 2N + 2m), P = R*N, m = dualised rows",
                      "avg_launch_ms": launch_ms, "sampled_launches": st["x_pass_sampled"]},
         "cpu_baseline": cpu,
         "bnb": bnb,

@@ -83,6 +83,8 @@ typedef struct {
                                   (0: default 2; < 0: no floor) */
   double gap_tol;              /* API 5: certified objective gap (relative, as tol); 0: = tol.  A tighter
                                   gap for an LP whose state warm-starts others (a B&B root) */
+  double warm_omega_cap;       /* API 5: warm starts: the primal weight stays <= this x the parent's
+                                  (0: default 4; < 0: no cap).  DESIGN.md §4 "Warm starts" */
 } nep_lp_opts;
 
 typedef struct {

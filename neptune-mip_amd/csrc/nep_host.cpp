@@ -570,8 +570,6 @@ int setup_device(Model &m, int max_batch, void *stream) {
   v.rs_suff = 0.2; v.rs_nec = 0.9; v.rs_art = 0.36; v.omega_smooth = 0.5;   // necessary 0.9: DESIGN.md §4
   if (const char *e = std::getenv("NEP_RESTART")) std::sscanf(e, "%lf,%lf,%lf", &v.rs_suff, &v.rs_nec, &v.rs_art);
   if (const char *e = std::getenv("NEP_OMEGA_SMOOTH")) v.omega_smooth = std::atof(e);
-  v.warm_omega_cap = 0.0;
-  if (const char *e = std::getenv("NEP_WARM_OMEGA_CAP")) v.warm_omega_cap = std::atof(e);
   int rc;
   if ((rc = upload(m, &v.rows, m.rows))) return rc;
   if ((rc = upload(m, &v.frow, m.frow))) return rc;
@@ -609,7 +607,7 @@ int setup_dense(Model &m, const nep_model_desc &d) {
   v.skty = (int64_t)F * NP + NP + 4;
   v.stpart = (int64_t)F * NTS;
   v.sbpart = (int64_t)(F + m.JB) * NBS;
-  v.snpart = (int64_t)F * 3 * NP;
+  v.snpart = (int64_t)F * 2 * NP;
   v.srpart = (int64_t)F * 2 * NP;
   if ((rc = dalloc(m, &v.x, (size_t)B * v.sx))) return rc;
   if ((rc = dalloc(m, &v.xa, (size_t)B * v.sx))) return rc;
@@ -863,6 +861,7 @@ nep_lp_opts resolve_opts(const nep_lp_opts *opts) {
   o.check_every = 64;
   o.warm_start = 0;
   o.warm_omega_floor = 2.0;
+  o.warm_omega_cap = 4.0;
   if (opts) {
     if (opts->tol > 0) o.tol = opts->tol;
     o.cutoff = opts->cutoff;
@@ -871,6 +870,7 @@ nep_lp_opts resolve_opts(const nep_lp_opts *opts) {
     o.warm_start = opts->warm_start;
     if (opts->warm_omega_floor != 0) o.warm_omega_floor = opts->warm_omega_floor < 0 ? 0.0 : opts->warm_omega_floor;
     o.gap_tol = opts->gap_tol;
+    if (opts->warm_omega_cap != 0) o.warm_omega_cap = opts->warm_omega_cap < 0 ? 0.0 : opts->warm_omega_cap;
   }
   if (!(o.gap_tol > 0)) o.gap_tol = o.tol;
   return o;
@@ -893,6 +893,7 @@ int submit(Model &m, int n, const int32_t *slots, const double *lbi, const doubl
   m.run = o;
   DeviceView &v = m.v;
   v.warm_omega_floor = o.warm_omega_floor;
+  v.warm_omega_cap = o.warm_omega_cap;
   v.max_iters = o.max_iters;
   // tol / cutoff of every LP in flight: device memory, read by the (graph-replayed) blocks
   m.prm_host[0] = o.tol;

@@ -14,7 +14,7 @@
 //   y     [n_dual] f64  duals of the dualised rows   + anchor ya, activity kz (iterate) / kza (anchor)
 //   kty   [F*NP + NP + 4] f32  packed duals the x pass needs: y1+y2 per (f,j), y5 per j, yS
 //   tpart [F][NTS] f64  per-function scalars of the rows (score row, objective, Lagrangian, movement)
-//   npart [F][3][NP] f64 per-(function, node) shares of the node rows: memory, c, CPU
+//   npart [F][2][NP] f64 per-(function, node) shares of the node rows: c (memory = mem_f * c), CPU
 //   rpart [F][2][NP] f64 the same memory / c shares at the repaired certificate point
 //   bpart [F+JB][NBS] f64 per-block scalars of the small variables
 //   ctrl  Ctrl          step sizes, primal weight, restart state, status
@@ -50,6 +50,7 @@ struct AnchorEnt {
 };
 
 constexpr int kWave = 64;
+constexpr int64_t kOmegaTrained = 1024;  // warm_omega_cap applies when the parent lineage iterated this much
 constexpr int kNodeWaves = 16;           // waves per node-pass workgroup (each sums F/16 functions)
 constexpr int kNodeThreads = kWave * kNodeWaves;
 constexpr int kNodeJ = 16;               // nodes per node-pass workgroup
@@ -90,6 +91,8 @@ struct Ctrl {
   double omega_lo, omega_hi;
   int64_t k, k_since_restart, ks_base;   // ks_base: Halpern counter at the block's first iteration
   int64_t max_iters;                     // this LP's iteration limit (nep_lp_opts of its submit)
+  int64_t k_lineage;                     // iterations along the warm-start lineage (parent's + own): the
+                                         // primal weight counts as adapted (warm cap) from kOmegaTrained on
   int32_t status, active, restart_pending;
   int32_t exact;                         // 1: the node box fixes the objective (see scalar_pass)
 };
@@ -137,7 +140,7 @@ struct DeviceView {
   // passed by value would stay frozen at capture time.
   const double *prm;
   double warm_omega_floor;               // warm starts: primal weight kept >= this x the parent's (0: off)
-  double warm_omega_cap;                 // warm starts: primal weight kept <= this x the parent's (0: off; NEP_WARM_OMEGA_CAP)
+  double warm_omega_cap;                 // warm starts: primal weight kept <= this x the parent's (0: off)
   // restart rule on the fixed-point residual (sufficient / necessary / artificial, PDLP's 0.2 / 0.8 /
   // 0.36; necessary 0.9 here, measured) and the primal-weight smoothing (0.5); NEP_RESTART /
   // NEP_OMEGA_SMOOTH override them

@@ -421,12 +421,15 @@ void x_pass(DeviceView v, const int32_t *__restrict__ slots, int plain, int it, 
       AnchorEnt ae{0, 0.f};
       if (lane < acn) ae = aent[(int64_t)r * kAnchorK + lane];
       // scatter the pairs into the lanes that own their destinations (ac is zero from load_row)
+      // (destination j lives in lane (j >> 2) & 63, register 4 * (j >> 8) + (j & 3): see load_row)
       for (int k = 0; k < acn; ++k) {
         const int jk = __builtin_amdgcn_readlane(ae.j, k);
         const float vk = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ae.v), k));
+        const int ek = ((jk >> 8) << 2) | (jk & 3);   // wave-uniform
+        const bool mine = lane == ((jk >> 2) & (kWave - 1));
 #pragma unroll
         for (int e = 0; e < E; ++e)
-          if (4 * (lane + kWave * (e / 4)) + (e & 3) == jk) ac[e] = vk;
+          if (e == ek) ac[e] = mine ? vk : ac[e];
       }
     }
     const float m = ri.m, w = ri.w, wobj = ri.wobj, wsc = ri.wsc;
@@ -640,7 +643,7 @@ void x_pass(DeviceView v, const int32_t *__restrict__ slots, int plain, int it, 
   const double *lb = v.lb + slot * v.sint, *ub = v.ub + slot * v.sint;
   double *y = v.y + slot * v.sdual, *ya = v.ya + slot * v.sdual, *kz = v.kz + slot * v.sdual;
   double *kza = v.kza + slot * v.sdual;
-  double *np_ = v.npart + slot * v.snpart + (int64_t)f * 3 * NP;
+  double *np_ = v.npart + slot * v.snpart + (int64_t)f * 2 * NP;
   const double memf = v.mem_f[f];
   const double yD3a = v.step2 ? y[dl.oD3a] : 0.0, yD3b = v.step2 ? y[dl.oD3b] : 0.0;
   const double yD4 = v.step2 ? y[dl.oD4] : 0.0;
@@ -688,9 +691,8 @@ void x_pass(DeviceView v, const int32_t *__restrict__ slots, int plain, int it, 
       dual_step<CHECK, INIT>(v, y, ya, kz, kza, dl.oD2 + idx, mtn + cn, yd2, sigma, copy_anchor, halp, lamd, a, true);
     }
     kty[(int64_t)f * NP + j] = (float)(y1n + y2n);
-    np_[j] = memf * cn;
-    np_[NP + j] = cn;
-    np_[2 * NP + j] = U;
+    np_[j] = cn;                 // node_pass forms the memory share mem_f * c itself
+    np_[NP + j] = U;
     sumc += cn;
     if (CHECK) {
       // Certificate point: the routing x̂ of this iteration with the small variables REPAIRED, in
@@ -759,6 +761,7 @@ void x_pass(DeviceView v, const int32_t *__restrict__ slots, int plain, int it, 
   }
 }
 
+template <bool ALL>
 __device__ __forceinline__ void write_bpart(double *bp, const SmallAcc &a, double sumc, double score_n,
                                             double score_n_rep, int lane) {
   double vals[NBS];
@@ -777,8 +780,10 @@ __device__ __forceinline__ void write_bpart(double *bp, const SmallAcc &a, doubl
   vals[BS_TLO] = vals[BS_THI] = 0.0;
 #pragma unroll
   for (int q = 0; q < kNLam; ++q) vals[BS_LK0 + q] = 0.0;
+  // plain step-2 iterations: scalar_pass reads only the row fields (ALL = false)
 #pragma unroll
   for (int k = 0; k < NBS; ++k) {
+    if (!ALL && k != BS_SCORE_N && k != BS_SUMC_NEW) continue;
     const double t = (k == BS_RES) ? wave_max_d(vals[k]) : wave_sum_d(vals[k]);
     if (lane == 0) bp[k] = t;
   }
@@ -838,10 +843,11 @@ __global__ __launch_bounds__(kNodeThreads) void node_pass(DeviceView v, const in
     if (jl < v.N) {
       const double *np_ = v.npart + slot * v.snpart;
       for (int f = f0; f < f1; ++f) {
-        const double *p = np_ + (int64_t)f * 3 * NP;
-        memc += p[jl];
-        sumc += p[NP + jl];
-        U += p[2 * NP + jl];
+        const double *p = np_ + (int64_t)f * 2 * NP;
+        const double c = p[jl];
+        memc += __dmul_rn(v.mem_f[f], c);   // the product x_pass used to store: same rounding, no FMA
+        sumc += c;
+        U += p[NP + jl];
       }
       if (CHECK) {
         const double *rp = v.rpart + slot * v.srpart;
@@ -905,7 +911,10 @@ __global__ __launch_bounds__(kNodeThreads) void node_pass(DeviceView v, const in
       }
     }
   }
-  write_bpart(v.bpart + slot * v.sbpart + ((int64_t)F + jb) * NBS, a, 0.0, score_n, score_n_rep, lane);
+  // the node blocks' scalar partials: read by scalar_pass on init / certificate iterations, and for the
+  // step-2 score row on every step-2 iteration (plain step-1 iterations skip 21 wave reductions)
+  if (CHECK || INIT) write_bpart<true>(v.bpart + slot * v.sbpart + ((int64_t)F + jb) * NBS, a, 0.0, score_n, score_n_rep, lane);
+  else if (v.step2) write_bpart<false>(v.bpart + slot * v.sbpart + ((int64_t)F + jb) * NBS, a, 0.0, score_n, score_n_rep, lane);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1115,6 +1124,7 @@ __global__ __launch_bounds__(256) void scalar_pass(DeviceView v, const int32_t *
   // iteration), a whole block afterwards — per slot, so slots may join between blocks
   const int64_t done = ctrl->k == 0 ? 1 : block_len;
   ctrl->k += done;
+  ctrl->k_lineage += done;
   ctrl->k_since_restart += done;
   ctrl->restart_pending = 0;
   if (tot[TS_EMPTY] > 0) { ctrl->status = 2; ctrl->active = 0; return; }
@@ -1230,7 +1240,14 @@ __global__ void init_slot(DeviceView v, const int32_t *__restrict__ slots, const
     // the 512x256 bench children: 81/96 certified within 20k iterations without a floor, 95/96 with
     // floor 2, 62k iterations in all instead of 304k; tools/floor_probe.py).
     if (warm && v.warm_omega_floor > 0) ctrl->omega_lo = fmin(ctrl->omega * v.warm_omega_floor, ctrl->omega_hi);
-    if (warm && v.warm_omega_cap > 0) ctrl->omega_hi = fmax(ctrl->omega * v.warm_omega_cap, ctrl->omega_lo);
+    // ... and, once that weight has been adapted over kOmegaTrained iterations of its lineage, at most
+    // warm_omega_cap times it: without a cap the first restart after a warm start can raise it 50x on
+    // the dual's large move toward the fixings, and the child then stalls at the node-LP limit (512x256
+    // bench seed 0: 39/128 children certified, 125/128 with cap 4).  A weight that never
+    // adapted (a root certified in a few iterations) is left free.
+    if (!warm) ctrl->k_lineage = 0;
+    if (warm && v.warm_omega_cap > 0 && ctrl->k_lineage >= kOmegaTrained)
+      ctrl->omega_hi = fmax(ctrl->omega * v.warm_omega_cap, ctrl->omega_lo);
     ctrl->tau = eta / ctrl->omega;
     ctrl->sigma = eta * ctrl->omega;
     ctrl->status = 1;

@@ -52,7 +52,7 @@ def _counters(d, F):
         q = ("select k.name, k.grid_x * k.grid_y / k.workgroup_x, p.counter_name, p.value from counters_collection p "
              "join kernels k on k.dispatch_id = p.dispatch_id")
         for name, wgs, cname, v in c.execute(q):
-            if "x_pass" in name and "false, false" in name:
+            if "x_pass" in name and "false, false, false" in name:   # steady state: not CHECK/INIT/FIRST
                 vals.setdefault((cname, int(wgs) // F), []).append(float(v))
     return vals
 
@@ -75,8 +75,23 @@ def summarize(fetch_dir, write_dir):
     print(json.dumps(out, indent=1))
 
 
+def summarize_sq(d):
+    """Average of every counter of one PMC pass (e.g. the SQ_* issue / wait counters) over the
+    steady-state x_pass launches with the most LP slots."""
+    import bench
+    a = bench.parse([])
+    c = _counters(d, a.functions)
+    top = max(k[1] for k in c)
+    out = {"workload": bench.workload_name(a), "kernel": "x_pass<CPL,false,false,false>", "lps_per_launch": top,
+           "counters": {k[0]: sum(v) / len(v) for k, v in c.items() if k[1] == top},
+           "launches": max(len(v) for k, v in c.items() if k[1] == top)}
+    print(json.dumps(out, indent=1))
+
+
 if __name__ == "__main__":
     if sys.argv[1] == "run":
         run()
+    elif sys.argv[1] == "sq":
+        summarize_sq(sys.argv[2])
     else:
         summarize(sys.argv[2], sys.argv[3])
