@@ -143,8 +143,14 @@ struct Model {
   std::vector<int32_t> act;     // slots currently iterating
   std::vector<uint8_t> busy;    // per slot: iterating
   nep_lp_opts run{};            // options of the LPs in flight
+  // pipelined blocks (advance): the block launched last, not yet waited for — the slots it iterates,
+  // whether it carries the sampled x-pass events — and the pinned copy of the slots' Ctrl it ends with
+  bool inflight = false, inflight_sampled = false;
+  std::vector<int32_t> launched;
+  Ctrl *h_ctrl = nullptr;
   ~Model() {
     if (stream) (void)hipStreamSynchronize(stream);
+    if (h_ctrl) (void)hipHostFree(h_ctrl);
     for (void *p : allocs) (void)hipFree(p);
     for (hipGraphExec_t g : block_graph)
       if (g) (void)hipGraphExecDestroy(g);
@@ -630,6 +636,11 @@ int setup_dense(Model &m, const nep_model_desc &d) {
   if ((rc = dalloc(m, &v.npart, (size_t)B * v.snpart))) return rc;
   if ((rc = dalloc(m, &v.rpart, (size_t)B * v.srpart))) return rc;
   if ((rc = dalloc(m, &v.ctrl, (size_t)B))) return rc;
+  {
+    void *h = nullptr;
+    if (hipHostMalloc(&h, sizeof(Ctrl) * B) != hipSuccess) return fail(NEP_ERR_NOMEM, "hipHostMalloc (Ctrl)");
+    m.h_ctrl = static_cast<Ctrl *>(h);
+  }
   if ((rc = dalloc(m, &m.d_prm, 3))) return rc;
   v.prm = m.d_prm;
   if ((rc = dalloc(m, &m.d_slots, (size_t)B))) return rc;
@@ -987,69 +998,82 @@ hipError_t block_graph(Model &m, int na, hipGraphExec_t *out) {
   return hipSuccess;
 }
 
+// One block of `ce` iterations on the iterating slots (m.act), enqueued without waiting: it == 0 is
+// the certificate iteration (a plain PDHG step whose input dual is the previous block's plain
+// output, so it satisfies the row sign constraints and its Lagrangian is a valid bound); restarts
+// decided there take effect at it == 1; it == ce - 1 is plain again; the others are reflected
+// Halpern steps.  Every 4th block runs eagerly with one steady-state x-pass launch bracketed by HIP
+// events on the model's stream (nep_get_stats); the others replay the block's launches as one HIP
+// graph (a block is 2-3 launches per iteration: at small sizes the iteration is launch-latency
+// bound).  The block ends with an async copy of every slot's Ctrl into pinned host memory.
+int launch_block(Model &m) {
+  DeviceView &v = m.v;
+  const int ce = m.run.check_every;
+  const int na = (int)m.act.size();
+  const int sample_it = (ce >= 4 && m.blocks % 4 == 0) ? 2 : -1;
+  m.blocks += 1;
+  bool eager = sample_it >= 0 || !m.graphs_ok;
+  if (!eager) {
+    hipGraphExec_t g = nullptr;
+    if (block_graph(m, na, &g) != hipSuccess) {
+      (void)hipGetLastError();
+      m.graphs_ok = false;   // e.g. a caller's stream that cannot be captured
+      eager = true;
+    } else {
+      HIPCHK(hipGraphLaunch(g, m.stream));
+      m.stats.x_pass_launches += ce;
+    }
+  }
+  for (int it = 0; it < ce && eager; ++it) {
+    const bool check = it == 0, first = it == 1;
+    const bool plain = !kHalpern || ce < 4 || it == 0 || it == ce - 1;
+    const bool sample = it == sample_it;
+    if (check && m.step2) HIPCHK(launch_dblock_pass(v, m.d_slots, na, m.stream));
+    if (sample) HIPCHK(hipEventRecord(m.ev0, m.stream));
+    HIPCHK(launch_x_pass(v, m.d_slots, na, check, false, first, plain, it, m.stream));
+    if (sample) HIPCHK(hipEventRecord(m.ev1, m.stream));
+    HIPCHK(launch_node_pass(v, m.d_slots, na, check, false, first, plain, it, m.stream));
+    if (m.step2 || check) HIPCHK(launch_scalar_pass(v, m.d_slots, na, check, false, first, plain, it, ce, m.stream));
+    m.stats.x_pass_launches += 1;
+  }
+  HIPCHK(hipMemcpyAsync(m.h_ctrl, v.ctrl, sizeof(Ctrl) * m.max_batch, hipMemcpyDeviceToHost, m.stream));
+  m.stats.lp_iterations += (int64_t)na * ce;
+  m.launched = m.act;
+  m.inflight = true;
+  m.inflight_sampled = sample_it >= 0;
+  return NEP_OK;
+}
+
 // Run blocks of `check_every` PDHG iterations on every iterating slot until at least `min_done`
 // of them have finished (min_done <= 0: exactly one block).  Finished slots are reported in
-// done[0 .. *n_done) with their results.
+// done[0 .. *n_done) with their results.  Blocks are pipelined: once a block's results are read,
+// the next block of the still-iterating slots is enqueued BEFORE returning, so the device keeps
+// iterating while the caller branches, presolves and submits the next nodes (those join at the
+// block after; their initialisation is stream-ordered behind the block in flight).
 int advance(Model &m, int min_done, int32_t *n_done, int32_t *done, double *obj, double *pobj, int32_t *status,
             int64_t *iters) {
   *n_done = 0;
-  DeviceView &v = m.v;
-  const int ce = m.run.check_every;
-  std::vector<Ctrl> ctrl(m.max_batch);
-  while (!m.act.empty()) {
-    const int na = (int)m.act.size();
-    // Block of `ce` iterations: it == 0 is the certificate iteration (a plain PDHG step whose
-    // input dual is the previous block's plain output, so it satisfies the row sign constraints
-    // and its Lagrangian is a valid bound); restarts decided there take effect at it == 1;
-    // it == ce - 1 is plain again; the others are reflected Halpern steps.  One steady-state
-    // x-pass launch per block is bracketed by HIP events on the model's stream; the events are
-    // read after the block's own stream sync, so sampling adds no synchronisation.
-    // Every 4th block runs eagerly with one steady-state x-pass launch bracketed by HIP events
-    // (nep_get_stats); the others replay the block's launches as one HIP graph (a block is 2-3
-    // launches per iteration: at small sizes the iteration is launch-latency bound).
-    const int sample_it = (ce >= 4 && m.blocks % 4 == 0) ? 2 : -1;
-    m.blocks += 1;
-    bool eager = sample_it >= 0 || !m.graphs_ok;
-    if (!eager) {
-      hipGraphExec_t g = nullptr;
-      if (block_graph(m, na, &g) != hipSuccess) {
-        (void)hipGetLastError();
-        m.graphs_ok = false;   // e.g. a caller's stream that cannot be captured
-        eager = true;
-      } else {
-        HIPCHK(hipGraphLaunch(g, m.stream));
-        m.stats.x_pass_launches += ce;
-      }
+  while (true) {
+    if (!m.inflight) {
+      if (m.act.empty()) break;
+      int rc = launch_block(m);
+      if (rc) return rc;
     }
-    for (int it = 0; it < ce && eager; ++it) {
-      const bool check = it == 0, first = it == 1;
-      const bool plain = !kHalpern || ce < 4 || it == 0 || it == ce - 1;
-      const bool sample = it == sample_it;
-      if (check && m.step2) HIPCHK(launch_dblock_pass(v, m.d_slots, na, m.stream));
-      if (sample) HIPCHK(hipEventRecord(m.ev0, m.stream));
-      HIPCHK(launch_x_pass(v, m.d_slots, na, check, false, first, plain, it, m.stream));
-      if (sample) HIPCHK(hipEventRecord(m.ev1, m.stream));
-      HIPCHK(launch_node_pass(v, m.d_slots, na, check, false, first, plain, it, m.stream));
-      if (m.step2 || check) HIPCHK(launch_scalar_pass(v, m.d_slots, na, check, false, first, plain, it, ce, m.stream));
-      m.stats.x_pass_launches += 1;
-    }
-    HIPCHK(hipMemcpyAsync(ctrl.data(), v.ctrl, sizeof(Ctrl) * m.max_batch, hipMemcpyDeviceToHost, m.stream));
     HIPCHK(hipStreamSynchronize(m.stream));
-    if (sample_it >= 0) {
+    m.inflight = false;
+    if (m.inflight_sampled) {
       float ms = 0.f;
       HIPCHK(hipEventElapsedTime(&ms, m.ev0, m.ev1));
       m.stats.x_pass_ms += ms;
       m.stats.x_pass_sampled += 1;
-      m.stats.x_pass_lp_iters += na;
+      m.stats.x_pass_lp_iters += (int64_t)m.launched.size();
     }
-    m.stats.lp_iterations += (int64_t)na * ce;
-    std::vector<int32_t> still;
-    for (int s : m.act) {
-      if (ctrl[s].active) {
-        still.push_back(s);
-        continue;
-      }
-      const Ctrl &c = ctrl[s];
+    // results of the slots that block iterated (slots submitted meanwhile are not in it)
+    std::vector<uint8_t> fin(m.max_batch, 0);
+    for (int s : m.launched) {
+      const Ctrl &c = m.h_ctrl[s];
+      if (c.active) continue;
+      fin[s] = 1;
       const int k = (*n_done)++;
       done[k] = s;
       status[k] = c.status;
@@ -1058,15 +1082,21 @@ int advance(Model &m, int min_done, int32_t *n_done, int32_t *done, double *obj,
       obj[k] = c.status == NEP_LP_INFEASIBLE ? INF : (c.status == NEP_LP_OPTIMAL ? c.lagr : c.best_lagr);
       m.busy[s] = 0;
     }
-    if (still.size() != m.act.size()) {
+    if (*n_done > 0) {
+      std::vector<int32_t> still;
+      for (int s : m.act)
+        if (!fin[s]) still.push_back(s);
       m.act.swap(still);
       if (!m.act.empty())
         HIPCHK(hipMemcpyAsync(m.d_slots, m.act.data(), m.act.size() * sizeof(int32_t), hipMemcpyHostToDevice,
                               m.stream));
     }
+    if (!m.act.empty()) {
+      int rc = launch_block(m);   // the next block runs while the caller handles the finished slots
+      if (rc) return rc;
+    }
     if (min_done <= 0 || *n_done >= min_done) break;
   }
-  HIPCHK(hipStreamSynchronize(m.stream));
   return NEP_OK;
 }
 
