@@ -85,6 +85,9 @@ typedef struct {
                                   gap for an LP whose state warm-starts others (a B&B root) */
   double warm_omega_cap;       /* API 5: warm starts: the primal weight stays <= this x the parent's
                                   (0: default 4; < 0: no cap).  DESIGN.md §4 "Warm starts" */
+  double polish_after;         /* API 5: primal feasibility polishing may start after this many
+                                  iterations (0: default — 256 for warm starts, never for cold starts;
+                                  < 0: never).  DESIGN.md §4 "Polishing" */
 } nep_lp_opts;
 
 typedef struct {

@@ -628,6 +628,7 @@ int setup_dense(Model &m, const nep_model_desc &d) {
   if ((rc = dalloc(m, &v.ub, (size_t)B * v.sint))) return rc;
   if ((rc = dalloc(m, &v.y, (size_t)B * v.sdual))) return rc;
   if ((rc = dalloc(m, &v.ya, (size_t)B * v.sdual))) return rc;
+  if ((rc = dalloc(m, &v.ybak, (size_t)B * v.sdual))) return rc;
   if ((rc = dalloc(m, &v.kz, (size_t)B * v.sdual))) return rc;
   if ((rc = dalloc(m, &v.kza, (size_t)B * v.sdual))) return rc;
   if ((rc = dalloc(m, &v.kty, (size_t)B * v.skty))) return rc;
@@ -882,8 +883,12 @@ nep_lp_opts resolve_opts(const nep_lp_opts *opts) {
     if (opts->warm_omega_floor != 0) o.warm_omega_floor = opts->warm_omega_floor < 0 ? 0.0 : opts->warm_omega_floor;
     o.gap_tol = opts->gap_tol;
     if (opts->warm_omega_cap != 0) o.warm_omega_cap = opts->warm_omega_cap < 0 ? 0.0 : opts->warm_omega_cap;
+    o.polish_after = opts->polish_after;
   }
   if (!(o.gap_tol > 0)) o.gap_tol = o.tol;
+  // polishing: by default only warm-started LPs (B&B children) polish; a cold LP (a root) iterates on
+  // to its own certificate, whose more converged duals its children then start from
+  if (o.polish_after == 0) o.polish_after = o.warm_start ? 256.0 : -1.0;
   return o;
 }
 
@@ -905,6 +910,7 @@ int submit(Model &m, int n, const int32_t *slots, const double *lbi, const doubl
   DeviceView &v = m.v;
   v.warm_omega_floor = o.warm_omega_floor;
   v.warm_omega_cap = o.warm_omega_cap;
+  v.polish_after = o.polish_after < 0 ? -1 : (int64_t)o.polish_after;
   v.max_iters = o.max_iters;
   // tol / cutoff of every LP in flight: device memory, read by the (graph-replayed) blocks
   m.prm_host[0] = o.tol;

@@ -95,6 +95,12 @@ struct Ctrl {
                                          // primal weight counts as adapted (warm cap) from kOmegaTrained on
   int32_t status, active, restart_pending;
   int32_t exact;                         // 1: the node box fixes the objective (see scalar_pass)
+  // primal feasibility polishing: once the gap to the best Lagrangian bound is closed
+  // and only the primal residual is left, the LP iterates on its feasibility problem (objective 0,
+  // duals restarted from 0) from the current point; polish_bound keeps that best bound
+  int32_t polish, polish_pending;       // pending: 1 = enter (duals saved, from 0), 2 = leave (duals restored)
+  double polish_bound;
+  int64_t polish_k0, polish_next;        // iteration polishing started; earliest iteration to start (-1: never)
 };
 
 // row-family offsets inside y / kz / rho / lo / hi
@@ -129,6 +135,7 @@ struct DeviceView {
   uint8_t *mask;
   double *zi, *zia, *lb, *ub;
   double *zr;                            // [n_int] the certificate's repaired small variables (last check)
+  double *ybak;                          // [n_dual] the duals kept while an LP polishes (Ctrl::polish)
   double *y, *ya, *kz, *kza;             // duals, anchor, activity K z of the iterate and of the anchor
   float *kty;
   double *tpart, *bpart, *npart;
@@ -141,6 +148,7 @@ struct DeviceView {
   const double *prm;
   double warm_omega_floor;               // warm starts: primal weight kept >= this x the parent's (0: off)
   double warm_omega_cap;                 // warm starts: primal weight kept <= this x the parent's (0: off)
+  int64_t polish_after;                  // submit option: polishing may start after this many iterations (-1: never)
   // restart rule on the fixed-point residual (sufficient / necessary / artificial, PDLP's 0.2 / 0.8 /
   // 0.36; necessary 0.9 here, measured) and the primal-weight smoothing (0.5); NEP_RESTART /
   // NEP_OMEGA_SMOOTH override them

@@ -354,7 +354,16 @@ void x_pass(DeviceView v, const int32_t *__restrict__ slots, int plain, int it, 
   float *__restrict__ th_row = v.theta + (int64_t)slot * v.R;   // per-row simplex thresholds (hints)
   const uint8_t *__restrict__ mask = v.mask + slot * v.smask + (int64_t)f * NP;
   float *__restrict__ kty = v.kty + slot * v.skty;
-  const float ys = kty[(int64_t)F * NP + NP];
+  // polishing: objective off (cs = 0); at its first iteration the duals count as 0 (the originals are
+  // kept in ybak), at the first iteration after it they are read back from ybak
+  const int pol_sw = FIRST ? ctrl->polish_pending : 0;
+  const bool pol_enter = pol_sw == 1, pol_leave = pol_sw == 2;
+  const double *ybak = v.ybak + slot * v.sdual;
+  const bool polishing = ctrl->polish != 0;
+  const float cs = polishing ? 0.f : 1.f;
+  // (oS exists in step 2 only, which never polishes; the guard keeps the index in range regardless)
+  const float ys = pol_enter ? 0.f
+                             : ((pol_leave && v.step2) ? (float)ybak[v.dl.oS] : kty[(int64_t)F * NP + NP]);
 
   // Per-function column constants (packed duals kx = y1 + y2 and cy5 = cpr * y5) and the per-wave
   // column accumulators (C1/C2 column sums, C5 W-weighted sums) live in LDS, not in registers:
@@ -368,8 +377,14 @@ void x_pass(DeviceView v, const int32_t *__restrict__ slots, int plain, int it, 
   double *lSd = reinterpret_cast<double *>(lS), *lWd = reinterpret_cast<double *>(lW);
   double *lKd = reinterpret_cast<double *>(lC + NP), *lCd = lKd + NP;
   for (int j = threadIdx.x; j < NP; j += kWave * TW) {
-    lK[j] = kty[(int64_t)f * NP + j];
-    lC[j] = v.cpr[(int64_t)f * NP + j] * kty[(int64_t)F * NP + j];
+    if (pol_leave) {
+      const bool in = j < N;
+      lK[j] = in ? (float)(ybak[v.dl.o1 + f * N + j] + ybak[v.dl.o2 + f * N + j]) : 0.f;
+      lC[j] = in ? v.cpr[(int64_t)f * NP + j] * (float)ybak[v.dl.o5 + j] : 0.f;
+    } else {
+      lK[j] = pol_enter ? 0.f : kty[(int64_t)f * NP + j];
+      lC[j] = pol_enter ? 0.f : v.cpr[(int64_t)f * NP + j] * kty[(int64_t)F * NP + j];
+    }
     if (CHECK) {
       const double *yv = v.y + slot * v.sdual;
       const bool in = j < N;
@@ -433,6 +448,7 @@ void x_pass(DeviceView v, const int32_t *__restrict__ slots, int plain, int it, 
       }
     }
     const float m = ri.m, w = ri.w, wobj = ri.wobj, wsc = ri.wsc;
+    const float wg = polishing ? 0.f : wobj;   // objective off while polishing (a select on the uniform row value)
     float kx[E], cy5[E];
 #pragma unroll
     for (int q = 0; q < CPL; ++q) {
@@ -451,7 +467,7 @@ void x_pass(DeviceView v, const int32_t *__restrict__ slots, int plain, int it, 
     const float gs = wsc * ys;
 #pragma unroll
     for (int e = 0; e < E; ++e) {
-      const float g = wobj * dc[e] - (m * kx[e] + w * cy5[e] + gs * dc[e]);
+      const float g = wg * dc[e] - (m * kx[e] + w * cy5[e] + gs * dc[e]);
       vv[e] = xc[e] - tau * g;
       if ((mbits >> e) & 1u) s += vv[e];
     }
@@ -647,6 +663,7 @@ void x_pass(DeviceView v, const int32_t *__restrict__ slots, int plain, int it, 
   const double memf = v.mem_f[f];
   const double yD3a = v.step2 ? y[dl.oD3a] : 0.0, yD3b = v.step2 ? y[dl.oD3b] : 0.0;
   const double yD4 = v.step2 ? y[dl.oD4] : 0.0;
+  const double csd = cs;   // polishing: small-variable costs off as well
   SmallAcc a;
   double sumc = 0.0, sumc_rep = 0.0;
   for (int j = threadIdx.x; j < N; j += kWave * TW) {
@@ -665,10 +682,18 @@ void x_pass(DeviceView v, const int32_t *__restrict__ slots, int plain, int it, 
     const double S = CHECK ? Sd : (double)Sf;
     const double U = CHECK ? Ud * (double)v.cpr[(int64_t)f * NP + j] : (double)(Uf * v.cpr[(int64_t)f * NP + j]);
     const int idx = f * N + j;
-    const double y1 = y[dl.o1 + idx], y2 = y[dl.o2 + idx];
-    const double y3 = y[dl.o3 + j];
-    const double y6 = v.has_n ? y[dl.o6 + j] : 0.0;
-    const double y7 = v.has_n ? y[dl.o7 + j] : 0.0;
+    // (polishing: at its first iteration every dual counts as 0 — this f's rows C1/C2 are kept in
+    // ybak, node_pass keeps the node rows — and after it they are read back)
+    const double *ysrc = pol_leave ? ybak : y;
+    double y1 = ysrc[dl.o1 + idx], y2 = ysrc[dl.o2 + idx];
+    double y3 = ysrc[dl.o3 + j];
+    double y6 = v.has_n ? ysrc[dl.o6 + j] : 0.0;
+    double y7 = v.has_n ? ysrc[dl.o7 + j] : 0.0;
+    if (pol_enter) {
+      v.ybak[slot * v.sdual + dl.o1 + idx] = y1;
+      v.ybak[slot * v.sdual + dl.o2 + idx] = y2;
+      y1 = y2 = y3 = y6 = y7 = 0.0;
+    }
     double kty_c = -v.M * y1 - y2 + memf * y3 + y6 + y7;
     double yd1 = 0.0, yd2 = 0.0;
     if (v.step2) {
@@ -676,7 +701,7 @@ void x_pass(DeviceView v, const int32_t *__restrict__ slots, int plain, int it, 
       yd2 = y[dl.oD2 + idx];
       kty_c += -yd1 + yd2 - yD3a + yD3b + v.sigma4 * yD4;
     }
-    const double cn = primal_step<CHECK>(v, zi, zia, lb, ub, il.oc + idx, v.cost_int[il.oc + idx] - kty_c, taud,
+    const double cn = primal_step<CHECK>(v, zi, zia, lb, ub, il.oc + idx, csd * v.cost_int[il.oc + idx] - kty_c, taud,
                                          copy_anchor, halp, lamd, a, v.step2);
     const double y1n = dual_step<CHECK, INIT>(v, y, ya, kz, kza, dl.o1 + idx, S - v.M * cn, y1, sigma, copy_anchor,
                                               halp, lamd, a);
@@ -833,6 +858,25 @@ __global__ __launch_bounds__(kNodeThreads) void node_pass(DeviceView v, const in
       nrm3 = v.rownorm[dl.o3 + j];
       nrm5 = v.rownorm[dl.o5 + j];
     }
+    const int pol_sw = first ? ctrl->polish_pending : 0;
+    double *yb = v.ybak + slot * v.sdual;
+    if (pol_sw == 1) {          // polishing starts: the node rows' duals kept, the feasibility problem's from 0
+      yb[dl.o3 + j] = p3.y;
+      yb[dl.o5 + j] = p5.y;
+      if (v.has_n) {
+        yb[dl.o6 + j] = p6.y;
+        yb[dl.o7 + j] = p7.y;
+      }
+      p3.y = p5.y = p6.y = p7.y = 0.0;
+      yS = 0.0;
+    } else if (pol_sw == 2) {   // polishing ends uncertified: the kept duals come back
+      p3.y = yb[dl.o3 + j];
+      p5.y = yb[dl.o5 + j];
+      if (v.has_n) {
+        p6.y = yb[dl.o6 + j];
+        p7.y = yb[dl.o7 + j];
+      }
+    }
   }
   {
     const int jj = threadIdx.x % kNodeJ, g = threadIdx.x / kNodeJ;
@@ -896,7 +940,8 @@ __global__ __launch_bounds__(kNodeThreads) void node_pass(DeviceView v, const in
     kty[(int64_t)F * NP + j] = (float)y5n;
     if (v.has_n) {
       const double kty_n = -v.M * p6.y - p7.y + v.score_n_coef * yS;
-      const double nn = primal_step_p<CHECK>(zi, zia, il.on + j, pn.cost - kty_n, pn, tau, copy_anchor, halp, lam, a);
+      const double ncost = ctrl->polish ? 0.0 : pn.cost;   // polishing: objective off (the certificate keeps it)
+      const double nn = primal_step_p<CHECK>(zi, zia, il.on + j, ncost - kty_n, pn, tau, copy_anchor, halp, lam, a);
       dual_step_p<CHECK, INIT>(y, ya, kz, kza, dl.o6 + j, sumc - v.M * nn, p6, sigma, copy_anchor, halp, lam, a);
       dual_step_p<CHECK, INIT>(y, ya, kz, kza, dl.o7 + j, sumc - nn, p7, sigma, copy_anchor, halp, lam, a);
       score_n = v.score_n_coef * nn;
@@ -965,6 +1010,12 @@ __global__ __launch_bounds__(256) void dblock_pass(DeviceView v, const int32_t *
   if (q < 2 + kNLam)
     v.bpart[slot * v.sbpart + (int64_t)f * NBS + BS_TLO + q] = red[0][q] + red[1][q] + red[2][q] + red[3][q];
 }
+
+// Primal feasibility polishing (scalar_pass): after nep_lp_opts.polish_after iterations, an LP whose best
+// Lagrangian bound is within half the gap tolerance of its repaired point's objective and whose
+// primal residual is in (tol, kPolishRes] switches to its feasibility problem.
+constexpr double kPolishRes = 1e-3;
+constexpr int64_t kPolishBudget = 512;   // iterations; then the LP goes back to its own objective and duals
 
 // ---------------------------------------------------------------------------------------------
 // scalar_pass: one workgroup per slot.  Step-2 scalar rows (D3a, D3b, D4, score) and the
@@ -1070,7 +1121,11 @@ __global__ __launch_bounds__(256) void scalar_pass(DeviceView v, const int32_t *
       __syncthreads();
     }
   }
-  if (tid != 0) return;
+  // the slot's certificate, status and restart decisions: thread 0 (a lambda, so that every thread
+  // meets the barrier below); a polished LP that certifies gets its kept duals back (restore_duals)
+  __shared__ int restore_duals;
+  if (tid == 0) restore_duals = 0;
+  if (tid == 0) [&]() {
 
   const DualLayout &dl = v.dl;
   const IntLayout &il = v.il;
@@ -1127,6 +1182,7 @@ __global__ __launch_bounds__(256) void scalar_pass(DeviceView v, const int32_t *
   ctrl->k_lineage += done;
   ctrl->k_since_restart += done;
   ctrl->restart_pending = 0;
+  ctrl->polish_pending = 0;
   if (tot[TS_EMPTY] > 0) { ctrl->status = 2; ctrl->active = 0; return; }
   // certificate point, completed: allocated / deallocated repaired from the repaired sum c
   // (D3: a <= sumOld - sum c, d <= sum c - sumOld; D4: a + d >= sigma4 (sumOld - sum c); costs
@@ -1170,28 +1226,67 @@ __global__ __launch_bounds__(256) void scalar_pass(DeviceView v, const int32_t *
     ctrl->active = 0;
     return;
   }
-  ctrl->lagr = lagr;
-  if (lagr > ctrl->best_lagr) ctrl->best_lagr = lagr;
-  ctrl->pres = res;
-  ctrl->gap = gap;
-  if (isfinite(lagr) && res <= tol && gap <= gap_tol * fmax(1.0, fabs(lagr))) {
-    ctrl->status = 0; ctrl->active = 0; return;
+  if (ctrl->polish) {
+    // Polishing: the iterate solves the feasibility problem, whose Lagrangian bounds nothing here.
+    // The bound is the best one taken before polishing; the repaired point's objective (reference
+    // costs) is measured against it.
+    const double b = ctrl->polish_bound;
+    ctrl->lagr = b;
+    ctrl->pres = res;
+    ctrl->gap = pobj - b;
+    if (res <= tol && pobj - b <= gap_tol * fmax(1.0, fabs(b))) {
+      ctrl->status = 0;
+      ctrl->active = 0;
+      restore_duals = 1;
+      return;
+    }
+  } else {
+    ctrl->lagr = lagr;
+    if (lagr > ctrl->best_lagr) ctrl->best_lagr = lagr;
+    ctrl->pres = res;
+    ctrl->gap = gap;
+    if (isfinite(lagr) && res <= tol && gap <= gap_tol * fmax(1.0, fabs(lagr))) {
+      ctrl->status = 0; ctrl->active = 0; return;
+    }
   }
   if (ctrl->best_lagr > cutoff) { ctrl->status = 3; ctrl->active = 0; return; }
   if (ctrl->k >= ctrl->max_iters) { ctrl->status = 1; ctrl->active = 0; return; }
   if (!isfinite(pobj) || !isfinite(a.mvz) || !isfinite(a.mvy)) { ctrl->status = 4; ctrl->active = 0; return; }
 
+  // primal feasibility polishing (step 1): the best bound already meets the gap test against the
+  // repaired point's objective and only its primal residual is left — the tail of the node LPs,
+  // whose CPU rows (C5) close last (tools/tail_probe.py).  From here the LP iterates on its
+  // feasibility problem (objective off, duals restarted from 0) from the current point; it is
+  // certified once the repaired point is feasible within tol and its objective still within the
+  // gap tolerance of the bound kept.
+  bool polish_now = false;
+  if (ctrl->polish) {
+    if (ctrl->k - ctrl->polish_k0 >= kPolishBudget) {   // not certified within the budget: back to the LP
+      ctrl->polish = 0;
+      ctrl->polish_pending = 2;
+      ctrl->polish_next = ctrl->k + 4 * kPolishBudget;
+      polish_now = true;                                 // (restart: the anchors take the restored duals)
+    }
+  } else if (!v.step2 && ctrl->polish_next >= 0 && ctrl->k >= ctrl->polish_next && res > tol && res <= kPolishRes &&
+             isfinite(ctrl->best_lagr) &&
+             fabs(pobj - ctrl->best_lagr) <= 0.5 * gap_tol * fmax(1.0, fabs(ctrl->best_lagr))) {
+    ctrl->polish = 1;
+    ctrl->polish_pending = 1;   // consumed by the passes of the block's next iteration (it == 1)
+    ctrl->polish_bound = ctrl->best_lagr;
+    ctrl->polish_k0 = ctrl->k;
+    polish_now = true;
+  }
   // restart test on the fixed-point residual of the last iteration (ω-weighted norm)
   const double w = ctrl->omega;
   const double fpr = sqrt(w * a.mvz + a.mvy / w);
   if (ctrl->last_restart_fpr < 0) ctrl->last_restart_fpr = fpr;
-  const bool restart = (fpr <= v.rs_suff * ctrl->last_restart_fpr) ||
+  const bool restart = polish_now || (fpr <= v.rs_suff * ctrl->last_restart_fpr) ||
                        (fpr <= v.rs_nec * ctrl->last_restart_fpr && fpr > ctrl->prev_fpr) ||
                        (ctrl->k_since_restart >= v.rs_art * ctrl->k);
   ctrl->prev_fpr = fpr;
   if (restart) {
     const double dz = sqrt(a.dsz), dy = sqrt(a.dsy);
-    if (dz > 1e-10 && dy > 1e-10) {
+    if (!polish_now && dz > 1e-10 && dy > 1e-10) {   // (entering polishing keeps the weight)
       double nw = exp(v.omega_smooth * log(dy / dz) + (1.0 - v.omega_smooth) * log(w));
       nw = fmin(fmax(nw, ctrl->omega_lo), ctrl->omega_hi);
       ctrl->omega = nw;
@@ -1205,6 +1300,18 @@ __global__ __launch_bounds__(256) void scalar_pass(DeviceView v, const int32_t *
     ctrl->prev_fpr = INFINITY;
   } else {
     ctrl->ks_base += block_len;
+  }
+  }();
+  // (also when a polishing LP stops uncertified: its bound is the kept one, its state the LP's duals)
+  if (tid == 0 && ctrl->polish && !ctrl->active) restore_duals = 1;
+  __syncthreads();
+  if (restore_duals) {
+    // The certified point is the polished primal; its dual state goes back to the LP's own duals (kept
+    // when polishing started), so children warm-started from this slot start from them, not from
+    // the feasibility problem's.
+    double *y = v.y + slot * v.sdual;
+    const double *yb = v.ybak + slot * v.sdual;
+    for (int i = tid; i < v.dl.n_dual; i += 256) y[i] = yb[i];
   }
 }
 
@@ -1255,6 +1362,10 @@ __global__ void init_slot(DeviceView v, const int32_t *__restrict__ slots, const
     ctrl->exact = exact[blockIdx.y];
     ctrl->max_iters = v.max_iters;
     ctrl->restart_pending = 1;
+    ctrl->polish = ctrl->polish_pending = 0;   // a warm start does not inherit its parent's polishing
+    ctrl->polish_bound = -INFINITY;
+    ctrl->polish_k0 = 0;
+    ctrl->polish_next = v.polish_after;   // this LP's submit option (-1: it never polishes)
     ctrl->best_lagr = -INFINITY;
     ctrl->pobj = ctrl->lagr = ctrl->pres = ctrl->gap = NAN;
   }
