@@ -95,3 +95,12 @@ def test_node_presolve_incremental_equals_full(name, k):
     assert not ok_f[2::4].any()
     for b in np.nonzero(ok_f)[0]:
         np.testing.assert_array_equal(box_f[b], box_n[b])
+
+
+def test_request_unknown_solver_type_raises():
+    """core.request resolves solver.type through the SOLVERS whitelist (the reference: eval, main.py:44);
+    an unknown type raises before any engine call (the reference's server answers HTTP 500)."""
+    import pytest
+    from core.request import solve_request
+    with pytest.raises(KeyError):
+        solve_request({"solver": {"type": "NotASolver"}})
