@@ -661,8 +661,10 @@ void x_pass(DeviceView v, const int32_t *__restrict__ slots, int plain, int it, 
   double *kza = v.kza + slot * v.sdual;
   double *np_ = v.npart + slot * v.snpart + (int64_t)f * 2 * NP;
   const double memf = v.mem_f[f];
-  const double yD3a = v.step2 ? y[dl.oD3a] : 0.0, yD3b = v.step2 ? y[dl.oD3b] : 0.0;
-  const double yD4 = v.step2 ? y[dl.oD4] : 0.0;
+  // (step-2 scalar rows, owned by scalar_pass: 0 at the first polishing iteration, kept values after it)
+  const double *yst = pol_leave ? ybak : y;
+  const double yD3a = (v.step2 && !pol_enter) ? yst[dl.oD3a] : 0.0, yD3b = (v.step2 && !pol_enter) ? yst[dl.oD3b] : 0.0;
+  const double yD4 = (v.step2 && !pol_enter) ? yst[dl.oD4] : 0.0;
   const double csd = cs;   // polishing: small-variable costs off as well
   SmallAcc a;
   double sumc = 0.0, sumc_rep = 0.0;
@@ -697,8 +699,13 @@ void x_pass(DeviceView v, const int32_t *__restrict__ slots, int plain, int it, 
     double kty_c = -v.M * y1 - y2 + memf * y3 + y6 + y7;
     double yd1 = 0.0, yd2 = 0.0;
     if (v.step2) {
-      yd1 = y[dl.oD1 + idx];
-      yd2 = y[dl.oD2 + idx];
+      yd1 = ysrc[dl.oD1 + idx];
+      yd2 = ysrc[dl.oD2 + idx];
+      if (pol_enter) {   // D1/D2 rows of this f: kept, the feasibility problem's from 0
+        v.ybak[slot * v.sdual + dl.oD1 + idx] = yd1;
+        v.ybak[slot * v.sdual + dl.oD2 + idx] = yd2;
+        yd1 = yd2 = 0.0;
+      }
       kty_c += -yd1 + yd2 - yD3a + yD3b + v.sigma4 * yD4;
     }
     const double cn = primal_step<CHECK>(v, zi, zia, lb, ub, il.oc + idx, csd * v.cost_int[il.oc + idx] - kty_c, taud,
@@ -708,9 +715,9 @@ void x_pass(DeviceView v, const int32_t *__restrict__ slots, int plain, int it, 
     const double y2n = dual_step<CHECK, INIT>(v, y, ya, kz, kza, dl.o2 + idx, S - cn, y2, sigma, copy_anchor, halp,
                                               lamd, a);
     if (v.step2) {
-      const double mfn = primal_step<CHECK>(v, zi, zia, lb, ub, il.omf + idx, v.cost_int[il.omf + idx] - yd1, taud,
+      const double mfn = primal_step<CHECK>(v, zi, zia, lb, ub, il.omf + idx, csd * v.cost_int[il.omf + idx] - yd1, taud,
                                             copy_anchor, halp, lamd, a, true);
-      const double mtn = primal_step<CHECK>(v, zi, zia, lb, ub, il.omt + idx, v.cost_int[il.omt + idx] - yd2, taud,
+      const double mtn = primal_step<CHECK>(v, zi, zia, lb, ub, il.omt + idx, csd * v.cost_int[il.omt + idx] - yd2, taud,
                                             copy_anchor, halp, lamd, a, true);
       dual_step<CHECK, INIT>(v, y, ya, kz, kza, dl.oD1 + idx, mfn - cn, yd1, sigma, copy_anchor, halp, lamd, a, true);
       dual_step<CHECK, INIT>(v, y, ya, kz, kza, dl.oD2 + idx, mtn + cn, yd2, sigma, copy_anchor, halp, lamd, a, true);
@@ -870,6 +877,7 @@ __global__ __launch_bounds__(kNodeThreads) void node_pass(DeviceView v, const in
       p3.y = p5.y = p6.y = p7.y = 0.0;
       yS = 0.0;
     } else if (pol_sw == 2) {   // polishing ends uncertified: the kept duals come back
+      if (v.step2) yS = yb[dl.oS];
       p3.y = yb[dl.o3 + j];
       p5.y = yb[dl.o5 + j];
       if (v.has_n) {
@@ -1150,11 +1158,21 @@ __global__ __launch_bounds__(256) void scalar_pass(DeviceView v, const int32_t *
   if (v.step2) {
     const double sumc = tot[NTS + BS_SUMC_NEW];
     const double score = tot[TS_SCORE] + tot[NTS + BS_SCORE_N];
-    const double yD3a = y[dl.oD3a], yD3b = y[dl.oD3b], yD4 = y[dl.oD4], yS = y[dl.oS];
+    double yD3a = y[dl.oD3a], yD3b = y[dl.oD3b], yD4 = y[dl.oD4], yS = y[dl.oS];
+    // polishing: these rows' duals are kept / restarted from 0 / read back like the others
+    const int pol_sw = first ? ctrl->polish_pending : 0;
+    double *yb = v.ybak + slot * v.sdual;
+    if (pol_sw == 1) {
+      yb[dl.oD3a] = yD3a; yb[dl.oD3b] = yD3b; yb[dl.oD4] = yD4; yb[dl.oS] = yS;
+      yD3a = yD3b = yD4 = yS = 0.0;
+    } else if (pol_sw == 2) {
+      yD3a = yb[dl.oD3a]; yD3b = yb[dl.oD3b]; yD4 = yb[dl.oD4]; yS = yb[dl.oS];
+    }
+    const double csd = ctrl->polish ? 0.0 : 1.0;
     // allocated (a): D3a coef -1, D4 coef +1 ; deallocated (d): D3b coef -1, D4 coef +1
-    const double an = primal_step<CHECK>(v, zi, zia, lb, ub, il.oa, v.cost_int[il.oa] - (-yD3a + yD4), tau,
+    const double an = primal_step<CHECK>(v, zi, zia, lb, ub, il.oa, csd * v.cost_int[il.oa] - (-yD3a + yD4), tau,
                                          copy_anchor, halp, lam, a, true);
-    const double dn = primal_step<CHECK>(v, zi, zia, lb, ub, il.od, v.cost_int[il.od] - (-yD3b + yD4), tau,
+    const double dn = primal_step<CHECK>(v, zi, zia, lb, ub, il.od, csd * v.cost_int[il.od] - (-yD3b + yD4), tau,
                                          copy_anchor, halp, lam, a, true);
     dual_step<CHECK, INIT>(v, y, ya, kz, kza, dl.oD3a, -sumc - an, yD3a, sigma, copy_anchor, halp, lam, a, true);
     dual_step<CHECK, INIT>(v, y, ya, kz, kza, dl.oD3b, sumc - dn, yD3b, sigma, copy_anchor, halp, lam, a, true);
@@ -1267,7 +1285,7 @@ __global__ __launch_bounds__(256) void scalar_pass(DeviceView v, const int32_t *
       ctrl->polish_next = ctrl->k + 4 * kPolishBudget;
       polish_now = true;                                 // (restart: the anchors take the restored duals)
     }
-  } else if (!v.step2 && ctrl->polish_next >= 0 && ctrl->k >= ctrl->polish_next && res > tol && res <= kPolishRes &&
+  } else if (ctrl->polish_next >= 0 && ctrl->k >= ctrl->polish_next && res > tol && res <= kPolishRes &&
              isfinite(ctrl->best_lagr) &&
              fabs(pobj - ctrl->best_lagr) <= 0.5 * gap_tol * fmax(1.0, fabs(ctrl->best_lagr))) {
     ctrl->polish = 1;
