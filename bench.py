@@ -66,7 +66,8 @@ def parse(argv=None):
     ap.add_argument("--warm-omega-floor", type=float, default=0.0,
                     help="warm-start primal-weight floor x the parent's (0: engine default)")
     ap.add_argument("--root-max-iters", type=int, default=400000)
-    ap.add_argument("--check-every", type=int, default=16, help="PDHG iterations per certificate check (node LPs)")
+    ap.add_argument("--check-every", type=int, default=12,
+                    help="PDHG iterations per certificate check (node LPs; 8/12/16/24 measured, DESIGN.md §6)")
     ap.add_argument("--root-check-every", type=int, default=64)
     ap.add_argument("--root-gap-tol", type=float, default=0.0,
                     help="after the root certifies at --tol, continue it (warm, same slot) until its objective gap "

@@ -91,7 +91,7 @@ class BranchAndBound:
 
     def __init__(self, lp, workload, fn_mem, node_mem, batch=16, tol=1e-7, gap=1e-6, max_iters=5000,
                  node_limit=20000, time_limit=None, upper_bound=math.inf, flow_tol=1e-4, log=None, comm=None,
-                 warm=True, root_max_iters=200000, check_every=16, polish_tol=1e-8, polish_iters=20000,
+                 warm=True, root_max_iters=200000, check_every=12, polish_tol=1e-8, polish_iters=20000,
                  seed_leaves=None, integer_bound=None, improve=None):
         self.lp = lp
         self.N, self.F = lp.N, lp.F
