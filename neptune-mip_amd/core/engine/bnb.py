@@ -387,8 +387,9 @@ class BranchAndBound:
             r = lp.advance(1)
         if len(r["slots"]) and int(r["status"][0]) == LP_OPTIMAL:
             res.objective = float(r["primal_obj"][0])
-            res.z, _ = lp.solution(slot, dense_x=False)
+            res.z, res.x = lp.solution(slot, dense_x=True)
             res.polished = True
+        # (uncertified: the slot's state moved on; res.x / res.z stay the certified leaf's, fetched before)
 
     # ---------------------------------------------------------------------------------------
     def solve(self):
@@ -471,8 +472,11 @@ class BranchAndBound:
                 node = self.inflight.pop(slot, None)
                 if node is not None and int(r["status"][i]) not in (LP_INFEASIBLE, LP_CUTOFF):
                     open_bounds.append(max(node.bound, float(r["obj"][i])))
-        if res.objective is not None and res.incumbent_slot is not None and self.polish_tol:
-            self._polish(res)
+        if res.objective is not None and res.incumbent_slot is not None:
+            # the certified leaf's routing, fetched once before the polish re-solve may move the slot
+            _, res.x = lp.solution(res.incumbent_slot, dense_x=True)
+            if self.polish_tol:
+                self._polish(res)
         open_bounds += [h[0] for h in self.heap] + [n.bound for n in self.pending] + [n.bound for n in self.retry]
         open_bounds += self.unresolved_bounds
         res.bound = min(open_bounds + [inc])
@@ -485,8 +489,7 @@ class BranchAndBound:
             if owner < comm.world:
                 own = comm.rank == owner
                 z = res.z if own else np.zeros(self.lp.n_int)
-                x = lp.solution(res.incumbent_slot, dense_x=True)[1] if own else \
-                    np.zeros((self.N, self.F, self.N), np.float32)
+                x = res.x if own else np.zeros((self.N, self.F, self.N), np.float32)
                 res.z = comm.bcast(np.asarray(z, np.float64), owner)
                 res.x = comm.bcast(np.asarray(x, np.float32), owner)
                 res.objective = inc
@@ -494,8 +497,6 @@ class BranchAndBound:
             res.nodes = comm.sum(res.nodes - self.presplit[0]) + self.presplit[0]
             res.lps = comm.sum(res.lps - self.presplit[1]) + self.presplit[1]
             res.certified = comm.sum(res.certified - self.presplit[2]) + self.presplit[2]
-        elif res.incumbent_slot is not None:
-            _, res.x = lp.solution(res.incumbent_slot, dense_x=True)
         unresolved_below = any(b < inc - self._gap_abs(inc) for b in self.unresolved_bounds)
         if comm.world > 1:
             unresolved_below = comm.sum(int(unresolved_below)) > 0
