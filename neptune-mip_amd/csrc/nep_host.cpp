@@ -146,6 +146,7 @@ struct Model {
   // pipelined blocks (advance): the block launched last, not yet waited for — the slots it iterates,
   // whether it carries the sampled x-pass events — and the pinned copy of the slots' Ctrl it ends with
   bool inflight = false, inflight_sampled = false;
+  int pipe_max_done = INT_MAX;
   std::vector<int32_t> launched;
   Ctrl *h_ctrl = nullptr;
   ~Model() {
@@ -576,6 +577,7 @@ int setup_device(Model &m, int max_batch, void *stream) {
   v.rs_suff = 0.2; v.rs_nec = 0.9; v.rs_art = 0.36; v.omega_smooth = 0.5;   // necessary 0.9: DESIGN.md §4
   if (const char *e = std::getenv("NEP_RESTART")) std::sscanf(e, "%lf,%lf,%lf", &v.rs_suff, &v.rs_nec, &v.rs_art);
   if (const char *e = std::getenv("NEP_OMEGA_SMOOTH")) v.omega_smooth = std::atof(e);
+  if (const char *e = std::getenv("NEP_PIPELINE_MAX_DONE")) m.pipe_max_done = std::atoi(e);
   int rc;
   if ((rc = upload(m, &v.rows, m.rows))) return rc;
   if ((rc = upload(m, &v.frow, m.frow))) return rc;
@@ -1097,11 +1099,15 @@ int advance(Model &m, int min_done, int32_t *n_done, int32_t *done, double *obj,
         HIPCHK(hipMemcpyAsync(m.d_slots, m.act.data(), m.act.size() * sizeof(int32_t), hipMemcpyHostToDevice,
                               m.stream));
     }
-    if (!m.act.empty()) {
-      int rc = launch_block(m);   // the next block runs while the caller handles the finished slots
+    // the next block runs while the caller handles the finished slots — unless more than
+    // pipe_max_done slots just finished and the call returns: then the caller's refill joins the
+    // very next block instead of the one after (NEP_PIPELINE_MAX_DONE; default: always pipeline)
+    const bool returning = min_done <= 0 || *n_done >= min_done;
+    if (!m.act.empty() && (!returning || *n_done <= m.pipe_max_done)) {
+      int rc = launch_block(m);
       if (rc) return rc;
     }
-    if (min_done <= 0 || *n_done >= min_done) break;
+    if (returning) break;
   }
   return NEP_OK;
 }
