@@ -578,6 +578,13 @@ int setup_device(Model &m, int max_batch, void *stream) {
   if (const char *e = std::getenv("NEP_RESTART")) std::sscanf(e, "%lf,%lf,%lf", &v.rs_suff, &v.rs_nec, &v.rs_art);
   if (const char *e = std::getenv("NEP_OMEGA_SMOOTH")) v.omega_smooth = std::atof(e);
   if (const char *e = std::getenv("NEP_PIPELINE_MAX_DONE")) m.pipe_max_done = std::atoi(e);
+  v.polish_res = kPolishRes;
+  v.polish_budget = kPolishBudget;
+  if (const char *e = std::getenv("NEP_POLISH")) {   // "res,budget"
+    long long b = v.polish_budget;
+    std::sscanf(e, "%lf,%lld", &v.polish_res, &b);
+    v.polish_budget = b;
+  }
   int rc;
   if ((rc = upload(m, &v.rows, m.rows))) return rc;
   if ((rc = upload(m, &v.frow, m.frow))) return rc;

@@ -51,6 +51,8 @@ struct AnchorEnt {
 
 constexpr int kWave = 64;
 constexpr int64_t kOmegaTrained = 1024;  // warm_omega_cap applies when the parent lineage iterated this much
+constexpr double kPolishRes = 1e-3;        // polishing entry: primal residual at most this
+constexpr int64_t kPolishBudget = 512;     // polishing iterations before the LP goes back to its own objective
 constexpr int kNodeWaves = 16;           // waves per node-pass workgroup (each sums F/16 functions)
 constexpr int kNodeThreads = kWave * kNodeWaves;
 constexpr int kNodeJ = 16;               // nodes per node-pass workgroup
@@ -149,6 +151,8 @@ struct DeviceView {
   double warm_omega_floor;               // warm starts: primal weight kept >= this x the parent's (0: off)
   double warm_omega_cap;                 // warm starts: primal weight kept <= this x the parent's (0: off)
   int64_t polish_after;                  // submit option: polishing may start after this many iterations (-1: never)
+  double polish_res;                     // polishing starts only with the primal residual <= this (NEP_POLISH, kPolishRes)
+  int64_t polish_budget;                 // polishing iterations before going back to the LP (NEP_POLISH, kPolishBudget)
   // restart rule on the fixed-point residual (sufficient / necessary / artificial, PDLP's 0.2 / 0.8 /
   // 0.36; necessary 0.9 here, measured) and the primal-weight smoothing (0.5); NEP_RESTART /
   // NEP_OMEGA_SMOOTH override them

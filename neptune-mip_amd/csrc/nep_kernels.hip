@@ -1022,8 +1022,7 @@ __global__ __launch_bounds__(256) void dblock_pass(DeviceView v, const int32_t *
 // Primal feasibility polishing (scalar_pass): after nep_lp_opts.polish_after iterations, an LP whose best
 // Lagrangian bound is within half the gap tolerance of its repaired point's objective and whose
 // primal residual is in (tol, kPolishRes] switches to its feasibility problem.
-constexpr double kPolishRes = 1e-3;
-constexpr int64_t kPolishBudget = 512;   // iterations; then the LP goes back to its own objective and duals
+// (kPolishRes / kPolishBudget: nep_internal.h; NEP_POLISH="res,budget" overrides them)
 
 // ---------------------------------------------------------------------------------------------
 // scalar_pass: one workgroup per slot.  Step-2 scalar rows (D3a, D3b, D4, score) and the
@@ -1279,13 +1278,13 @@ __global__ __launch_bounds__(256) void scalar_pass(DeviceView v, const int32_t *
   // gap tolerance of the bound kept.
   bool polish_now = false;
   if (ctrl->polish) {
-    if (ctrl->k - ctrl->polish_k0 >= kPolishBudget) {   // not certified within the budget: back to the LP
+    if (ctrl->k - ctrl->polish_k0 >= v.polish_budget) {   // not certified within the budget: back to the LP
       ctrl->polish = 0;
       ctrl->polish_pending = 2;
-      ctrl->polish_next = ctrl->k + 4 * kPolishBudget;
+      ctrl->polish_next = ctrl->k + 4 * v.polish_budget;
       polish_now = true;                                 // (restart: the anchors take the restored duals)
     }
-  } else if (ctrl->polish_next >= 0 && ctrl->k >= ctrl->polish_next && res > tol && res <= kPolishRes &&
+  } else if (ctrl->polish_next >= 0 && ctrl->k >= ctrl->polish_next && res > tol && res <= v.polish_res &&
              isfinite(ctrl->best_lagr) &&
              fabs(pobj - ctrl->best_lagr) <= 0.5 * gap_tol * fmax(1.0, fabs(ctrl->best_lagr))) {
     ctrl->polish = 1;
