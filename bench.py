@@ -73,13 +73,15 @@ def parse(argv=None):
                     help="after the root certifies at --tol, continue it (warm, same slot) until its objective gap "
                          "is below this: the children warm-start from a well-converged root (0 = off)")
     ap.add_argument("--cold", action="store_true", help="cold-start every node LP")
-    ap.add_argument("--cpu-budget", type=float, default=25.0, help="seconds for the CPU baseline (0 = skip)")
+    ap.add_argument("--cpu-budget", type=float, default=45.0,
+                    help="seconds for the CPU baseline (0 = skip); the bench-size attempt gets what the fit leaves, "
+                         ">= 30 s")
     ap.add_argument("--cpu-workers", type=int, default=16,
                     help="CPU baseline worker processes (capped at the host's cores; 16 = the GPU box's share)")
     ap.add_argument("--bnb-seconds", type=float, default=20.0,
                     help="time limit of the product branch-and-bound section (0 = skip)")
-    ap.add_argument("--bnb-nodes", type=int, default=256)
-    ap.add_argument("--bnb-functions", type=int, default=128)
+    ap.add_argument("--bnb-sizes", default="256x128,512x256",
+                    help="instances of the product B&B section (BASELINE configs 3 and 4), NxF comma-separated")
     ap.add_argument("--traffic", default=os.path.join(REPO, "profiles", "traffic.json"))
     return ap.parse_args(argv)
 
@@ -107,25 +109,46 @@ def node_bounds(n_int, F, N, B, k, seed):
     return lb, ub
 
 
-def _dnf_probe(N, F, seed, seconds):
-    """Try to build the literal reference model at the bench size in a child process, killed after
-    `seconds`: the CPU path's 'did not finish' evidence at 512x256."""
+def _dnf_probe(N, F, seed, fix, seconds):
+    """One node LP of the bench workload at the bench size on the CPU path itself: the literal reference
+    model (oracle/formulation.py, 67 M routing columns / 269 M nonzeros at 512x256) built and handed to
+    HiGHS in a child process with a wall budget of `seconds` (HiGHS time_limit + a kill after it).
+    Reports its LP time, or "DNF > T" with the stage it reached."""
     import subprocess
-    code = ("import sys; sys.path[:0]=%r\n"
+    code = ("import sys, time, numpy as np; sys.path[:0]=%r\n"
             "from core.utils.synthetic import synthetic_payload\n"
             "from oracle.inputs import data_to_solver_input\n"
             "from oracle.formulation import build_model\n"
-            "p=synthetic_payload(%d,%d,seed=%d); d=data_to_solver_input(p,with_db=False)\n"
-            "m=build_model(d,'MinDelayAndUtilization',step=1,alpha=0.5); print('built', m['A'].shape)\n"
-            % ([PKG, REPO], N, F, seed))
+            "from oracle.solve import solve\n"
+            "t0=time.perf_counter(); p=synthetic_payload(%d,%d,seed=%d); d=data_to_solver_input(p,with_db=False)\n"
+            "m=build_model(d,'MinDelayAndUtilization',step=1,alpha=0.5)\n"
+            "print('built', m['A'].shape, m['A'].nnz, time.perf_counter()-t0, flush=True)\n"
+            "nx=%d*%d*%d; rng=np.random.default_rng(%d); idx=rng.choice(%d*%d, size=%d, replace=False)\n"
+            "lb=m['lb'].copy(); ub=m['ub'].copy(); v=rng.integers(0,2,size=%d).astype(float)\n"
+            "lb[nx+idx]=v; ub[nx+idx]=v; t1=time.perf_counter()\n"
+            "st,obj,_=solve(m, relax=True, lb=lb, ub=ub, time_limit=max(1.0, %f-(t1-t0)))\n"
+            "print('solved', st, obj, time.perf_counter()-t1, flush=True)\n"
+            % ([PKG, REPO], N, F, seed, N, N, F, seed, F, N, fix, fix, seconds))
     t0 = time.perf_counter()
+    out = {"seconds_budget": seconds, "stage": "model build"}
     try:
-        r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=seconds)
-        return {"finished": r.returncode == 0, "seconds": time.perf_counter() - t0, "stage": "model build"}
+        r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=seconds + 5)
+        lines = r.stdout.splitlines()
+        for ln in lines:
+            if ln.startswith("built"):
+                out["stage"] = "HiGHS LP"
+                out["build_s"] = float(ln.split()[-1])
+            if ln.startswith("solved"):
+                _, st, obj, sec = ln.split()
+                out.update(lp_status=int(st), lp_seconds=float(sec))
+        out["finished"] = out.get("lp_status") == 0
     except subprocess.TimeoutExpired:
-        return {"finished": False, "seconds": seconds, "stage": "model build",
-                "note": f"DNF > {seconds:.0f} s: the literal {N}x{F} model ({N * N * F:,} routing columns) was "
-                        f"not even built"}
+        out["finished"] = False
+    out["wall_s"] = time.perf_counter() - t0
+    if not out["finished"]:
+        out["note"] = (f"DNF > {seconds:.0f} s: the {N}x{F} node LP ({N * N * F:,} routing columns) reached "
+                       f"'{out['stage']}' and had not finished")
+    return out
 
 
 def cpu_baseline(N, F, seed, fix, budget, workers):
@@ -185,7 +208,7 @@ def cpu_baseline(N, F, seed, fix, budget, workers):
     pool_lps = len(sts) / wall
     log(f"cpu baseline: {w_used} workers solved {len(sts)} {n_l}x{f_l} node LPs in {wall:.2f}s "
         f"({pool_lps:.2f} LP/s)")
-    dnf = _dnf_probe(N, F, seed, max(5.0, budget - (time.perf_counter() - t_start)))
+    dnf = _dnf_probe(N, F, seed, fix, max(30.0, budget - (time.perf_counter() - t_start)))
     value = pool_lps / scale
     sample = ("HiGHS (oracle/solve.py, scipy %s) on the reference formulation (oracle/formulation.py), node LPs "
               "with %d c-fixings, same generator. Single-thread times %s; fit t ~ (N^2 F)^%.2f over the last %d "
@@ -193,26 +216,26 @@ def cpu_baseline(N, F, seed, fix, budget, workers):
               "value = that rate / %.0f (the fitted per-LP time ratio to %dx%d). At %dx%d itself: %s"
               % (__import__("scipy").__version__, fix, ", ".join(f"{a}x{b}: {t:.2f}s" for a, b, t, _ in pts),
                  p_exp, min(3, len(pts)), t_l * scale, N, F, w_used, len(sts), n_l, f_l, wall, pool_lps, scale,
-                 N, F, N, F, dnf.get("note", "finished the model build in %.1f s" % dnf["seconds"])))
+                 N, F, N, F, dnf.get("note", "one node LP solved by HiGHS in %.1f s" % dnf.get("lp_seconds", 0.0))))
     return {"value": value, "unit": "LP-relaxations/s", "cores": w_used, "kind": "port", "sample": sample,
             "extrapolated": True, "pool_lp_per_s_at": {"nodes": n_l, "functions": f_l, "value": pool_lps},
             "dnf_at_bench_size": dnf,
             "measured": [{"nodes": a, "functions": b, "seconds": t, "status": s} for a, b, t, s in pts]}
 
 
-def bnb_section(a, rank, world, dev):
+def bnb_section(a, rank, world, dev, N, F):
     """The product's own branch-and-bound (core/engine/bnb.py, the search SCIP runs inside
-    pywraplp Solve(), solver.py:35-40) on BASELINE config 3's instance (default 256x128, step-1
-    NeptuneMinDelayAndUtilization), time-limited: certified node LPs per second INSIDE the
-    B&B, nodes, incumbent, bound and gap.  With N ranks the search is the sharded one (subtrees per
-    rank, incumbent / termination all-reduces over RCCL: core/engine/comm.TorchComm)."""
+    pywraplp Solve(), solver.py:35-40) on BASELINE config 3's / 4's instance (256x128, 512x256, step-1
+    NeptuneMinDelayAndUtilization), time-limited: certified node LPs per second INSIDE the B&B, the
+    node-LP mix (finished LPs per status, iteration percentiles), nodes, incumbent, bound and gap.
+    With N ranks the search is the sharded one (subtrees per rank, one packed all-gather per loop over
+    RCCL: core/engine/comm.TorchComm)."""
     from core.engine.bnb import BranchAndBound
     from core.engine.comm import LocalComm, TorchComm
     from core.engine.lp import LPModel
     from core.solvers.neptune.neptune_step import NeptuneStep1CPUMinDelayAndUtilization
     from core.utils import data_to_solver_input
     from core.utils.synthetic import synthetic_payload
-    N, F = a.bnb_nodes, a.bnb_functions
     p = synthetic_payload(N, F, seed=a.seed)
     data = data_to_solver_input(p, with_db=False)
     alpha = p["solver"]["args"]["alpha"]
@@ -234,9 +257,13 @@ def bnb_section(a, rank, world, dev):
     m.close()
     inc = res.objective
     gap = None if inc is None else (inc - res.bound) / max(1.0, abs(inc))
+    d = res.as_dict()
+    finished = sum(v for k, v in res.lp_status.items() if k != "presolve_infeasible")
     return {"workload": f"synthetic_{N}x{F}_step1_MDU_product_bnb", "time_limit_s": a.bnb_seconds,
             "status": res.status, "wall_s": wall, "nodes": res.nodes, "leaves": res.leaves, "lps": res.lps,
             "certified_lps": res.certified, "certified_lp_per_s": res.certified / wall, "nodes_per_s": res.nodes / wall,
+            "certified_share": res.certified / max(1, finished), "lp_status_rank0": res.lp_status,
+            "lp_iters_p50_p90_p99_max_rank0": d["lp_iters_p50_p90_p99_max"],
             "lp_iterations": res.lp_iterations, "incumbent": inc, "bound": res.bound, "rel_gap": gap,
             "ranks": world}
 
@@ -384,7 +411,14 @@ def main():
         n_ok, n_it, n_done = int(sm[1]), int(sm[2]), int(sm[4])
     m.close()
     # the product's own B&B (every rank takes part: the sharded search when world > 1)
-    bnb = bnb_section(a, rank, world, dev) if a.bnb_seconds > 0 else None
+    bnb = None
+    if a.bnb_seconds > 0:
+        bnb = []
+        for size in a.bnb_sizes.split(","):
+            bn, bf = (int(t) for t in size.lower().split("x"))
+            bnb.append(bnb_section(a, rank, world, dev, bn, bf))
+            log(f"rank {rank}: bnb {size}: {bnb[-1]['certified_lps']} certified node LPs, status {bnb[-1]['status']}, "
+                f"gap {bnb[-1]['rel_gap']}")
     if rank != 0:
         if dist:
             td.destroy_process_group()

@@ -42,9 +42,11 @@ from collections import deque
 import numpy as np
 
 from .comm import LocalComm
-from .lp import LP_CUTOFF, LP_INFEASIBLE, LP_OPTIMAL
+from .lp import LP_CUTOFF, LP_INFEASIBLE, LP_ITERATION_LIMIT, LP_OPTIMAL
 
 OPTIMAL, INFEASIBLE, LIMIT = "OPTIMAL", "INFEASIBLE", "LIMIT"
+_STATUS_NAME = {LP_OPTIMAL: "certified", LP_ITERATION_LIMIT: "limit", LP_INFEASIBLE: "infeasible",
+                LP_CUTOFF: "cutoff"}
 NODE, LEAF, RETRY = 0, 1, 2
 
 
@@ -55,7 +57,8 @@ class BnBResult:
         self.status = INFEASIBLE
         self.objective = None
         self.z = None            # engine integer vector of the incumbent
-        self.x = None            # routing x[i][f][j] of the incumbent (float32; fetched once, at the end)
+        self.x = None            # routing x[i][f][j] of the incumbent: core.engine.routing.SparseRouting (the
+                                 # device-compacted entries, fetched once at the end; never the dense matrix)
         self.bound = -math.inf   # best proven lower bound
         self.nodes = 0           # branched (non-leaf) nodes whose LP finished
         self.leaves = 0
@@ -66,10 +69,17 @@ class BnBResult:
         self.seconds = 0.0
         self.incumbent_slot = None
         self.polished = False    # the incumbent's LP was re-solved at the polish tolerance
+        # node-LP mix: finished LPs per engine status (+ presolve-infeasible submits) and their iterations
+        self.lp_status = {"certified": 0, "limit": 0, "infeasible": 0, "cutoff": 0, "numerical": 0,
+                          "presolve_infeasible": 0}
+        self.lp_iters = []
 
     def as_dict(self):
-        return {k: getattr(self, k) for k in ("status", "objective", "bound", "nodes", "leaves", "lps", "certified",
-                                              "lp_iterations", "unresolved", "seconds", "polished")}
+        d = {k: getattr(self, k) for k in ("status", "objective", "bound", "nodes", "leaves", "lps", "certified",
+                                           "lp_iterations", "unresolved", "seconds", "polished", "lp_status")}
+        it = np.asarray(self.lp_iters, np.float64)
+        d["lp_iters_p50_p90_p99_max"] = ([float(v) for v in np.percentile(it, [50, 90, 99, 100])] if it.size else None)
+        return d
 
 
 class _Node:
@@ -277,6 +287,7 @@ class BranchAndBound:
                 self.slot_gen[slot] += 1
                 self.res.lps += 1
                 if int(st[b]) == LP_INFEASIBLE:
+                    self.res.lp_status["presolve_infeasible"] += 1
                     self.free.append(slot)
                 else:
                     self.inflight[slot] = node
@@ -285,6 +296,8 @@ class BranchAndBound:
         """Process one finished node LP; returns the (possibly improved) incumbent value."""
         res = self.res
         res.lp_iterations += iters
+        res.lp_iters.append(iters)
+        res.lp_status[_STATUS_NAME.get(st, "numerical")] += 1
         if st == LP_OPTIMAL:
             res.certified += 1
         if not self.root_ready and node.depth == 0 and node.kind == NODE:
@@ -387,9 +400,49 @@ class BranchAndBound:
             r = lp.advance(1)
         if len(r["slots"]) and int(r["status"][0]) == LP_OPTIMAL:
             res.objective = float(r["primal_obj"][0])
-            res.z, res.x = lp.solution(slot, dense_x=True)
+            res.z, _ = lp.solution(slot, dense_x=False)
+            res.x = lp.routing(slot)
             res.polished = True
         # (uncertified: the slot's state moved on; res.x / res.z stay the certified leaf's, fetched before)
+
+    def _finish_sharded(self, res, inc, limit_hit, unresolved_below):
+        """End of a sharded search: one all-gather of every rank's summary; the owner of the best
+        certified incumbent (lowest rank on ties, chosen on the certified objectives BEFORE any polish)
+        polishes it and broadcasts objective, integer vector and compacted routing entries."""
+        comm, lp = self.comm, self.lp
+        mine = res.objective is not None and res.incumbent_slot is not None and res.objective <= inc
+        g = comm.gather([res.bound, 1.0 if limit_hit else 0.0, 1.0 if unresolved_below else 0.0, 1.0 if mine else 0.0,
+                         res.nodes - self.presplit[0], res.lps - self.presplit[1], res.certified - self.presplit[2],
+                         1.0 if self.unresolved_bounds else 0.0])
+        res.bound = float(g[:, 0].min())
+        self._limit_hit = bool(g[:, 1].max() > 0)
+        self._unresolved_below = bool(g[:, 2].max() > 0)
+        self._any_unresolved = bool(g[:, 7].max() > 0)
+        # the pre-split phase ran identically on every rank: count it once
+        res.nodes = int(g[:, 4].sum()) + self.presplit[0]
+        res.lps = int(g[:, 5].sum()) + self.presplit[1]
+        res.certified = int(g[:, 6].sum()) + self.presplit[2]
+        owners = np.flatnonzero(g[:, 3] > 0)
+        if owners.size == 0:
+            res.objective, res.z, res.x = None, None, None
+            return
+        owner = int(owners[0])
+        own = comm.rank == owner
+        if own:
+            res.x = lp.routing(res.incumbent_slot)
+            if self.polish_tol:
+                self._polish(res)
+            head = np.array([res.objective, 1.0 if res.polished else 0.0, float(len(res.x.row))])
+        else:
+            head = np.zeros(3)
+        head = comm.bcast(head, owner)
+        k = int(head[2])
+        z = comm.bcast(np.asarray(res.z if own else np.zeros(lp.n_int), np.float64), owner)
+        row = comm.bcast(np.asarray(res.x.row if own else np.zeros(k), np.int32), owner)
+        dst = comm.bcast(np.asarray(res.x.dst if own else np.zeros(k), np.int32), owner)
+        val = comm.bcast(np.asarray(res.x.val if own else np.zeros(k), np.float64), owner)
+        res.objective, res.polished, res.z = float(head[0]), bool(head[1] > 0), z
+        res.x = lp.routing_from_entries(row, dst, val)
 
     # ---------------------------------------------------------------------------------------
     def solve(self):
@@ -429,10 +482,10 @@ class BranchAndBound:
             stop = res.nodes >= self.node_limit or bool(self.time_limit and time.time() - t0 > self.time_limit)
             open_n = len(self.heap) + len(self.pending) + len(self.retry) + len(self.inflight)
             if comm.world > 1:
-                # every rank takes the same stop / termination decision in the same loop iteration
-                inc = comm.min(inc)
-                stop = comm.sum(int(stop)) > 0
-                open_n = comm.sum(open_n) if sharded else open_n
+                # every rank takes the same stop / termination decision in the same loop iteration: one
+                # collective carries the incumbent (MIN), the stop flags (OR) and the open counts (SUM)
+                inc, stop, total = comm.agree(inc, stop, open_n)
+                open_n = total if sharded else open_n
             if open_n == 0:
                 break
             if stop:
@@ -472,36 +525,23 @@ class BranchAndBound:
                 node = self.inflight.pop(slot, None)
                 if node is not None and int(r["status"][i]) not in (LP_INFEASIBLE, LP_CUTOFF):
                     open_bounds.append(max(node.bound, float(r["obj"][i])))
-        if res.objective is not None and res.incumbent_slot is not None:
-            # the certified leaf's routing, fetched once before the polish re-solve may move the slot
-            _, res.x = lp.solution(res.incumbent_slot, dense_x=True)
-            if self.polish_tol:
-                self._polish(res)
         open_bounds += [h[0] for h in self.heap] + [n.bound for n in self.pending] + [n.bound for n in self.retry]
         open_bounds += self.unresolved_bounds
         res.bound = min(open_bounds + [inc])
-        if comm.world > 1:
-            res.bound = comm.min(res.bound)
-            limit_hit = comm.sum(int(limit_hit)) > 0
-            # the owner of the best incumbent (lowest rank on ties) broadcasts the placement
-            mine = res.objective is not None and res.objective <= inc
-            owner = int(comm.min(comm.rank if mine else comm.world))
-            if owner < comm.world:
-                own = comm.rank == owner
-                z = res.z if own else np.zeros(self.lp.n_int)
-                x = res.x if own else np.zeros((self.N, self.F, self.N), np.float32)
-                res.z = comm.bcast(np.asarray(z, np.float64), owner)
-                res.x = comm.bcast(np.asarray(x, np.float32), owner)
-                res.objective = inc
-            # the pre-split phase ran identically on every rank: count it once
-            res.nodes = comm.sum(res.nodes - self.presplit[0]) + self.presplit[0]
-            res.lps = comm.sum(res.lps - self.presplit[1]) + self.presplit[1]
-            res.certified = comm.sum(res.certified - self.presplit[2]) + self.presplit[2]
         unresolved_below = any(b < inc - self._gap_abs(inc) for b in self.unresolved_bounds)
-        if comm.world > 1:
-            unresolved_below = comm.sum(int(unresolved_below)) > 0
+        if comm.world == 1:
+            if res.objective is not None and res.incumbent_slot is not None:
+                # the certified leaf's routing, fetched once (compacted on the device) before the
+                # polish re-solve may move the slot
+                res.x = lp.routing(res.incumbent_slot)
+                if self.polish_tol:
+                    self._polish(res)
+        else:
+            self._finish_sharded(res, inc, limit_hit, unresolved_below)
+            limit_hit, unresolved_below = self._limit_hit, self._unresolved_below
+        any_unresolved = bool(self.unresolved_bounds) if comm.world == 1 else self._any_unresolved
         if res.objective is None:
-            res.status = LIMIT if (limit_hit or self.unresolved_bounds) else INFEASIBLE
+            res.status = LIMIT if (limit_hit or any_unresolved) else INFEASIBLE
         else:
             res.status = LIMIT if (limit_hit or unresolved_below) else OPTIMAL
         res.seconds = time.time() - t0

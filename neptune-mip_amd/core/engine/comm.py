@@ -1,10 +1,14 @@
 """Communicators for the sharded branch-and-bound.
 
-The only exchanges of the multi-GPU search are latency-bound scalars: all-reduce(MIN) of the
-incumbent bound, all-reduce(SUM) of open-node counts for termination, and one broadcast of the
-winning placement.  `TorchComm` carries them over `torch.distributed` — RCCL over xGMI with the
-"nccl" backend on MI355X (device tensors), gloo on CPU for the multi-process tests.  `LocalComm`
-is the single-process identity.
+The only exchanges of the multi-GPU search are latency-bound scalars and one placement:
+  * `agree(inc, stop, open)` — once per B&B loop, ONE collective (an all-gather of 3 numbers per rank):
+    the incumbent bound (MIN), whether any rank hit its limit (OR) and the open + in-flight node count
+    (SUM);
+  * `gather(values)` — the end-of-search summary (bounds, flags, counters) in one collective;
+  * `bcast` — the winning placement from its owner (the integer vector and the compacted routing
+    entries, never the dense x).
+`TorchComm` carries them over `torch.distributed` — RCCL over xGMI with the "nccl" backend on MI355X
+(device tensors), gloo on CPU for the multi-process tests.  `LocalComm` is the single-process identity.
 """
 import numpy as np
 
@@ -20,6 +24,12 @@ class LocalComm:
 
     def sum(self, v):
         return int(v)
+
+    def agree(self, inc, stop, open_n):
+        return float(inc), bool(stop), int(open_n)
+
+    def gather(self, values):
+        return np.asarray(values, np.float64).reshape(1, -1)
 
     def bcast(self, arr, src):
         return arr
@@ -49,6 +59,17 @@ class TorchComm:
 
     def sum(self, v):
         return int(self._reduce(int(v), self._d.ReduceOp.SUM, self._t.int64))
+
+    def gather(self, values):
+        """[world, k] float64: every rank's `values` (one all-gather, one host sync)."""
+        t = self._t.tensor(np.asarray(values, np.float64).ravel(), dtype=self._t.float64, device=self.device)
+        out = [self._t.empty_like(t) for _ in range(self.world)]
+        self._d.all_gather(out, t, group=self._g)
+        return self._t.stack(out).cpu().numpy()
+
+    def agree(self, inc, stop, open_n):
+        g = self.gather([inc, 1.0 if stop else 0.0, float(open_n)])
+        return float(g[:, 0].min()), bool(g[:, 1].max() > 0), int(round(g[:, 2].sum()))
 
     def bcast(self, arr, src):
         """Broadcast from the member of rank `src` WITHIN this communicator's group (torch's

@@ -298,6 +298,29 @@ class LPModel:
                "nep_lp_get_rows")
         return xb, rf, rs
 
+    def row_map(self):
+        """(row_f, row_src) of the aggregated routing rows (src = -1: the pooled zero-workload sources)."""
+        if getattr(self, "_rowmap", None) is None:
+            R = self.info.n_rows
+            rf = np.zeros(R, np.int32)
+            rs = np.zeros(R, np.int32)
+            _check(self._lib, self._lib.nep_lp_get_rows(self._h, 0, None, _ptr(rf, ctypes.c_int32),
+                                                        _ptr(rs, ctypes.c_int32)), "nep_lp_get_rows")
+            self._rowmap = (rf, rs)
+        return self._rowmap
+
+    def routing_from_entries(self, row, dst, val):
+        from .routing import SparseRouting
+        rf, rs = self.row_map()
+        return SparseRouting(self.N, self.F, rf, rs, self._keep["workload"], row, dst, val)
+
+    def routing(self, slot):
+        """The slot's routing x[i][f][j] as a SparseRouting: every nonzero of the aggregated rows, compacted
+        on the device (nep_lp_routing_entries, threshold 0, unrounded) — the dense N*F*N matrix never
+        crosses PCIe."""
+        row, dst, val = self.routing_entries(slot, threshold=0.0, round3=False)
+        return self.routing_from_entries(row, dst, val)
+
     def set_params(self, tol=1e-7, cutoff=math.inf):
         """tol / cutoff of every LP in flight (nep_lp_set_params): a B&B lowers the cutoff to each new
         incumbent without resubmitting."""
@@ -356,6 +379,14 @@ class LPModel:
         out = np.zeros(16)
         _check(self._lib, self._lib.nep_lp_get_diag(self._h, int(slot), _ptr(out)), "nep_lp_get_diag")
         return dict(zip(self.DIAG, out.tolist()))
+
+    def debug_state(self, slot, n_dual):
+        """Device state of a slot (nep_debug_state): duals y, row activities kz, node bounds lb / ub."""
+        y, kz = np.zeros(n_dual), np.zeros(n_dual)
+        lb, ub = np.zeros(self.n_int), np.zeros(self.n_int)
+        _check(self._lib, self._lib.nep_debug_state(self._h, int(slot), _ptr(y), _ptr(kz), None, _ptr(lb), _ptr(ub)),
+               "nep_debug_state")
+        return {"y": y, "kz": kz, "lb": lb, "ub": ub}
 
     def copy_state(self, src, dst):
         _check(self._lib, self._lib.nep_lp_copy_state(self._h, int(src), int(dst)), "nep_lp_copy_state")

@@ -14,11 +14,13 @@ the GPU solves normally (tests/test_gpu_request.py)."""
 import time
 
 from .solvers import SOLVERS
-from .utils import data_to_solver_input
+from .utils import check_input, data_to_solver_input
 
 
 def solve_request(payload):
-    """Response body of the reference's `serve()` for one payload (dict)."""
+    """Response body of the reference's `serve()` for one payload (dict).  A malformed payload fails
+    the reference's input assertions (`check_input`, main.py:35) before any engine call."""
+    check_input(payload)
     solver = payload.get("solver", {"type": "NeptuneMinDelayAndUtilization"})
     solver_type = solver.get("type")
     solver_args = solver.get("args", {})

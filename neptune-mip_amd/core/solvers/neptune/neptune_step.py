@@ -8,9 +8,11 @@ The reference enumerates the model row by row through pywraplp (`neptune/utils/v
 same model is built structurally by the engine (`nep_model_create`, csrc/nep_host.cpp build(); row
 map in DESIGN.md §2) and solved by the batched GPU branch-and-bound (core/engine/bnb.py).
 
-results() returns the dense x[i][f][j] and c[f][j] matrices of the reference's
-`output_x_and_c` (`neptune/utils/output.py:5-15`); step 1 stores them in data.prev_x / prev_c
-(`neptune_step1.py:21-27`) and the utilisation variants data.prev_n (:55-60).
+results() returns x[i][f][j] and c[f][j] of the reference's `output_x_and_c`
+(`neptune/utils/output.py:5-15`): c dense, x as a core.engine.routing.SparseRouting (the
+device-compacted nonzeros; `np.asarray(x)` gives the dense matrix on demand, the wire format is built
+from the entries); step 1 stores them in data.prev_x / prev_c (`neptune_step1.py:21-27`) and the
+utilisation variants data.prev_n (:55-60).
 """
 import math
 
@@ -18,6 +20,7 @@ import numpy as np
 
 from ...engine import lp as _lp
 from ...engine.bnb import OPTIMAL, BranchAndBound
+from ...engine.routing import SparseRouting
 from ..solver import Solver
 
 
@@ -100,7 +103,7 @@ class NeptuneStepBase(Solver):
         self.result = res
         if res.objective is not None:
             self._value = float(res.objective)
-            self.x_matrix = np.asarray(res.x, np.float64)
+            self.x_matrix = res.x
             c0, c1 = layout["c"]
             self.c_matrix = np.asarray(res.z[c0:c1], np.float64).reshape(F, N)
             if layout.get("n") is not None:
@@ -108,7 +111,7 @@ class NeptuneStepBase(Solver):
         else:
             # no feasible placement: the reference reads zeros back from the failed solve
             self._value = 0.0
-            self.x_matrix = np.zeros((N, F, N))
+            self.x_matrix = SparseRouting.empty(N, F)
             self.c_matrix = np.zeros((F, N))
             self.n_vector = np.zeros(N)
         self.log(f"Problem solved with status {res.status} and value {self._value} "
@@ -197,7 +200,10 @@ class NeptuneStep2Base(NeptuneStepBase):
             # constraints_step2.py:66-68: sum D[i,j] W[f,i] prev_x[i,f,j]
             D = np.asarray(d.node_delay_matrix, np.float64)
             W = np.asarray(d.workload_matrix, np.float64)
-            kw["prev_network_delay"] = float(np.einsum("ij,fi,ifj->", D, W, np.asarray(prev, np.float64)))
+            if isinstance(prev, SparseRouting):
+                kw["prev_network_delay"] = prev.network_delay(D, W)
+            else:
+                kw["prev_network_delay"] = float(np.einsum("ij,fi,ifj->", D, W, np.asarray(prev, np.float64)))
         return kw
 
     def upper_bound(self):

@@ -8,6 +8,15 @@ import numpy as np
 
 
 def convert_x_matrix(matrix, nodes, functions):
+    if hasattr(matrix, "wire_entries"):
+        # core.engine.routing.SparseRouting: the device-compacted entries, in the dense path's (i, f, j)
+        # order and with its threshold / rounding, so the dict is the same byte for byte
+        assert tuple(matrix.shape) == (len(nodes), len(functions), len(nodes))
+        out = {}
+        ii, ff, jj, vals = matrix.wire_entries(0.001)
+        for i, f, j, v in zip(ii.tolist(), ff.tolist(), jj.tolist(), vals.tolist()):
+            out.setdefault(nodes[i], {}).setdefault(functions[f], {})[nodes[j]] = float(v)
+        return out
     matrix = np.asarray(matrix)
     assert matrix.shape == (len(nodes), len(functions), len(nodes)), (
         f"X matrix shape malformed. matrix shape is {matrix.shape} but it should be "

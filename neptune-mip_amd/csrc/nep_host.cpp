@@ -25,7 +25,6 @@ hipError_t launch_x_pass(const DeviceView &v, const int32_t *slots, int nslots, 
                          bool plain, int it, hipStream_t s);
 hipError_t launch_node_pass(const DeviceView &v, const int32_t *slots, int nslots, bool check, bool init, bool first,
                             bool plain, int it, hipStream_t s);
-hipError_t launch_dblock_pass(const DeviceView &v, const int32_t *slots, int nslots, hipStream_t s);
 hipError_t launch_scalar_pass(const DeviceView &v, const int32_t *slots, int nslots, bool check, bool init,
                               bool first, bool plain, int it, int block_len, hipStream_t s);
 hipError_t launch_node_bounds(const DeviceView &v, const int32_t *slots, int nslots, const double *base_lb,
@@ -993,8 +992,7 @@ hipError_t block_graph(Model &m, int na, hipGraphExec_t *out) {
     for (int it = 0; it < ce && le == hipSuccess; ++it) {
       const bool check = it == 0, first = it == 1;
       const bool plain = !kHalpern || ce < 4 || it == 0 || it == ce - 1;
-      if (check && m.step2) le = launch_dblock_pass(m.v, m.d_slots, na, m.stream);
-      if (le == hipSuccess) le = launch_x_pass(m.v, m.d_slots, na, check, false, first, plain, it, m.stream);
+      le = launch_x_pass(m.v, m.d_slots, na, check, false, first, plain, it, m.stream);
       if (le == hipSuccess) le = launch_node_pass(m.v, m.d_slots, na, check, false, first, plain, it, m.stream);
       if (le == hipSuccess && (m.step2 || check))
         le = launch_scalar_pass(m.v, m.d_slots, na, check, false, first, plain, it, ce, m.stream);
@@ -1043,7 +1041,6 @@ int launch_block(Model &m) {
     const bool check = it == 0, first = it == 1;
     const bool plain = !kHalpern || ce < 4 || it == 0 || it == ce - 1;
     const bool sample = it == sample_it;
-    if (check && m.step2) HIPCHK(launch_dblock_pass(v, m.d_slots, na, m.stream));
     if (sample) HIPCHK(hipEventRecord(m.ev0, m.stream));
     HIPCHK(launch_x_pass(v, m.d_slots, na, check, false, first, plain, it, m.stream));
     if (sample) HIPCHK(hipEventRecord(m.ev1, m.stream));
@@ -1393,6 +1390,12 @@ int nep_lp_copy_state(void *model, int32_t src, int32_t dst) {
                         m.stream));
   HIPCHK(hipMemcpyAsync(v.kty + dst * v.skty, v.kty + src * v.skty, v.skty * sizeof(float), hipMemcpyDeviceToDevice,
                         m.stream));
+  // the certificate's repaired point travels with the status it belongs to: solution_z() of a copied
+  // certified slot returns the source's repaired point, not the destination's stale one
+  HIPCHK(hipMemcpyAsync(v.zr + dst * v.sint, v.zr + src * v.sint, v.sint * sizeof(double), hipMemcpyDeviceToDevice,
+                        m.stream));
+  HIPCHK(hipMemcpyAsync(v.rpart + dst * v.srpart, v.rpart + src * v.srpart, v.srpart * sizeof(double),
+                        hipMemcpyDeviceToDevice, m.stream));
   HIPCHK(hipMemcpyAsync(v.ctrl + dst, v.ctrl + src, sizeof(Ctrl), hipMemcpyDeviceToDevice, m.stream));
   HIPCHK(hipStreamSynchronize(m.stream));
   return NEP_OK;

@@ -65,8 +65,9 @@ struct RowInfo {
   int32_t src, f, pad0, pad1;
 };
 
-// per-function scalar partials
-enum { TS_SCORE = 0, TS_POBJ, TS_LAGR, TS_MOVE, TS_DIST, TS_EMPTY, NTS };
+// per-function scalar partials (TS_LAGR_REP: the routing rows' Lagrangian terms at the repaired
+// column prices, DESIGN.md §4 "Dual repair")
+enum { TS_SCORE = 0, TS_POBJ, TS_LAGR, TS_MOVE, TS_DIST, TS_EMPTY, TS_LAGR_REP, NTS };
 // per-block scalar partials of the small variables
 enum {
   BS_SUMC_NEW = 0,   // sum over (f,j) of c'            (step-2 rows D3/D4)
@@ -78,9 +79,11 @@ enum {
   BS_SUMC_REP,       // certificate: sum over (f,j) of the repaired c (step-2 rows D3/D4)
   BS_SCORE_N_REP,    // certificate: score-row n part of the repaired n
   BS_LAGR_D,         // step 2: the disruption block's share of the Lagrangian (c, moved, a, d; D1-D4)
+  BS_LAGR_REP,       // certificate: the small variables' / node rows' Lagrangian terms at the repaired duals
   BS_TLO, BS_THI,    // step 2: sum over (f,j) of the node box of c (the range of sum c)
   BS_LK0,            // step 2: the disruption block kept exact, one sum per price lambda_k of sum c
-  NBS = BS_LK0 + 6   //   (kNLam candidates; DESIGN.md §4 "Disruption block")
+  BS_LKR0 = BS_LK0 + 6,   //   (kNLam candidates; DESIGN.md §4 "Disruption block"), and the same at the
+  NBS = BS_LKR0 + 6       //   repaired column prices (DESIGN.md §4 "Dual repair")
 };
 constexpr int kNLam = 6;
 // BS_POBJ / BS_RES carry, on certificate iterations, the objective of the REPAIRED small variables and

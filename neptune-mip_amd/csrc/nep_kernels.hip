@@ -95,6 +95,7 @@ __device__ __forceinline__ double row_viol(double a, double lo, double hi) {
 struct SmallAcc {
   double lagr = 0, pobj = 0, res = 0, mvz = 0, mvy = 0, dsz = 0, dsy = 0;
   double lagrD = 0;   // Lagrangian terms of the step-2 disruption block (dblk calls)
+  double lagrR = 0;   // certificate: Lagrangian terms at the repaired duals (DESIGN.md §4 "Dual repair")
 };
 
 // ---------------------------------------------------------------------------------------------
@@ -131,6 +132,120 @@ __device__ __forceinline__ double dblock_item(double r, double lam, double old, 
     best = fmin(best, (r - lam) * c + cmf * fmax(lmf, c - old) + cmt * fmax(lmt, old - c));
   }
   return best;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Dual repair of the big-M row pairs at certificate iterations (DESIGN.md §4 "Dual repair").  C1/C2
+// (S - M c <= 0, S - c >= -eps) enter c's reduced cost as M*y1 + y2 and the routing columns as
+// y1 + y2 =: s; C6/C7 enter n's as M*y6 + y7 and c's as y6 + y7 =: t.  At an LP optimum an interior
+// c (e.g. c = S / M) has reduced cost exactly 0, so a dual error d in s moves the Lagrangian by M*d
+// (the box of c has width 1); and a column price the PDHG has not resolved at the 1e-6 level (the
+// 1/M price of routing flow to a destination that is not the old placement) drops that whole part
+// of the objective from the bound (tools/dual_repair_probe.py).  The repair re-prices
+// each pair from the iterate's own c (complementary slackness, as a crossover would):
+//   * c inside a linear piece of its (disruption-)cost: the price that makes that piece's slope 0;
+//   * c at 0 = its lower end: the lowest price keeping c = 0 a minimiser (lowering s never lowers the
+//     routing rows' terms, and c's term stays 0);
+//   * otherwise (c at an upper end / kink): the price among the breakpoints (s0 first) that
+//     maximises the pair's own terms, with the routing rows' change bounded pessimistically (raising
+//     s by D lowers every routing row of f by at most its weight times D, N in all).
+// s is split back as y1 = min(0, s), y2 = max(0, s); t alike from n.  Any sign-feasible dual gives a
+// valid bound: the certificate takes the better of the plain and the repaired one.
+// ---------------------------------------------------------------------------------------------
+constexpr double kRepairTol = 1e-7;   // an iterate within this of a box end / kink sits on it
+__device__ __forceinline__ double price_rc(double b, double s, double M) { return b + M * fmin(s, 0.0) + fmax(s, 0.0); }
+__device__ __forceinline__ double price_at(double b, double target, double M) {
+  const double d = target - b;   // the s with price_rc(b, s) == target
+  return d < 0.0 ? d / M : d;
+}
+// a (c or n) on its box [lb, ub] with reduced cost price_rc(b, s); z its iterate
+__device__ __forceinline__ double repair_box(double b, double s0, double z, double lb, double ub, double M,
+                                             double eps, double K) {
+  if (z > lb + kRepairTol && z < ub - kRepairTol) return price_at(b, 0.0, M);   // interior: reduced cost 0
+  if (z <= lb + kRepairTol && lb == 0.0) return price_at(b, 0.0, M);           // at 0: lowest price keeping it
+  const double cand[4] = {s0, 0.0, price_at(b, 0.0, M), -b};
+  double best = -INFINITY, sb = s0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const double s = cand[q], rc = price_rc(b, s, M);
+    const double val = fmin(rc * lb, rc * ub) - eps * fmax(s, 0.0) - K * fmax(s - s0, 0.0);
+    if (val > best) { best = val; sb = s; }
+  }
+  return sb;
+}
+// step 2: c with its disruption block (dblock_item) at the price lam of sum c; z its iterate.  The
+// block's cost in c has slopes (r - lam) - cmt / (r - lam) / (r - lam) + cmf on the pieces split at
+// the kinks old - lmt and old + lmf.
+__device__ __forceinline__ double repair_dblock(double b, double s0, double z, double lam, double old, double cmf,
+                                                double lmf, double cmt, double lmt, double clo, double chi, double M,
+                                                double eps, double K) {
+  const double k1 = old - lmt, k2 = old + lmf, t = kRepairTol;
+  const bool at_k = fabs(z - k1) <= t || fabs(z - k2) <= t;
+  const double piece = z < k1 ? -cmt : (z > k2 ? cmf : 0.0);          // slope constant of z's piece
+  if (z > clo + t && z < chi - t && !at_k) return price_at(b, lam - piece, M);
+  if (z <= clo + t && clo == 0.0 && clo < chi) {
+    // lowest price keeping c = 0 a minimiser: the slope right of 0 is >= 0
+    const double right = (0.0 >= k2 - t) ? cmf : ((0.0 >= k1 - t) ? 0.0 : -cmt);
+    return price_at(b, lam - right, M);
+  }
+  const double cand[5] = {s0, 0.0, price_at(b, lam + cmt, M), price_at(b, lam, M), price_at(b, lam - cmf, M)};
+  double best = -INFINITY, sb = s0;
+#pragma unroll
+  for (int q = 0; q < 5; ++q) {
+    const double s = cand[q];
+    const double val = dblock_item(price_rc(b, s, M), lam, old, cmf, lmf, cmt, lmt, clo, chi) - eps * fmax(s, 0.0) -
+                       K * fmax(s - s0, 0.0);
+    if (val > best) { best = val; sb = s; }
+  }
+  return sb;
+}
+// the price of sum c the repair aims at: the PDHG's own (lam[0]) snapped to a fixed candidate price
+// (+-ca, +-cd, 0) when within 1e-6 of it — the optimal price is usually one of them exactly, and
+// T = sum c ranges over [0, F N], so a price off by d costs up to F N d
+__device__ __forceinline__ double repair_lambda(const double (&lam)[kNLam]) {
+#pragma unroll
+  for (int q = 1; q < kNLam; ++q)
+    if (fabs(lam[0] - lam[q]) <= 1e-6 * fmax(1.0, fabs(lam[q]))) return lam[q];
+  return lam[0];
+}
+// n[j]'s reduced cost without C6/C7 (its cost and the step-2 score row); pre-update duals
+__device__ __forceinline__ double node_base(const DeviceView &v, const double *y, int j) {
+  return v.cost_int[v.il.on + j] - v.score_n_coef * (v.step2 ? y[v.dl.oS] : 0.0);
+}
+// node j's repaired C6/C7 price t* (n's own terms; raising t lowers each c[f, j]'s term by at most its
+// width: F in all); n: the iterate
+__device__ __forceinline__ double repair_node(const DeviceView &v, double t0, double b, double n, double lbn,
+                                              double ubn) {
+  return repair_box(b, t0, n, lbn, ubn, v.M, v.eps, (double)v.F);
+}
+__device__ __forceinline__ double repaired_node_price(const DeviceView &v, int slot, int j) {
+  const double *y = v.y + slot * v.sdual, *zi = v.zi + slot * v.sint;
+  const double *lb = v.lb + slot * v.sint, *ub = v.ub + slot * v.sint;
+  const int k = v.il.on + j;
+  return repair_node(v, y[v.dl.o6 + j] + y[v.dl.o7 + j], node_base(v, y, j), zi[k], lb[k], ub[k]);
+}
+// c[f, j]'s reduced cost without C1/C2 (and without the step-2 D rows, which dblock_item keeps exact),
+// at node j's repaired C6/C7 price
+__device__ __forceinline__ double repaired_c_base(const DeviceView &v, int slot, int f, int j) {
+  const double *y = v.y + slot * v.sdual;
+  double b = v.cost_int[v.il.oc + f * v.N + j] - v.mem_f[f] * y[v.dl.o3 + j];
+  if (v.has_n) b -= repaired_node_price(v, slot, j);
+  return b;
+}
+// the repaired column price s*[f, j] = y1 + y2 of C1/C2 (lam: the step-2 price of sum c); pre-update
+// duals and iterate (x_pass's certificate launch, before it updates them)
+__device__ __forceinline__ double repaired_col_price(const DeviceView &v, int slot, int f, int j, double lam) {
+  const double *y = v.y + slot * v.sdual, *zi = v.zi + slot * v.sint;
+  const double *lb = v.lb + slot * v.sint, *ub = v.ub + slot * v.sint;
+  const IntLayout &il = v.il;
+  const int idx = f * v.N + j;
+  const double b = repaired_c_base(v, slot, f, j), s0 = y[v.dl.o1 + idx] + y[v.dl.o2 + idx];
+  const double z = zi[il.oc + idx];
+  if (!v.step2) return repair_box(b, s0, z, lb[il.oc + idx], ub[il.oc + idx], v.M, v.eps, (double)v.N);
+  const double old = -v.lo[v.dl.oD1 + idx];
+  const double clo = fmax(lb[il.oc + idx], old - ub[il.omt + idx]), chi = fmin(ub[il.oc + idx], old + ub[il.omf + idx]);
+  return repair_dblock(b, s0, z, lam, old, v.cost_int[il.omf + idx], lb[il.omf + idx], v.cost_int[il.omt + idx],
+                       lb[il.omt + idx], clo, chi, v.M, v.eps, (double)v.N);
 }
 
 // Operands of one dual row / one small variable, loaded ahead of their update (node_pass issues
@@ -296,6 +411,49 @@ __device__ __forceinline__ void load_row(const float *__restrict__ xrow, const f
   }
 }
 
+// The certificate's pooled shift (one wave; x_pass, DESIGN.md §4 "Pooled shift"): S[j] the fp64
+// column sums of f, pm[j] the pooled row's flow.  Deficits are served in j order, each from the
+// donors in j order; deterministic.
+constexpr double kShiftMax = 1e-6;
+__device__ __forceinline__ void pooled_shift(const DeviceView &v, int slot, int f, double *S, double *pm, int lane) {
+  const int N = v.N;
+  const double *zi = v.zi + slot * v.sint, *lb = v.lb + slot * v.sint, *ub = v.ub + slot * v.sint;
+  const int oc = v.il.oc + f * N;
+  auto target = [&](int j) { return fmin(fmax(zi[oc + j], lb[oc + j]), ub[oc + j]); };
+  for (int j0 = 0; j0 < N; j0 += kWave) {
+    const int j = j0 + lane;
+    // only rounding-level deficits (<= kShiftMax): the returned routing is the stored fp32 x, which
+    // the shifted point may differ from by no more than that
+    const double need = j < N ? target(j) - v.eps - S[j] : 0.0;
+    uint64_t mask = __ballot(need > 0.0 && need <= kShiftMax);
+    while (mask) {
+      const int k = __builtin_ctzll(mask);
+      mask &= mask - 1;
+      const int jd = j0 + k;
+      double want = target(jd) - v.eps - S[jd];   // (re-read: earlier transfers may have moved S[jd])
+      for (int d0 = 0; d0 < N && want > 0.0; d0 += kWave) {
+        const int d = d0 + lane;
+        const double av = (d < N && d != jd) ? fmin(pm[d], S[d] + v.eps - target(d)) : 0.0;
+        uint64_t dm = __ballot(av > 0.0);
+        while (dm && want > 0.0) {
+          const int kd = __builtin_ctzll(dm);
+          dm &= dm - 1;
+          const int dj = d0 + kd;
+          const double t = fmin(want, __shfl(av, kd, kWave));
+          if (lane == 0) {
+            S[dj] -= t;
+            pm[dj] -= t;
+            S[jd] += t;
+            pm[jd] += t;
+          }
+          want -= t;
+        }
+        __builtin_amdgcn_wave_barrier();
+      }
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------------------------
 // x_pass: one workgroup = all routing rows of ONE function f of one LP slot, then the
 // per-(f, j) small variables of that f.
@@ -376,6 +534,15 @@ void x_pass(DeviceView v, const int32_t *__restrict__ slots, int plain, int it, 
   float *lS = lds, *lW = lds + SW * TW * NP, *lK = lW + SW * TW * NP, *lC = lK + NP;
   double *lSd = reinterpret_cast<double *>(lS), *lWd = reinterpret_cast<double *>(lW);
   double *lKd = reinterpret_cast<double *>(lC + NP), *lCd = lKd + NP;
+  double *lKr = lCd + NP;   // certificate: the repaired column prices s*[j] of f (DESIGN.md §4 "Dual repair")
+  double *lPm = lKr + NP;   // certificate: the pooled row's flow m * x̂[pooled, j] (fp64; DESIGN.md §4 "Pooled shift")
+  // the price of sum c the step-2 repair aims at (pre-update duals of D3a / D3b / D4)
+  double lam_rep = 0.0;
+  if (CHECK && v.step2) {
+    double lamk[kNLam];
+    dblock_lambdas(v, v.y + slot * v.sdual, lamk);
+    lam_rep = repair_lambda(lamk);
+  }
   for (int j = threadIdx.x; j < NP; j += kWave * TW) {
     if (pol_leave) {
       const bool in = j < N;
@@ -390,6 +557,8 @@ void x_pass(DeviceView v, const int32_t *__restrict__ slots, int plain, int it, 
       const bool in = j < N;
       lKd[j] = in ? yv[v.dl.o1 + f * N + j] + yv[v.dl.o2 + f * N + j] : 0.0;
       lCd[j] = in ? (double)v.cpr[(int64_t)f * NP + j] * yv[v.dl.o5 + j] : 0.0;
+      lKr[j] = in ? repaired_col_price(v, slot, f, j, lam_rep) : 0.0;
+      lPm[j] = 0.0;
     }
   }
   const double ysd = (CHECK && v.step2) ? v.y[slot * v.sdual + v.dl.oS] : 0.0;
@@ -417,7 +586,7 @@ void x_pass(DeviceView v, const int32_t *__restrict__ slots, int plain, int it, 
 #pragma unroll
   for (int e = 0; e < E; ++e) cnt_f += __popcll(__ballot((mbits >> e) & 1u));
 
-  double s_score = 0.0, s_pobj = 0.0, s_lagr = 0.0, s_move = 0.0, s_dist = 0.0;
+  double s_score = 0.0, s_pobj = 0.0, s_lagr = 0.0, s_lagr_r = 0.0, s_move = 0.0, s_dist = 0.0;
   const double s_empty = (cnt_f == 0 && threadIdx.x == 0) ? (double)nrows : 0.0;
 
   for (int rr = wave; rr < nrows; rr += TW) {
@@ -472,18 +641,21 @@ void x_pass(DeviceView v, const int32_t *__restrict__ slots, int plain, int it, 
       if ((mbits >> e) & 1u) s += vv[e];
     }
     if (CHECK) {
-      // Lagrangian term of this row: min over the simplex of the reduced cost, in fp64
-      double gmin = INFINITY;
+      // Lagrangian term of this row: min over the simplex of the reduced cost, in fp64, at the PDHG
+      // duals and at the repaired column prices
+      double gmin = INFINITY, gmin_r = INFINITY;
 #pragma unroll
       for (int e = 0; e < E; ++e) {
         if ((mbits >> e) & 1u) {
           const int j = 4 * (lane + kWave * (e / 4)) + (e & 3);
-          const double g = (double)wobj * dc[e] - ((double)m * lKd[j] + (double)w * lCd[j] + (double)wsc * ysd * dc[e]);
-          gmin = fmin(gmin, g);
+          const double g0 = (double)wobj * dc[e] - ((double)w * lCd[j] + (double)wsc * ysd * dc[e]);
+          gmin = fmin(gmin, g0 - (double)m * lKd[j]);
+          gmin_r = fmin(gmin_r, g0 - (double)m * lKr[j]);
         }
       }
       gmin = wave_min_d(gmin);
-      if (lane == 0) s_lagr += gmin;
+      gmin_r = wave_min_d(gmin_r);
+      if (lane == 0) { s_lagr += gmin; s_lagr_r += gmin_r; }
     }
     // Projection onto {x >= 0, sum x = 1} over the allowed destinations: the threshold theta is
     // the root of f(t) = sum_j max(v_j - t, 0) - 1 (convex, decreasing).  Michelot's iteration is
@@ -551,6 +723,13 @@ void x_pass(DeviceView v, const int32_t *__restrict__ slots, int plain, int it, 
     float xn[E];
 #pragma unroll
     for (int e = 0; e < E; ++e) xn[e] = ((mbits >> e) & 1u) ? fmaxf(vv[e] - theta, 0.f) : 0.f;
+    if (CHECK && ri.src < 0) {   // the pooled row of f: its flow, for the certificate's pooled shift
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        const int j = 4 * (lane + kWave * (e / 4)) + (e & 3);
+        if (j < NP) lPm[j] = (double)m * (double)xn[e];
+      }
+    }
 
     // anchor row: needed by the Halpern combination and by the certificate's restart distance
     float xav[E];
@@ -649,6 +828,28 @@ void x_pass(DeviceView v, const int32_t *__restrict__ slots, int plain, int it, 
 
   // cross-wave reduction of the column partials (each wave's accumulators are in LDS)
   __syncthreads();
+  if (CHECK) {
+    // certificate: the column / CPU sums of f in fp64, reduced over the waves into wave 0's slots, then
+    // the pooled shift (DESIGN.md §4 "Pooled shift"): a destination j whose c the certificate wants
+    // at ~1 (the iterate's c) but whose fp32 column sum S_j fell short of c - eps by rounding takes the
+    // missing flow from the pooled row (zero-workload sources: no cost, CPU or score coefficient) at a
+    // destination with slack (S + eps above its own c); the certificate point is x̂ with the pooled row
+    // shifted by those fp64 amounts, the same simplex and the same objective.  Without it a deficit of
+    // d costs (2 F N - 1) d on step 2 (moved_to + allocated), ~1e-4 at 64x32 from fp32 rounding alone.
+    for (int j = threadIdx.x; j < N; j += kWave * TW) {
+      double Sd = 0.0, Ud = 0.0;
+#pragma unroll
+      for (int wv = 0; wv < TW; ++wv) {
+        Sd += lSd[wv * NP + j];
+        Ud += lWd[wv * NP + j];
+      }
+      lSd[j] = Sd;
+      lWd[j] = Ud;
+    }
+    __syncthreads();
+    if (wave == 0) pooled_shift(v, slot, f, lSd, lPm, lane);
+    __syncthreads();
+  }
 
   // per-(f, j) small variables and rows
   const DualLayout &dl = v.dl;
@@ -668,15 +869,21 @@ void x_pass(DeviceView v, const int32_t *__restrict__ slots, int plain, int it, 
   const double csd = cs;   // polishing: small-variable costs off as well
   SmallAcc a;
   double sumc = 0.0, sumc_rep = 0.0;
+  // step-2 certificate: the disruption block's exact terms per candidate price (PDHG / repaired duals)
+  // and f's share of the node box of sum c
+  double lamk[kNLam], dlk[kNLam], dlkr[kNLam], dtlo = 0.0, dthi = 0.0;
+#pragma unroll
+  for (int q = 0; q < kNLam; ++q) { lamk[q] = 0.0; dlk[q] = dlkr[q] = 0.0; }
+  if (CHECK && v.step2) dblock_lambdas(v, y, lamk);
   for (int j = threadIdx.x; j < N; j += kWave * TW) {
     float Sf = 0.f, Uf = 0.f;
     double Sd = 0.0, Ud = 0.0;
+    if (CHECK) {
+      Sd = lSd[j];   // reduced (and pooled-shifted) above
+      Ud = lWd[j];
+    } else {
 #pragma unroll
-    for (int wv = 0; wv < TW; ++wv) {
-      if (CHECK) {
-        Sd += lSd[wv * NP + j];
-        Ud += lWd[wv * NP + j];
-      } else {
+      for (int wv = 0; wv < TW; ++wv) {
         Sf += lS[wv * NP + j];
         Uf += lW[wv * NP + j];
       }
@@ -697,6 +904,30 @@ void x_pass(DeviceView v, const int32_t *__restrict__ slots, int plain, int it, 
       y1 = y2 = y3 = y6 = y7 = 0.0;
     }
     double kty_c = -v.M * y1 - y2 + memf * y3 + y6 + y7;
+    if (CHECK) {
+      // the bound's small-variable terms at the repaired duals (DESIGN.md §4 "Dual repair"), and on
+      // step 2 the disruption block kept exact (dblock_item) at both the PDHG and the repaired duals
+      const double sr = lKr[j];
+      const double rcr = price_rc(repaired_c_base(v, slot, f, j), sr, v.M);
+      const double clb = lb[il.oc + idx], cub = ub[il.oc + idx];
+      a.lagrR -= v.eps * fmax(sr, 0.0);
+      if (!v.step2) {
+        a.lagrR += fmin(clb * rcr, cub * rcr);
+      } else {
+        const double r0 = v.cost_int[il.oc + idx] - kty_c;   // c's reduced cost without the D rows
+        const double old = -v.lo[dl.oD1 + idx];
+        const double lmf = lb[il.omf + idx], lmt = lb[il.omt + idx];
+        const double clo = fmax(clb, old - ub[il.omt + idx]), chi = fmin(cub, old + ub[il.omf + idx]);
+        const double cmf = v.cost_int[il.omf + idx], cmt = v.cost_int[il.omt + idx];
+        dtlo += clb;
+        dthi += cub;
+#pragma unroll
+        for (int q = 0; q < kNLam; ++q) {
+          dlk[q] += dblock_item(r0, lamk[q], old, cmf, lmf, cmt, lmt, clo, chi);
+          dlkr[q] += dblock_item(rcr, lamk[q], old, cmf, lmf, cmt, lmt, clo, chi);
+        }
+      }
+    }
     double yd1 = 0.0, yd2 = 0.0;
     if (v.step2) {
       yd1 = ysrc[dl.oD1 + idx];
@@ -774,7 +1005,16 @@ void x_pass(DeviceView v, const int32_t *__restrict__ slots, int plain, int it, 
   vals[NTS + BS_SUMC_REP] = sumc_rep;
   vals[NTS + BS_SCORE_N_REP] = 0.0;
   vals[NTS + BS_LAGR_D] = a.lagrD;
-  constexpr int NW = NTS + BS_TLO;   // the fields from BS_TLO on are dblock_pass's
+  vals[TS_LAGR_REP] = s_lagr_r;
+  vals[NTS + BS_LAGR_REP] = a.lagrR;
+  vals[NTS + BS_TLO] = dtlo;
+  vals[NTS + BS_THI] = dthi;
+#pragma unroll
+  for (int q = 0; q < kNLam; ++q) {
+    vals[NTS + BS_LK0 + q] = dlk[q];
+    vals[NTS + BS_LKR0 + q] = dlkr[q];
+  }
+  constexpr int NW = NTS + NBS;
 #pragma unroll
   for (int k = 0; k < NW; ++k) {
     const bool needed = INIT || CHECK || k == TS_SCORE || k == NTS + BS_SUMC_NEW;
@@ -809,9 +1049,10 @@ __device__ __forceinline__ void write_bpart(double *bp, const SmallAcc &a, doubl
   vals[BS_DIST_Z] = a.dsz;
   vals[BS_DIST_Y] = a.dsy;
   vals[BS_LAGR_D] = a.lagrD;
+  vals[BS_LAGR_REP] = a.lagrR;
   vals[BS_TLO] = vals[BS_THI] = 0.0;
 #pragma unroll
-  for (int q = 0; q < kNLam; ++q) vals[BS_LK0 + q] = 0.0;
+  for (int q = 0; q < kNLam; ++q) vals[BS_LK0 + q] = vals[BS_LKR0 + q] = 0.0;
   // plain step-2 iterations: scalar_pass reads only the row fields (ALL = false)
 #pragma unroll
   for (int k = 0; k < NBS; ++k) {
@@ -941,6 +1182,16 @@ __global__ __launch_bounds__(kNodeThreads) void node_pass(DeviceView v, const in
     // certificate point (see x_pass): C3 at the repaired c, C5 (x only)
     a.res = fmax(a.res, row_viol(memr, p3.lo, p3.hi) / nrm3);
     a.res = fmax(a.res, row_viol(U, p5.lo, p5.hi) / nrm5);
+    // the node rows' and n's bound terms at the repaired duals (C6/C7 at node j's price t*: the same
+    // t* x_pass priced c with, from the same pre-update duals; DESIGN.md §4 "Dual repair")
+    a.lagrR += row_lagr(p3.y, p3.lo, p3.hi) + row_lagr(p5.y, p5.lo, p5.hi);
+    if (v.has_n) {
+      const double bn = node_base(v, y, j);
+      const double ts = repair_node(v, p6.y + p7.y, bn, pn.z, pn.lb, pn.ub);
+      const double rcn = price_rc(bn, ts, v.M);
+      a.lagrR += row_lagr(fmin(ts, 0.0), p6.lo, p6.hi) + row_lagr(fmax(ts, 0.0), p7.lo, p7.hi) +
+                 fmin(pn.lb * rcn, pn.ub * rcn);
+    }
   }
   if (valid) {
     dual_step_p<CHECK, INIT>(y, ya, kz, kza, dl.o3 + j, memc, p3, sigma, copy_anchor, halp, lam, a);
@@ -968,55 +1219,6 @@ __global__ __launch_bounds__(kNodeThreads) void node_pass(DeviceView v, const in
   // step-2 score row on every step-2 iteration (plain step-1 iterations skip 21 wave reductions)
   if (CHECK || INIT) write_bpart<true>(v.bpart + slot * v.sbpart + ((int64_t)F + jb) * NBS, a, 0.0, score_n, score_n_rep, lane);
   else if (v.step2) write_bpart<false>(v.bpart + slot * v.sbpart + ((int64_t)F + jb) * NBS, a, 0.0, score_n, score_n_rep, lane);
-}
-
-// ---------------------------------------------------------------------------------------------
-// dblock_pass (step-2 certificate iterations, launched BEFORE that iteration's x_pass so that it
-// reads the same duals y the rest of the bound uses): per (f, slot), the disruption-block terms of
-// the exact bound for each candidate price (dblock_item), and f's share of the node box of sum c.
-// Writes bpart[f][BS_TLO ..]; x_pass leaves those fields alone.
-// ---------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void dblock_pass(DeviceView v, const int32_t *__restrict__ slots) {
-  __shared__ double red[4][2 + kNLam];
-  const int f = blockIdx.x;
-  const int slot = slots[blockIdx.y];
-  const Ctrl *ctrl = v.ctrl + slot;
-  if (!ctrl->active) return;
-  const DualLayout &dl = v.dl;
-  const IntLayout &il = v.il;
-  const int N = v.N;
-  const double *y = v.y + slot * v.sdual;
-  const double *lb = v.lb + slot * v.sint, *ub = v.ub + slot * v.sint;
-  double lamk[kNLam], acc[2 + kNLam];
-  dblock_lambdas(v, y, lamk);
-#pragma unroll
-  for (int q = 0; q < 2 + kNLam; ++q) acc[q] = 0.0;
-  const double memf = v.mem_f[f];
-  for (int j = threadIdx.x; j < N; j += 256) {
-    const int idx = f * N + j;
-    double kty_c = -v.M * y[dl.o1 + idx] - y[dl.o2 + idx] + memf * y[dl.o3 + j];
-    if (v.has_n) kty_c += y[dl.o6 + j] + y[dl.o7 + j];
-    const double r = v.cost_int[il.oc + idx] - kty_c;   // c's reduced cost without the D rows
-    const double old = -v.lo[dl.oD1 + idx];
-    const double lmf = lb[il.omf + idx], lmt = lb[il.omt + idx];
-    const double clo = fmax(lb[il.oc + idx], old - ub[il.omt + idx]);
-    const double chi = fmin(ub[il.oc + idx], old + ub[il.omf + idx]);
-    const double cmf = v.cost_int[il.omf + idx], cmt = v.cost_int[il.omt + idx];
-    acc[0] += lb[il.oc + idx];
-    acc[1] += ub[il.oc + idx];
-#pragma unroll
-    for (int q = 0; q < kNLam; ++q) acc[2 + q] += dblock_item(r, lamk[q], old, cmf, lmf, cmt, lmt, clo, chi);
-  }
-  const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x >> 6;
-#pragma unroll
-  for (int q = 0; q < 2 + kNLam; ++q) {
-    const double t = wave_sum_d(acc[q]);
-    if (lane == 0) red[wave][q] = t;
-  }
-  __syncthreads();
-  const int q = threadIdx.x;
-  if (q < 2 + kNLam)
-    v.bpart[slot * v.sbpart + (int64_t)f * NBS + BS_TLO + q] = red[0][q] + red[1][q] + red[2][q] + red[3][q];
 }
 
 // Primal feasibility polishing (scalar_pass): after nep_lp_opts.polish_after iterations, an LP whose best
@@ -1153,6 +1355,7 @@ __global__ __launch_bounds__(256) void scalar_pass(DeviceView v, const int32_t *
   a.dsz = tot[TS_DIST] + tot[NTS + BS_DIST_Z];
   a.dsy = tot[NTS + BS_DIST_Y];
   a.lagrD = tot[NTS + BS_LAGR_D];
+  double score_lagr = 0.0;   // the step-2 score row's bound term (pre-update dual)
 
   if (v.step2) {
     const double sumc = tot[NTS + BS_SUMC_NEW];
@@ -1177,6 +1380,7 @@ __global__ __launch_bounds__(256) void scalar_pass(DeviceView v, const int32_t *
     dual_step<CHECK, INIT>(v, y, ya, kz, kza, dl.oD3b, sumc - dn, yD3b, sigma, copy_anchor, halp, lam, a, true);
     dual_step<CHECK, INIT>(v, y, ya, kz, kza, dl.oD4, dn + an + v.sigma4 * sumc, yD4, sigma, copy_anchor, halp, lam,
                            a, true);
+    if (CHECK) score_lagr = row_lagr(yS, v.lo[dl.oS], v.hi[dl.oS]);
     dual_step<CHECK, INIT>(v, y, ya, kz, kza, dl.oS, score, yS, sigma, copy_anchor, halp, lam, a);
     float *kty = v.kty + slot * v.skty;
     kty[(int64_t)v.F * v.NP + v.NP] = (float)y[dl.oS];
@@ -1227,6 +1431,18 @@ __global__ __launch_bounds__(256) void scalar_pass(DeviceView v, const int32_t *
 #pragma unroll
     for (int q = 0; q < kNLam; ++q)
       if (isfinite(gmin[q][0])) lagr = fmax(lagr, a.lagr + tot[NTS + BS_LK0 + q] + gmin[q][0]);
+  }
+  // ... and the same bound at the repaired duals (DESIGN.md §4 "Dual repair"): the larger one stands
+  {
+    double lr = tot[TS_LAGR_REP] + tot[NTS + BS_LAGR_REP];
+    if (v.step2) {
+      double best = -INFINITY;
+#pragma unroll
+      for (int q = 0; q < kNLam; ++q)
+        if (isfinite(gmin[q][0])) best = fmax(best, tot[NTS + BS_LKR0 + q] + gmin[q][0]);
+      lr += score_lagr + best;
+    }
+    if (lr > lagr) lagr = lr;
   }
   const double gap = pobj - lagr;
   const double tol = v.prm[0], cutoff = v.prm[1], gap_tol = v.prm[2];
@@ -1431,7 +1647,7 @@ static hipError_t launch_x_tw(const DeviceView &v, const int32_t *slots, int nsl
                               bool first, bool plain, int it, hipStream_t s) {
   dim3 grid(8 * ((v.F * nslots + 7) / 8)), block(kWave * TW);
   const size_t lds = (size_t)(2 * TW + 2) * v.NP * sizeof(float) +
-                    (check ? (size_t)2 * TW * v.NP * sizeof(float) + 2 * v.NP * sizeof(double) : 0);
+                    (check ? (size_t)2 * TW * v.NP * sizeof(float) + 4 * v.NP * sizeof(double) : 0);
   const int pl = plain ? 1 : 0;
   // non-temporal routing streams only when the iterating slots' x + anchor exceed ~160 MB (see ld_x4)
   const int nt = (double)nslots * 2.0 * (double)v.sx * sizeof(float) > 160e6 ? 1 : 0;
@@ -1452,8 +1668,8 @@ static hipError_t launch_x_tw(const DeviceView &v, const int32_t *slots, int nsl
 static int tile_waves(const DeviceView &v, int nslots) {
   int tw = 4;
   while (tw < 16 && (int64_t)nslots * v.F * tw < 4096) tw *= 2;
-  // LDS of the certificate variant: fp64 column sums + fp32 CPU sums + constants (fp32 and fp64)
-  while (tw > 4 && (size_t)(4 * tw + 2) * v.NP * sizeof(float) + 2 * v.NP * sizeof(double) > 144 * 1024) tw /= 2;
+  // LDS of the certificate variant: fp64 column / CPU sums + constants (fp32, fp64, repaired prices, pooled flow)
+  while (tw > 4 && (size_t)(4 * tw + 2) * v.NP * sizeof(float) + 4 * v.NP * sizeof(double) > 144 * 1024) tw /= 2;
   return tw;
 }
 
@@ -1486,11 +1702,6 @@ hipError_t launch_node_pass(const DeviceView &v, const int32_t *slots, int nslot
   if (init) hipLaunchKernelGGL((node_pass<false, true>), grid, block, 0, s, v, slots, fi, pl, it);
   else if (check) hipLaunchKernelGGL((node_pass<true, false>), grid, block, 0, s, v, slots, fi, pl, it);
   else hipLaunchKernelGGL((node_pass<false, false>), grid, block, 0, s, v, slots, fi, pl, it);
-  return hipGetLastError();
-}
-
-hipError_t launch_dblock_pass(const DeviceView &v, const int32_t *slots, int nslots, hipStream_t s) {
-  hipLaunchKernelGGL(dblock_pass, dim3(v.F, nslots), dim3(256), 0, s, v, slots);
   return hipGetLastError();
 }
 

@@ -3,6 +3,7 @@ the reference's model restated as one CSR (oracle/formulation.py).  Lets the CPU
 product's branch-and-bound (core/engine/bnb.py) and step orchestration (core/solvers) without a
 GPU.  Routing rows are the literal per-(f, i) rows (no zero-workload pooling)."""
 import math
+import zlib
 
 import numpy as np
 
@@ -21,6 +22,7 @@ class OracleLP:
         prev_x = getattr(data, "prev_x", None)
         if prev_x is None or not np.size(prev_x):
             prev_x = np.zeros((self.N, self.F, self.N))
+        prev_x = np.asarray(prev_x, np.float64)
         self.m = build_model(data, variant, step=1 if self.step == 1 else 2,
                              mode="delete" if self.step == 2 else "create", alpha=alpha,
                              soften_step1_sol=soften_step1_sol, max_score=max_score, prev_x=prev_x)
@@ -128,5 +130,64 @@ class OracleLP:
         xd = x[:self.nx].reshape(self.F, self.N, self.N).transpose(1, 0, 2).astype(np.float32) if dense_x else None
         return z, xd
 
+    def routing(self, slot):
+        from core.engine.routing import SparseRouting
+        return SparseRouting.from_dense(self.solution(slot, dense_x=True)[1])
+
+    def routing_from_entries(self, row, dst, val):
+        from core.engine.routing import SparseRouting
+        N, F = self.N, self.F
+        return SparseRouting(N, F, np.repeat(np.arange(F), N), np.tile(np.arange(N), F), np.ones((F, N)), row, dst,
+                             val)
+
     def close(self):
         self._sol = {}
+
+
+class StreamingOracleLP(OracleLP):
+    """OracleLP whose node LPs finish after a deterministic, node-dependent number of blocks (1-3
+    advance() rounds, from a hash of the node box), so the branch-and-bound's streaming path sees LPs
+    finish out of submission order as on the engine; and whose polish re-solve (tol <= 1e-8) reports
+    a primal objective slightly ABOVE the certified one (the engine's polished value can land above
+    the pre-polish incumbent: round-2 ADVICE)."""
+
+    def submit(self, slots, lb=None, ub=None, tol=1e-7, cutoff=math.inf, max_iters=0, check_every=64,
+               warm_start=False, warm_omega_floor=0.0):
+        slots = np.asarray(slots).reshape(-1)
+        self._cutoff = cutoff
+        r = self.solve(slots, lb, ub, tol=tol, cutoff=math.inf)
+        if not hasattr(self, "_pend"):
+            self._pend = {}
+        st = np.zeros(len(slots), np.int32)
+        for b, s in enumerate(slots):
+            if int(r["status"][b]) == LP_INFEASIBLE:
+                st[b] = LP_INFEASIBLE
+                continue
+            st[b] = LP_ITERATION_LIMIT
+            key = np.concatenate([np.nan_to_num(lb[b], posinf=7, neginf=-7), np.nan_to_num(ub[b], posinf=7, neginf=-7)]) \
+                if lb is not None else np.zeros(1)
+            blocks = 1 + zlib.crc32(key.tobytes()) % 3   # deterministic across ranks
+            obj = float(r["obj"][b])
+            pobj = obj + (1e-9 * max(1.0, abs(obj)) if tol <= 1e-8 else 0.0)
+            self._pend[int(s)] = [blocks, obj, pobj]
+        return st
+
+    def active(self):
+        return len(getattr(self, "_pend", {}))
+
+    def advance(self, min_done=1):
+        pend = getattr(self, "_pend", {})
+        done = []
+        while pend:
+            for s in sorted(pend):
+                pend[s][0] -= 1
+            fin = sorted(s for s in pend if pend[s][0] <= 0)
+            done += [(s, pend.pop(s)) for s in fin]
+            if min_done <= 0 or len(done) >= min_done:
+                break
+        cut = getattr(self, "_cutoff", math.inf)
+        obj = np.array([v[1] for _, v in done])
+        st = np.array([LP_CUTOFF if v[1] > cut else LP_OPTIMAL for _, v in done], np.int32)
+        return {"slots": np.array([s for s, _ in done], np.int32), "obj": obj,
+                "primal_obj": np.array([v[2] for _, v in done]), "status": st,
+                "iters": np.full(len(done), 12, np.int64)}

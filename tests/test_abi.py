@@ -100,7 +100,11 @@ def test_node_presolve_incremental_equals_full(name, k):
 def test_request_unknown_solver_type_raises():
     """core.request resolves solver.type through the SOLVERS whitelist (the reference: eval, main.py:44);
     an unknown type raises before any engine call (the reference's server answers HTTP 500)."""
+    import copy
     import pytest
     from core.request import solve_request
+    from golden_util import payload
+    p = copy.deepcopy(payload("payload"))
+    p["solver"] = {"type": "NotASolver"}
     with pytest.raises(KeyError):
-        solve_request({"solver": {"type": "NotASolver"}})
+        solve_request(p)

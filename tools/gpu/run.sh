@@ -1,0 +1,51 @@
+#!/bin/bash
+# The GPU-box measurement recipes, parameterised (replaces the one-off round-2 call scripts; the index
+# of what each past call measured is tools/gpu/README.md).  Run from this container as
+#   /usr/local/graft/bin/gpurun --timeout 900 -- bash tools/gpu/run.sh <out-name> <recipe> [<recipe> ...]
+# Outputs go to gpurun_out/<out-name>/.  Every GPU step runs under its own time limit; the first failing
+# step ends the call (no retries, nothing after a fault).  Recipes:
+#   tests          python -m pytest tests -m gpu (all GPU tests, -x, per-test timeout)
+#   tests:<files>  the GPU tests of the given comma-separated test files only
+#   smoke          __graft_entry__.smoke()
+#   bench          python bench.py (defaults: CPU baseline + product B&B sections included)
+#   bench:<args>   python bench.py <args, comma-separated> (e.g. bench:--seed,1,--cpu-budget,0)
+#   profile        rocprofv3 --kernel-trace --stats over an 8-step bench -> kernel_stats_by_slots.csv
+#   traffic        separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over tools/traffic.py -> traffic.json
+#   sq             SQ wave / wait / VALU counters of the steady x_pass -> sq.json
+#   probe:<args>   tools/step2_probe.py <args, comma-separated>
+#   py:<script>    python tools/<script> (a dev probe)
+set -u
+cd "$GRAFT_REPO_ROOT"
+export TMPDIR=/tmp
+O=gpurun_out/$1; shift; mkdir -p "$O"
+step() {   # step <name> <seconds> <command...>: run, log, stop the call on failure
+  local name=$1 secs=$2; shift 2
+  echo "== $name: $*"
+  timeout -k 10 "$secs" "$@" > "$O/$name.log" 2>&1
+  local rc=$?
+  echo "   rc=$rc"; grep -v "amdgpu\|Initializ" "$O/$name.log" | tail -25
+  [ $rc -eq 0 ] || exit $rc
+}
+for r in "$@"; do
+  case $r in
+    tests) step pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ;;
+    tests:*) a=${r#tests:}; step pytest_sel 900 python -u -m pytest ${a//,/ } -m gpu -v -s --timeout 300 --timeout-method thread ;;
+    smoke) step smoke 240 python -u -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) step bench 600 python -u bench.py ; grep "^{" "$O/bench.log" | tail -1 > "$O/bench.json" ;;
+    bench:*) a=${r#bench:}; step bench_args 600 python -u bench.py ${a//,/ } ; grep "^{" "$O/bench_args.log" | tail -1 > "$O/bench_args.json" ;;
+    profile)
+      step profile 300 rocprofv3 --kernel-trace --stats -d /tmp/prof -o run -- python3 bench.py --steps 8 --cpu-budget 0 --bnb-seconds 0
+      python3 tools/prof_summary.py /tmp/prof > "$O/kernel_stats_by_slots.csv"; cp /tmp/prof/*/*stats.csv "$O/" 2>/dev/null
+      head -12 "$O/kernel_stats_by_slots.csv" | cut -c1-160 ;;
+    traffic)
+      step pmc_fetch 120 rocprofv3 --pmc FETCH_SIZE -d /tmp/pmc_fetch -o run -- python3 tools/traffic.py run
+      step pmc_write 120 rocprofv3 --pmc WRITE_SIZE -d /tmp/pmc_write -o run -- python3 tools/traffic.py run
+      python3 tools/traffic.py summarize /tmp/pmc_fetch /tmp/pmc_write > "$O/traffic.json"; cat "$O/traffic.json" ;;
+    sq)
+      step pmc_sq 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU -d /tmp/pmc_sq -o run -- python3 tools/traffic.py run
+      python3 tools/traffic.py sq /tmp/pmc_sq > "$O/sq.json"; cat "$O/sq.json" ;;
+    probe:*) a=${r#probe:}; step probe 600 python -u tools/step2_probe.py ${a//,/ } ;;
+    py:*) a=${r#py:}; step "py_${a%%.py*}" 600 python -u tools/${a//,/ } ;;
+    *) echo "unknown recipe $r"; exit 2 ;;
+  esac
+done
