@@ -69,6 +69,7 @@ class BnBResult:
         self.seconds = 0.0
         self.incumbent_slot = None
         self.polished = False    # the incumbent's LP was re-solved at the polish tolerance
+        self.repaired = None     # the CPU repair of the returned routing succeeded (None: not run)
         # node-LP mix: finished LPs per engine status (+ presolve-infeasible submits) and their iterations
         self.lp_status = {"certified": 0, "limit": 0, "infeasible": 0, "cutoff": 0, "numerical": 0,
                           "presolve_infeasible": 0}
@@ -76,7 +77,8 @@ class BnBResult:
 
     def as_dict(self):
         d = {k: getattr(self, k) for k in ("status", "objective", "bound", "nodes", "leaves", "lps", "certified",
-                                           "lp_iterations", "unresolved", "seconds", "polished", "lp_status")}
+                                           "lp_iterations", "unresolved", "seconds", "polished", "repaired",
+                                           "lp_status")}
         it = np.asarray(self.lp_iters, np.float64)
         d["lp_iters_p50_p90_p99_max"] = ([float(v) for v in np.percentile(it, [50, 90, 99, 100])] if it.size else None)
         return d
@@ -102,7 +104,7 @@ class BranchAndBound:
     def __init__(self, lp, workload, fn_mem, node_mem, batch=16, tol=1e-7, gap=1e-6, max_iters=5000,
                  node_limit=20000, time_limit=None, upper_bound=math.inf, flow_tol=1e-4, log=None, comm=None,
                  warm=True, root_max_iters=200000, check_every=12, polish_tol=1e-8, polish_iters=20000,
-                 seed_leaves=None, integer_bound=None, improve=None):
+                 seed_leaves=None, integer_bound=None, improve=None, repair=None):
         self.lp = lp
         self.N, self.F = lp.N, lp.F
         L = lp.layout()
@@ -129,6 +131,9 @@ class BranchAndBound:
         self.integer_bound = integer_bound
         # improve(idx, val, value) -> [(idx, val)]: neighbour leaves of each new incumbent (local search)
         self.improve = improve
+        # repair(x, z) -> (x', objective change, ok): the returned routing moved within its placement so
+        # it meets the reference checker's absolute CPU tolerance (core.engine.routing.repair_cpu)
+        self.repair = repair
         self.node_limit, self.time_limit = node_limit, time_limit
         self.ub0 = upper_bound
         self.flow_tol = flow_tol
@@ -539,6 +544,12 @@ class BranchAndBound:
         else:
             self._finish_sharded(res, inc, limit_hit, unresolved_below)
             limit_hit, unresolved_below = self._limit_hit, self._unresolved_below
+        if res.objective is not None and self.repair is not None:
+            # identical on every rank (the owner's routing was broadcast)
+            res.x, dobj, res.repaired = self.repair(res.x, res.z)
+            res.objective += dobj
+            if not res.repaired:
+                self.log("incumbent routing: CPU repair incomplete")
         any_unresolved = bool(self.unresolved_bounds) if comm.world == 1 else self._any_unresolved
         if res.objective is None:
             res.status = LIMIT if (limit_hit or any_unresolved) else INFEASIBLE

@@ -80,3 +80,102 @@ class SparseRouting:
         i, f, j, v = self.entries()
         keep = v > threshold
         return i[keep], f[keep], j[keep], np.round(v[keep], 3)
+
+    def cpu_usage(self, W, cpr):
+        """sum_{f,i} W[f,i] cpr[f,j] x[i,f,j] per destination j (constraints_step1.py:57-65), fp64."""
+        W = np.asarray(W, np.float64).reshape(self.F, self.N)
+        cpr = np.asarray(cpr, np.float64).reshape(self.F, self.N)
+        f = self.row_f[self.row]
+        src = self.row_src[self.row]
+        k = src >= 0
+        return np.bincount(self.dst[k], weights=self.val[k] * W[f[k], src[k]] * cpr[f[k], self.dst[k]],
+                           minlength=self.N)
+
+
+def repair_cpu(x, W, cpr, cores, c_open, coef=None, floor=1.0, max_moves=100000):
+    """Make a leaf's routing meet the reference checker's CPU rows at an ABSOLUTE tolerance.
+
+    The engine certifies C5 relative to the row norm; the reference's offline checker
+    (`efttc/utils/constraints_step1.py:68-78`) accepts CPU_j <= cores_j + 1e-6 absolutely, so a
+    certified routing can exceed a large node's cores by up to tol * rownorm (~1e-5).  The repair
+    moves that excess flow of loaded rows (W > 0) from an overloaded destination j to another
+    destination j' the placement opens for the same function (c[f, j'] = 1, so C1 holds) with CPU
+    room, cheapest first by the change of `coef(f, i, j)` per unit of CPU relief; a source's row sum
+    (C4) is unchanged, and j's column sum stays >= `floor` (C2 with c = 1) — every move is checked.
+    Every overloaded node ends at CPU_j <= cores_j (not merely + 1e-6).
+
+    x       SparseRouting of a leaf (every c fixed)
+    c_open  [F, N] bool: the leaf's c
+    coef    coef(f, i, j) -> the per-unit objective (or score-row) coefficient of x[i, f, j]
+            (broadcasting arrays); None: every move costs 0
+    Returns (SparseRouting, sum of t * (coef(j') - coef(j)) over the moves, ok); ok = False when an
+    overloaded node has no admissible move left (the routing is returned as far as repaired)."""
+    F, N = x.F, x.N
+    W = np.asarray(W, np.float64).reshape(F, N)
+    cpr = np.asarray(cpr, np.float64).reshape(F, N)
+    cores = np.asarray(cores, np.float64).reshape(N)
+    c_open = np.asarray(c_open, bool).reshape(F, N)
+    cpu = x.cpu_usage(W, cpr)
+    lim = cores - 1e-12 * np.maximum(1.0, np.abs(cores))
+    over = np.flatnonzero(cpu > cores)
+    if over.size == 0:
+        return x, 0.0, True
+    row, dst, val = x.row.copy(), x.dst.copy(), x.val.copy()
+    f_of, src_of = x.row_f, x.row_src
+    weight = np.array([1.0 if s >= 0 else float(x.zero_src[f].size) for f, s in zip(f_of, src_of)])
+    colsum = np.zeros(F * N)
+    np.add.at(colsum, f_of[row] * N + dst, val * weight[row])
+    where = {(int(r), int(d)): k for k, (r, d) in enumerate(zip(row, dst))}
+    delta, ok, moves = 0.0, True, 0
+    jj = np.arange(N)
+    for j in over:
+        while cpu[j] > lim[j] and moves < max_moves:
+            ks = np.flatnonzero((dst == j) & (val > 0) & (src_of[row] >= 0))
+            if ks.size == 0:
+                ok = False
+                break
+            fk, ik = f_of[row[ks]], src_of[row[ks]]
+            relief = W[fk, ik] * cpr[fk, j]
+            cap_col = np.where(c_open[fk, j], colsum[fk * N + j] - floor, val[ks])
+            cap = np.minimum(val[ks], cap_col)
+            good = (relief > 0) & (cap > 0)
+            if not good.any():
+                ok = False
+                break
+            ks, fk, ik, relief, cap = ks[good], fk[good], ik[good], relief[good], cap[good]
+            # destinations: open for f, not j, with CPU room
+            load = W[fk, ik][:, None] * cpr[fk, :]                       # [K, N] CPU per unit at j'
+            room = (lim - cpu)[None, :]
+            cap_d = np.where(load > 0, np.where(room > 0, room / np.where(load > 0, load, 1.0), 0.0), np.inf)
+            cap2 = np.minimum(cap[:, None], cap_d)
+            adm = c_open[fk, :] & (jj[None, :] != j) & (cap2 > 1e-15)
+            if not adm.any():
+                ok = False
+                break
+            dc = np.zeros((ks.size, N)) if coef is None else \
+                np.asarray(coef(fk[:, None], ik[:, None], jj[None, :]), np.float64) - \
+                np.asarray(coef(fk, ik, np.full(ks.size, j)), np.float64)[:, None]
+            score = np.where(adm, dc / relief[:, None], np.inf)
+            a, jd = np.unravel_index(int(np.argmin(score)), score.shape)
+            t = min(float(cap2[a, jd]), (cpu[j] - lim[j]) / relief[a])
+            k, f, i = int(ks[a]), int(fk[a]), int(ik[a])
+            val[k] -= t
+            key = (int(row[k]), int(jd))
+            if key in where:
+                val[where[key]] += t
+            else:
+                where[key] = len(val)
+                row, dst, val = np.append(row, row[k]), np.append(dst, jd), np.append(val, t)
+            cpu[j] -= t * relief[a]
+            cpu[jd] += t * load[a, jd]
+            colsum[f * N + j] -= t
+            colsum[f * N + jd] += t
+            delta += t * float(dc[a, jd])
+            moves += 1
+        if cpu[j] > lim[j]:
+            ok = False
+    keep = val > 0
+    out = SparseRouting.__new__(SparseRouting)
+    out.N, out.F, out.row_f, out.row_src, out.zero_src = N, F, x.row_f, x.row_src, x.zero_src
+    out.row, out.dst, out.val = row[keep].astype(np.int32), dst[keep].astype(np.int32), val[keep]
+    return out, delta, ok

@@ -20,7 +20,7 @@ import numpy as np
 
 from ...engine import lp as _lp
 from ...engine.bnb import OPTIMAL, BranchAndBound
-from ...engine.routing import SparseRouting
+from ...engine.routing import SparseRouting, repair_cpu
 from ..solver import Solver
 
 
@@ -80,6 +80,30 @@ class NeptuneStepBase(Solver):
         worth solving (a local-search heuristic), or None."""
         return None
 
+    def routing_coef(self):
+        """(objective coefficient of x[i, f, j] as coef(f, i, j), or None when the objective has no
+        routing term; the coefficient the CPU repair should keep low)."""
+        return None, None
+
+    def routing_repair(self, layout):
+        """repair(x, z) -> (x', objective change, ok): the incumbent's routing moved within its placement
+        until every node's CPU meets the reference checker's absolute tolerance
+        (efttc/utils/constraints_step1.py:68-78; core.engine.routing.repair_cpu)."""
+        d = self.data
+        F, N = len(d.functions), len(d.nodes)
+        c0, c1 = layout["c"]
+        obj, pref = self.routing_coef()
+
+        def repair(x, z):
+            c_open = np.asarray(z[c0:c1], np.float64).reshape(F, N) > 0.5
+            x2, dpref, ok = repair_cpu(x, d.workload_matrix, d.core_per_req_matrix, d.node_cores_matrix, c_open,
+                                       coef=pref)
+            dobj = 0.0
+            if obj is not None and x2 is not x:
+                dobj = dpref if obj is pref else _routing_delta(x, x2, obj)
+            return x2, dobj, ok
+        return repair
+
     def solve(self):
         self.init_objective()
         data = self.data
@@ -95,7 +119,7 @@ class NeptuneStepBase(Solver):
                                  time_limit=self.time_limit,
                                  upper_bound=ub * (1 + 1e-6) + 1e-6 if math.isfinite(ub) else ub, log=self.log,
                                  seed_leaves=self.seed_leaves(model.layout()), integer_bound=self.integer_bound(model.layout()),
-                                 improve=self.improve(model.layout()))
+                                 improve=self.improve(model.layout()), repair=self.routing_repair(model.layout()))
             res = bnb.solve()
             layout = model.layout()
         finally:
@@ -129,6 +153,35 @@ def _max_delay_per_source(data):
     return D.max(axis=1)
 
 
+def _mwd(data):
+    """objectives.py:36-43: sum_{f,i} W[f,i] * max{D[i,j'] : D[i,j'] <= maxdelay[f]}, vectorised over the
+    distinct max delays."""
+    W = np.asarray(data.workload_matrix, np.float64)
+    D = np.asarray(data.node_delay_matrix, np.float64)
+    md = np.asarray(data.max_delay_matrix, np.float64)
+    mwd = 0.0
+    for mdv in np.unique(md):
+        best = np.where(D <= mdv, D, -np.inf).max(axis=1)
+        mwd += float((W[md == mdv] * best[None, :]).sum())
+    return mwd
+
+
+def _routing_delta(x0, x1, coef):
+    """sum coef(f, i, j) (x1 - x0) over the loaded rows of two SparseRoutings of one model."""
+    tot = 0.0
+    for x, s in ((x1, 1.0), (x0, -1.0)):
+        f, src = x.row_f[x.row], x.row_src[x.row]
+        k = src >= 0
+        tot += s * float(np.sum(np.asarray(coef(f[k], src[k], x.dst[k]), np.float64) * x.val[k]))
+    return tot
+
+
+def _delay_coef(data, scale):
+    """coef(f, i, j) = scale[f, i] * D[i, j]"""
+    D = np.asarray(data.node_delay_matrix, np.float64)
+    return lambda f, i, j: scale[f, i] * D[i, j]
+
+
 class NeptuneStep1CPUBase(NeptuneStepBase):
     pass
 
@@ -152,6 +205,11 @@ class NeptuneStep1CPUMinDelay(NeptuneStep1CPUBase):
         W = np.asarray(self.data.workload_matrix, np.float64)
         return float((W * _max_delay_per_source(self.data)[None, :]).sum())
 
+    def routing_coef(self):
+        # minimize_network_delay (objectives.py:4-11): D[i, j] W[f, i]
+        c = _delay_coef(self.data, np.asarray(self.data.workload_matrix, np.float64))
+        return c, c
+
 
 class NeptuneStep1CPUMinDelayAndUtilization(NeptuneStep1CPUMinUtilization):
     VARIANT = "MinDelayAndUtilization"
@@ -170,16 +228,22 @@ class NeptuneStep1CPUMinDelayAndUtilization(NeptuneStep1CPUMinUtilization):
     def upper_bound(self):
         W = np.asarray(self.data.workload_matrix, np.float64)
         D = np.asarray(self.data.node_delay_matrix, np.float64)
-        md = np.asarray(self.data.max_delay_matrix, np.float64)
         ub = float(self.alpha)
         if W.sum():
-            mwd = 0.0                     # objectives.py:36-43, vectorised over the distinct max delays
-            for mdv in np.unique(md):
-                best = np.where(D <= mdv, D, -np.inf).max(axis=1)
-                mwd += float((W[md == mdv] * best[None, :]).sum())
+            mwd = _mwd(self.data)
             if mwd > 0:
                 ub += (1 - self.alpha) * float((W * D.max(axis=1)[None, :]).sum()) / mwd
         return ub
+
+    def routing_coef(self):
+        # minimize_node_delay_and_utilization (objectives.py:30-53): (1 - alpha) W[f, i] D[i, j] / MWD, no x
+        # terms when sum W = 0
+        W = np.asarray(self.data.workload_matrix, np.float64)
+        mwd = _mwd(self.data) if W.sum() else 0.0
+        if mwd <= 0:
+            return None, None
+        c = _delay_coef(self.data, (1 - self.alpha) * W / mwd)
+        return c, c
 
 
 class NeptuneStep2Base(NeptuneStepBase):
@@ -365,6 +429,20 @@ class NeptuneStep2Base(NeptuneStepBase):
                 out.append((np.concatenate(ids), np.concatenate(vs)))
             return out
         return neighbours
+
+    def routing_coef(self):
+        # minimize_disruption (objectives.py:55-63) has no routing term; moves prefer lowering the score
+        # row: D6 (MinDelay, constraints_step2.py:57-69) D[i, j] W[f, i], D7 (MinDelayAndUtilization, :76-88)
+        # (1 - alpha) W[f, i] D[i, j] / max(maxdelay[f], max_k D[k, i]); MinUtilization's D5 has no x
+        d = self.data
+        W = np.asarray(d.workload_matrix, np.float64)
+        if self.VARIANT == "MinDelay":
+            return None, _delay_coef(d, W)
+        if self.VARIANT == "MinDelayAndUtilization":
+            D = np.asarray(d.node_delay_matrix, np.float64)
+            md = np.maximum(np.asarray(d.max_delay_matrix, np.float64)[:, None], D.max(axis=0)[None, :])   # [f, i]
+            return None, _delay_coef(d, (1 - self.alpha) * W / md)
+        return None, None
 
     def results(self):
         # neptune_step2.py:43-51: no side effects on data (the prints are logs only)
