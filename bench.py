@@ -262,7 +262,11 @@ def bnb_section(a, rank, world, dev, N, F):
     return {"workload": f"synthetic_{N}x{F}_step1_MDU_product_bnb", "time_limit_s": a.bnb_seconds,
             "status": res.status, "wall_s": wall, "nodes": res.nodes, "leaves": res.leaves, "lps": res.lps,
             "certified_lps": res.certified, "certified_lp_per_s": res.certified / wall, "nodes_per_s": res.nodes / wall,
-            "certified_share": res.certified / max(1, finished), "lp_status_rank0": res.lp_status,
+            "certified_share": res.certified / max(1, finished),
+            "resolved_lps": d["resolved"], "resolved_lp_per_s": d["resolved"] / wall,
+            "resolved_share": d["resolved"] / max(1, res.lps),
+            "lp_status_rank0": res.lp_status, "lp_status_by_kind_rank0": res.lp_status_kind,
+            "drained_at_stop": res.drained,
             "lp_iters_p50_p90_p99_max_rank0": d["lp_iters_p50_p90_p99_max"],
             "lp_iterations": res.lp_iterations, "incumbent": inc, "bound": res.bound, "rel_gap": gap,
             "ranks": world}

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define NEP_API_VERSION 5
+#define NEP_API_VERSION 6
 
 /* variants: neptune.py:41-66 (NeptuneMinDelay / MinUtilization / MinDelayAndUtilization) */
 enum { NEP_MIN_DELAY = 0, NEP_MIN_UTILIZATION = 1, NEP_MIN_DELAY_AND_UTILIZATION = 2 };
@@ -47,7 +47,11 @@ enum {
   NEP_LP_ITERATION_LIMIT = 1,  /* obj still holds a VALID lower bound (Lagrangian) */
   NEP_LP_INFEASIBLE = 2,       /* proven by presolve (empty routing row, crossed bounds, row activity) */
   NEP_LP_CUTOFF = 3,           /* Lagrangian bound exceeded opts.cutoff: node can be pruned */
-  NEP_LP_NUMERICAL = 4
+  NEP_LP_NUMERICAL = 4,
+  NEP_LP_BOUND = 5             /* API 6, opts.bound_res > 0 only: the bound has converged (within gap_tol of
+                                  the repaired point's objective, whose residual is <= bound_res) but the
+                                  point is not certified feasible at tol; obj = the VALID Lagrangian bound.
+                                  For B&B nodes that branch on the bound (not incumbents) */
 };
 
 typedef struct {
@@ -88,6 +92,9 @@ typedef struct {
   double polish_after;         /* API 5: primal feasibility polishing may start after this many
                                   iterations (0: default — 256 for warm starts, never for cold starts;
                                   < 0: never).  DESIGN.md §4 "Polishing" */
+  double bound_res;            /* API 6: > 0: an LP whose bound has converged (gap <= gap_tol) while its
+                                  repaired point's residual is within bound_res stops with NEP_LP_BOUND
+                                  (0: never; a B&B sets it on branching nodes, never on leaves) */
 } nep_lp_opts;
 
 typedef struct {

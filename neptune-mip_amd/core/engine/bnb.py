@@ -42,12 +42,13 @@ from collections import deque
 import numpy as np
 
 from .comm import LocalComm
-from .lp import LP_CUTOFF, LP_INFEASIBLE, LP_ITERATION_LIMIT, LP_OPTIMAL
+from .lp import LP_BOUND, LP_CUTOFF, LP_INFEASIBLE, LP_ITERATION_LIMIT, LP_OPTIMAL
 
 OPTIMAL, INFEASIBLE, LIMIT = "OPTIMAL", "INFEASIBLE", "LIMIT"
 _STATUS_NAME = {LP_OPTIMAL: "certified", LP_ITERATION_LIMIT: "limit", LP_INFEASIBLE: "infeasible",
-                LP_CUTOFF: "cutoff"}
+                LP_CUTOFF: "cutoff", LP_BOUND: "bound"}
 NODE, LEAF, RETRY = 0, 1, 2
+_KIND_NAME = {NODE: "node", LEAF: "leaf", RETRY: "retry"}
 
 
 class BnBResult:
@@ -71,14 +72,20 @@ class BnBResult:
         self.polished = False    # the incumbent's LP was re-solved at the polish tolerance
         self.repaired = None     # the CPU repair of the returned routing succeeded (None: not run)
         # node-LP mix: finished LPs per engine status (+ presolve-infeasible submits) and their iterations
-        self.lp_status = {"certified": 0, "limit": 0, "infeasible": 0, "cutoff": 0, "numerical": 0,
+        self.lp_status = {"certified": 0, "bound": 0, "limit": 0, "infeasible": 0, "cutoff": 0, "numerical": 0,
                           "presolve_infeasible": 0}
+        self.lp_status_kind = {k: dict.fromkeys(self.lp_status, 0) for k in ("node", "leaf", "retry")}
         self.lp_iters = []
+        self.drained = 0         # LPs still iterating at a stop decision (stopped at their next check)
+        # wall seconds by phase: device waits in advance, host work per finished LP, submits (incl.
+        # warm-start copies), the drain after a stop, the end (routing fetch, polish, repair)
+        self.timing = dict.fromkeys(("advance", "finish", "submit", "drain", "end"), 0.0)
 
     def as_dict(self):
         d = {k: getattr(self, k) for k in ("status", "objective", "bound", "nodes", "leaves", "lps", "certified",
                                            "lp_iterations", "unresolved", "seconds", "polished", "repaired",
-                                           "lp_status")}
+                                           "lp_status", "lp_status_kind", "drained", "timing")}
+        d["resolved"] = sum(v for k, v in self.lp_status.items() if k not in ("limit", "numerical"))
         it = np.asarray(self.lp_iters, np.float64)
         d["lp_iters_p50_p90_p99_max"] = ([float(v) for v in np.percentile(it, [50, 90, 99, 100])] if it.size else None)
         return d
@@ -104,7 +111,8 @@ class BranchAndBound:
     def __init__(self, lp, workload, fn_mem, node_mem, batch=16, tol=1e-7, gap=1e-6, max_iters=5000,
                  node_limit=20000, time_limit=None, upper_bound=math.inf, flow_tol=1e-4, log=None, comm=None,
                  warm=True, root_max_iters=200000, check_every=12, polish_tol=1e-8, polish_iters=20000,
-                 seed_leaves=None, integer_bound=None, improve=None, repair=None):
+                 seed_leaves=None, integer_bound=None, improve=None, repair=None, node_bound_res=1e-2,
+                 retry_res=1e-2):
         self.lp = lp
         self.N, self.F = lp.N, lp.F
         L = lp.layout()
@@ -134,6 +142,14 @@ class BranchAndBound:
         # repair(x, z) -> (x', objective change, ok): the returned routing moved within its placement so
         # it meets the reference checker's absolute CPU tolerance (core.engine.routing.repair_cpu)
         self.repair = repair
+        # branching nodes (not leaves, not the root) stop once their bound has converged, with the repaired
+        # point's residual <= node_bound_res (engine status LP_BOUND): a node branches on its bound, which
+        # is valid at any dual point, so it need not iterate on to primal feasibility at tol (0: off)
+        self.node_bound_res = node_bound_res
+        # an uncertified leaf is re-solved with the root budget only when its repaired point's residual
+        # at the node-LP limit is <= retry_res (a leaf the rounding made CPU-infeasible ends far above it
+        # and would burn the root budget); otherwise its bound stays as an unresolved one
+        self.retry_res = retry_res
         self.node_limit, self.time_limit = node_limit, time_limit
         self.ub0 = upper_bound
         self.flow_tol = flow_tol
@@ -185,28 +201,69 @@ class BranchAndBound:
         fl = flow.ravel().astype(np.float64)
         closed = (fixed >= 0) | (np.repeat(nfix[None, :] == 0.0, F, axis=0).ravel())
         zc = np.zeros(F * N) if zc is None else np.asarray(zc, np.float64).ravel()
+        usedl, rooml, fmem = used.tolist(), room.tolist(), self.fn_mem.tolist()
+
+        def open_in_order(ks):
+            """Greedy first-fit of the candidates ks (flat (f, j), in priority order) into the node memories.
+            A destination's decisions depend only on its own earlier ones, so every destination whose
+            candidates all fit is decided at once (prefix sums); only the few that fill up are walked."""
+            if ks.size == 0:
+                return
+            fj, jj = np.divmod(ks, N)
+            o = np.argsort(jj, kind="stable")
+            js, ks_o = jj[o], ks[o]
+            ms = self.fn_mem[fj[o]]
+            cs = np.cumsum(ms)
+            start = np.flatnonzero(np.r_[True, js[1:] != js[:-1]])
+            base = np.repeat(cs[start] - ms[start], np.diff(np.r_[start, len(js)]))
+            avail = np.asarray(rooml)[js] - np.asarray(usedl)[js]
+            fits = (cs - base) <= avail
+            seg_ok = np.logical_and.reduceat(fits, start)
+            okm = np.repeat(seg_ok, np.diff(np.r_[start, len(js)]))
+            opened = ks_o[okm].tolist()
+            np.add.at(used_acc := np.zeros(N), js[okm], ms[okm])
+            for j, u in zip(np.flatnonzero(used_acc).tolist(), used_acc[used_acc > 0].tolist()):
+                usedl[j] += u
+            for s0, e0 in zip(start[~seg_ok].tolist(), (np.r_[start, len(js)][1:][~seg_ok]).tolist()):
+                j = int(js[s0])
+                seg_k, seg_m = ks_o[s0:e0].tolist(), ms[s0:e0]
+                tail_min = np.minimum.accumulate(seg_m[::-1])[::-1].tolist()   # smallest memory still to come
+                for q, (k, mq) in enumerate(zip(seg_k, seg_m.tolist())):
+                    left = rooml[j] - usedl[j]
+                    if left < tail_min[q]:
+                        break                                                # nothing left fits here
+                    if mq <= left:
+                        opened.append(k)
+                        usedl[j] += mq
+            c[opened] = 1.0
+
         half = np.flatnonzero(~closed & (zc >= 0.5))
-        for k in half[np.argsort(-zc[half], kind="stable")]:
-            f, j = divmod(int(k), N)
-            if used[j] + self.fn_mem[f] <= room[j]:
-                c[k] = 1.0
-                used[j] += self.fn_mem[f]
-        cand = np.flatnonzero(~closed & (c < 0.5) & (fl > self.flow_tol)) if by_flow else np.zeros(0, np.int64)
-        for k in cand[np.argsort(-fl[cand], kind="stable")]:
-            f, j = divmod(int(k), N)
-            if used[j] + self.fn_mem[f] <= room[j]:
-                c[k] = 1.0
-                used[j] += self.fn_mem[f]
-        for f in np.flatnonzero(cm.sum(axis=1) < 1):
-            order = np.lexsort((-fl[f * N:(f + 1) * N], -zc[f * N:(f + 1) * N]))
-            for j in order:
-                k = f * N + int(j)
-                if not closed[k] and used[j] + self.fn_mem[f] <= room[j]:
-                    c[k] = 1.0
-                    used[j] += self.fn_mem[f]
-                    break
-            else:
-                return None
+        open_in_order(half[np.argsort(-zc[half], kind="stable")])
+        if by_flow:
+            cand = np.flatnonzero(~closed & (c < 0.5) & (fl > self.flow_tol))
+            open_in_order(cand[np.argsort(-fl[cand], kind="stable")])
+        need = np.flatnonzero(cm.sum(axis=1) < 1)
+        if need.size:
+            # each function left without a destination: the open-able destination with the largest LP c,
+            # then flow (lowest index on ties), or the next one in that order that still has room
+            ZC, FL, CL = zc.reshape(F, N)[need], fl.reshape(F, N)[need], closed.reshape(F, N)[need]
+            zcm = np.where(CL, -np.inf, ZC)
+            top = zcm.max(axis=1)
+            first = np.where(CL | (zcm < top[:, None]), -np.inf, FL).argmax(axis=1).tolist()
+            opened = []
+            for r, f in enumerate(need.tolist()):
+                if top[r] == -np.inf:
+                    return None
+                j = first[r]
+                if usedl[j] + fmem[f] > rooml[j]:
+                    order = np.lexsort((-FL[r], -ZC[r]))
+                    j = next((jj for jj in order[~CL[r][order]].tolist() if usedl[jj] + fmem[f] <= rooml[jj]), None)
+                    if j is None:
+                        return None
+                opened.append(f * N + j)
+                usedl[j] += fmem[f]
+            c[opened] = 1.0
+        used = np.asarray(usedl)
         idx = [np.arange(c0, c1)]
         val = [c]
         if self.n_range is not None:
@@ -266,7 +323,8 @@ class BranchAndBound:
                     copies.append((src, slot))
                 warm = True
             budget = self.root_max_iters if (node.kind == RETRY or not self.root_ready) else self.max_iters
-            groups.setdefault((warm, budget), []).append((slot, node))
+            bres = self.node_bound_res if (node.kind == NODE and self.root_ready) else 0.0
+            groups.setdefault((warm, budget, bres), []).append((slot, node))
         # warm-start copies: a slot that is both a parent state (source) and a new node's slot
         # (destination) is read before it is overwritten; a cycle falls back to the root's state
         while copies:
@@ -279,7 +337,7 @@ class BranchAndBound:
             src, dst = copies.pop(k)
             lp.copy_state(src, dst)
         cutoff = min(inc, self.ub0)
-        for (warm, budget), its in groups.items():
+        for (warm, budget, bres), its in groups.items():
             slots = np.array([s for s, _ in its], np.int32)
             lb = np.full((len(its), n_int), -np.inf)
             ub = np.full((len(its), n_int), np.inf)
@@ -287,12 +345,13 @@ class BranchAndBound:
                 lb[b, node.idx] = node.val
                 ub[b, node.idx] = node.val
             st = lp.submit(slots, lb, ub, tol=self.tol, cutoff=cutoff if math.isfinite(cutoff) else math.inf,
-                           max_iters=budget, check_every=self.check_every, warm_start=warm)
+                           max_iters=budget, check_every=self.check_every, warm_start=warm, bound_res=bres)
             for b, (slot, node) in enumerate(its):
                 self.slot_gen[slot] += 1
                 self.res.lps += 1
                 if int(st[b]) == LP_INFEASIBLE:
                     self.res.lp_status["presolve_infeasible"] += 1
+                    self.res.lp_status_kind[_KIND_NAME[node.kind]]["presolve_infeasible"] += 1
                     self.free.append(slot)
                 else:
                     self.inflight[slot] = node
@@ -303,6 +362,7 @@ class BranchAndBound:
         res.lp_iterations += iters
         res.lp_iters.append(iters)
         res.lp_status[_STATUS_NAME.get(st, "numerical")] += 1
+        res.lp_status_kind[_KIND_NAME[node.kind]][_STATUS_NAME.get(st, "numerical")] += 1
         if st == LP_OPTIMAL:
             res.certified += 1
         if not self.root_ready and node.depth == 0 and node.kind == NODE:
@@ -350,7 +410,7 @@ class BranchAndBound:
                                 self.pending.appendleft(_Node(self._ibound(idx, val), idx,
                                                               np.asarray(val, np.float64), LEAF, (slot, self.slot_gen[slot]),
                                                               node.depth))
-            elif node.kind == LEAF:
+            elif node.kind == LEAF and self.lp.diag(slot)["pres"] <= self.retry_res:
                 self.retry.append(_Node(bound, node.idx, node.val, RETRY, (slot, self.slot_gen[slot]), node.depth))
             else:
                 res.unresolved += 1
@@ -512,24 +572,40 @@ class BranchAndBound:
                 items.append((self.free.popleft(), node))
                 if not self.root_ready:
                     break                 # the root runs alone (its state warm-starts everything after)
+            tm = res.timing
+            t1 = time.perf_counter()
             if items:
                 self._submit(items, inc)
+            t2 = time.perf_counter()
+            tm["submit"] += t2 - t1
             if not self.inflight:
                 continue
-            # before the frontier is dealt every rank must stay identical: drain each batch whole
-            r = lp.advance(1 if sharded else len(self.inflight))
+            # before the frontier is dealt every rank must stay identical: drain each batch whole.  Under a
+            # time limit the sharded loop comes back after every block, so a stop is never held up by
+            # long LPs (a leaf's retry runs the root budget)
+            r = lp.advance((0 if self.time_limit else 1) if sharded else len(self.inflight))
+            t3 = time.perf_counter()
+            tm["advance"] += t3 - t2
             for i, slot in enumerate(r["slots"].tolist()):
                 node = self.inflight.pop(slot)
                 inc = self._finish(slot, node, int(r["status"][i]), float(r["obj"][i]), float(r["primal_obj"][i]),
                                    int(r["iters"][i]), inc)
-        # drain what still iterates (a stop decision): their bounds stay valid
+            tm["finish"] += time.perf_counter() - t3
+        # drain what still iterates (a stop decision): a cutoff of -inf stops every LP in flight at its next
+        # certificate check (one block), with its best Lagrangian bound, which stays valid for its node
+        t_end = time.perf_counter()
         open_bounds = [n.bound for n in self.inflight.values()]
+        res.drained = len(self.inflight)
+        if lp.active() > 0:
+            lp.set_params(self.tol, -math.inf)
         while lp.active() > 0:
             r = lp.advance(lp.active())
             for i, slot in enumerate(r["slots"].tolist()):
                 node = self.inflight.pop(slot, None)
-                if node is not None and int(r["status"][i]) not in (LP_INFEASIBLE, LP_CUTOFF):
+                if node is not None and int(r["status"][i]) != LP_INFEASIBLE:
                     open_bounds.append(max(node.bound, float(r["obj"][i])))
+        res.timing["drain"] = time.perf_counter() - t_end
+        t_end = time.perf_counter()
         open_bounds += [h[0] for h in self.heap] + [n.bound for n in self.pending] + [n.bound for n in self.retry]
         open_bounds += self.unresolved_bounds
         res.bound = min(open_bounds + [inc])
@@ -555,5 +631,6 @@ class BranchAndBound:
             res.status = LIMIT if (limit_hit or any_unresolved) else INFEASIBLE
         else:
             res.status = LIMIT if (limit_hit or unresolved_below) else OPTIMAL
+        res.timing["end"] = time.perf_counter() - t_end
         res.seconds = time.time() - t0
         return res

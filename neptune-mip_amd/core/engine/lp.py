@@ -15,10 +15,10 @@ LIB_PATH = os.environ.get("NEPTUNE_LP_LIB",
 
 MIN_DELAY, MIN_UTILIZATION, MIN_DELAY_AND_UTILIZATION = 0, 1, 2
 STEP1, STEP2_DELETE, STEP2_CREATE = 1, 2, 3
-LP_OPTIMAL, LP_ITERATION_LIMIT, LP_INFEASIBLE, LP_CUTOFF, LP_NUMERICAL = 0, 1, 2, 3, 4
+LP_OPTIMAL, LP_ITERATION_LIMIT, LP_INFEASIBLE, LP_CUTOFF, LP_NUMERICAL, LP_BOUND = 0, 1, 2, 3, 4, 5
 VARIANTS = {"MinDelay": MIN_DELAY, "MinUtilization": MIN_UTILIZATION,
             "MinDelayAndUtilization": MIN_DELAY_AND_UTILIZATION}
-API_VERSION = 5
+API_VERSION = 6
 
 _dp = ctypes.POINTER(ctypes.c_double)
 
@@ -42,7 +42,7 @@ class LpOpts(ctypes.Structure):
                 ("check_every", ctypes.c_int32), ("warm_start", ctypes.c_int32),
                 ("warm_omega_floor", ctypes.c_double), ("gap_tol", ctypes.c_double),
                 ("warm_omega_cap", ctypes.c_double),
-                ("polish_after", ctypes.c_double)]
+                ("polish_after", ctypes.c_double), ("bound_res", ctypes.c_double)]
 
 
 class ModelInfo(ctypes.Structure):
@@ -225,7 +225,8 @@ class LPModel:
         return lbp, ubp
 
     def solve(self, slots, lb=None, ub=None, tol=1e-7, cutoff=math.inf, max_iters=200000, check_every=64,
-              warm_start=False, warm_omega_floor=0.0, gap_tol=0.0, warm_omega_cap=0.0, polish_after=0.0):
+              warm_start=False, warm_omega_floor=0.0, gap_tol=0.0, warm_omega_cap=0.0, polish_after=0.0,
+              bound_res=0.0):
         """Solve len(slots) node LPs.  lb/ub: [B, n_int] bounds on the integer vector (None = root).
         Returns dict of numpy arrays: obj (certified LP value = Lagrangian bound), primal_obj, status, iters."""
         slots = np.ascontiguousarray(np.asarray(slots, dtype=np.int32).reshape(-1))
@@ -236,7 +237,8 @@ class LPModel:
         status = np.zeros(B, np.int32)
         iters = np.zeros(B, np.int64)
         opts = LpOpts(float(tol), float(cutoff), int(max_iters), int(check_every), 1 if warm_start else 0,
-                      float(warm_omega_floor), float(gap_tol), float(warm_omega_cap), float(polish_after))
+                      float(warm_omega_floor), float(gap_tol), float(warm_omega_cap), float(polish_after),
+                      float(bound_res))
         _check(self._lib, self._lib.nep_lp_solve_batch(
             self._h, B, _ptr(slots, ctypes.c_int32), _ptr(lbp), _ptr(ubp), ctypes.byref(opts), _ptr(obj), _ptr(pobj),
             _ptr(status, ctypes.c_int32), _ptr(iters, ctypes.c_int64)), "nep_lp_solve_batch")
@@ -244,7 +246,8 @@ class LPModel:
 
     # streaming form (nep_lp_submit / nep_lp_advance): a B&B keeps every slot busy
     def submit(self, slots, lb=None, ub=None, tol=1e-7, cutoff=math.inf, max_iters=200000, check_every=64,
-               warm_start=False, warm_omega_floor=0.0, gap_tol=0.0, warm_omega_cap=0.0, polish_after=0.0):
+               warm_start=False, warm_omega_floor=0.0, gap_tol=0.0, warm_omega_cap=0.0, polish_after=0.0,
+              bound_res=0.0):
         """Start node LPs in free slots; returns their presolve status (LP_INFEASIBLE: proven
         infeasible, not started; LP_ITERATION_LIMIT: iterating)."""
         slots = np.ascontiguousarray(np.asarray(slots, dtype=np.int32).reshape(-1))
@@ -252,7 +255,8 @@ class LPModel:
         lbp, ubp = self._bounds(B, lb, ub)
         status = np.zeros(B, np.int32)
         opts = LpOpts(float(tol), float(cutoff), int(max_iters), int(check_every), 1 if warm_start else 0,
-                      float(warm_omega_floor), float(gap_tol), float(warm_omega_cap), float(polish_after))
+                      float(warm_omega_floor), float(gap_tol), float(warm_omega_cap), float(polish_after),
+                      float(bound_res))
         _check(self._lib, self._lib.nep_lp_submit(self._h, B, _ptr(slots, ctypes.c_int32), _ptr(lbp), _ptr(ubp),
                                                   ctypes.byref(opts), _ptr(status, ctypes.c_int32)),
                "nep_lp_submit")

@@ -110,6 +110,11 @@ struct Model {
   // device
   hipStream_t stream = nullptr;
   bool own_stream = false;
+  // auxiliary stream: work on slots that are NOT iterating — the initialisation of newly submitted
+  // slots, warm-start copies and every read of a finished slot (flows, solution, compaction, scorers)
+  // — so none of it queues behind the pipelined block on `stream`; ev_aux orders `stream` after it
+  hipStream_t aux = nullptr;
+  hipEvent_t ev_aux = nullptr;
   DeviceView v{};
   std::vector<void *> allocs;
   double *d_prm = nullptr;      // {tol, cutoff} of the LPs in flight (DeviceView::prm)
@@ -150,12 +155,15 @@ struct Model {
   Ctrl *h_ctrl = nullptr;
   ~Model() {
     if (stream) (void)hipStreamSynchronize(stream);
+    if (aux) (void)hipStreamSynchronize(aux);
     if (h_ctrl) (void)hipHostFree(h_ctrl);
     for (void *p : allocs) (void)hipFree(p);
     for (hipGraphExec_t g : block_graph)
       if (g) (void)hipGraphExecDestroy(g);
     if (ev0) (void)hipEventDestroy(ev0);
     if (ev1) (void)hipEventDestroy(ev1);
+    if (ev_aux) (void)hipEventDestroy(ev_aux);
+    if (aux) (void)hipStreamDestroy(aux);
     if (own_stream && stream) (void)hipStreamDestroy(stream);
   }
 };
@@ -567,6 +575,8 @@ int setup_device(Model &m, int max_batch, void *stream) {
   }
   HIPCHK(hipEventCreate(&m.ev0));
   HIPCHK(hipEventCreate(&m.ev1));
+  HIPCHK(hipStreamCreateWithFlags(&m.aux, hipStreamNonBlocking));
+  HIPCHK(hipEventCreateWithFlags(&m.ev_aux, hipEventDisableTiming));
   DeviceView &v = m.v;
   v.N = m.N; v.NP = m.NP; v.F = m.F; v.R = m.R; v.JB = m.JB; v.CPL = m.CPL;
   v.has_n = m.has_n; v.step2 = m.step2; v.variant = m.variant;
@@ -892,6 +902,7 @@ nep_lp_opts resolve_opts(const nep_lp_opts *opts) {
     o.gap_tol = opts->gap_tol;
     if (opts->warm_omega_cap != 0) o.warm_omega_cap = opts->warm_omega_cap < 0 ? 0.0 : opts->warm_omega_cap;
     o.polish_after = opts->polish_after;
+    o.bound_res = opts->bound_res > 0 ? opts->bound_res : 0.0;
   }
   if (!(o.gap_tol > 0)) o.gap_tol = o.tol;
   // polishing: by default only warm-started LPs (B&B children) polish; a cold LP (a root) iterates on
@@ -920,11 +931,12 @@ int submit(Model &m, int n, const int32_t *slots, const double *lbi, const doubl
   v.warm_omega_cap = o.warm_omega_cap;
   v.polish_after = o.polish_after < 0 ? -1 : (int64_t)o.polish_after;
   v.max_iters = o.max_iters;
+  v.bound_res = o.bound_res;
   // tol / cutoff of every LP in flight: device memory, read by the (graph-replayed) blocks
   m.prm_host[0] = o.tol;
   m.prm_host[1] = o.cutoff;
   m.prm_host[2] = o.gap_tol;
-  HIPCHK(hipMemcpyAsync(m.d_prm, m.prm_host, sizeof(m.prm_host), hipMemcpyHostToDevice, m.stream));
+  HIPCHK(hipMemcpyAsync(m.d_prm, m.prm_host, sizeof(m.prm_host), hipMemcpyHostToDevice, m.aux));
   std::vector<int32_t> fresh, off(1, 0), ci, exact;
   std::vector<double> cl, cu;
   const size_t ni = (size_t)m.il.n_int;
@@ -950,27 +962,33 @@ int submit(Model &m, int n, const int32_t *slots, const double *lbi, const doubl
     off.push_back((int32_t)ci.size());
     max_chg = std::max(max_chg, (int)(ci.size() - c0));
   }
-  if (fresh.empty()) return NEP_OK;
+  if (fresh.empty()) {
+    HIPCHK(hipStreamSynchronize(m.aux));
+    return NEP_OK;
+  }
   const int nf = (int)fresh.size();
   // the node boxes on the device: base box copy + the packed changes scattered over it (a few
   // KB per node instead of the 2 x 8 x n_int bytes of bounds and the F x NP mask)
-  HIPCHK(hipMemcpyAsync(m.d_new, fresh.data(), nf * sizeof(int32_t), hipMemcpyHostToDevice, m.stream));
-  HIPCHK(hipMemcpyAsync(m.d_chg_off, off.data(), off.size() * sizeof(int32_t), hipMemcpyHostToDevice, m.stream));
+  HIPCHK(hipMemcpyAsync(m.d_new, fresh.data(), nf * sizeof(int32_t), hipMemcpyHostToDevice, m.aux));
+  HIPCHK(hipMemcpyAsync(m.d_chg_off, off.data(), off.size() * sizeof(int32_t), hipMemcpyHostToDevice, m.aux));
   if (!ci.empty()) {
-    HIPCHK(hipMemcpyAsync(m.d_chg_idx, ci.data(), ci.size() * sizeof(int32_t), hipMemcpyHostToDevice, m.stream));
-    HIPCHK(hipMemcpyAsync(m.d_chg_lb, cl.data(), cl.size() * sizeof(double), hipMemcpyHostToDevice, m.stream));
-    HIPCHK(hipMemcpyAsync(m.d_chg_ub, cu.data(), cu.size() * sizeof(double), hipMemcpyHostToDevice, m.stream));
+    HIPCHK(hipMemcpyAsync(m.d_chg_idx, ci.data(), ci.size() * sizeof(int32_t), hipMemcpyHostToDevice, m.aux));
+    HIPCHK(hipMemcpyAsync(m.d_chg_lb, cl.data(), cl.size() * sizeof(double), hipMemcpyHostToDevice, m.aux));
+    HIPCHK(hipMemcpyAsync(m.d_chg_ub, cu.data(), cu.size() * sizeof(double), hipMemcpyHostToDevice, m.aux));
   }
   HIPCHK(launch_node_bounds(v, m.d_new, nf, m.d_base_lb, m.d_base_ub, m.d_base_mask, m.d_chg_off, m.d_chg_idx,
-                            m.d_chg_lb, m.d_chg_ub, max_chg, m.stream));
-  HIPCHK(hipMemcpyAsync(m.d_exact, exact.data(), nf * sizeof(int32_t), hipMemcpyHostToDevice, m.stream));
-  HIPCHK(launch_init_slot(v, m.d_new, m.d_exact, nf, o.warm_start != 0, m.eta, m.omega0, m.stream));
-  HIPCHK(launch_x_pass(v, m.d_new, nf, false, true, true, true, 0, m.stream));
-  HIPCHK(launch_node_pass(v, m.d_new, nf, false, true, true, true, 0, m.stream));
-  HIPCHK(launch_scalar_pass(v, m.d_new, nf, false, true, true, true, 0, o.check_every, m.stream));
+                            m.d_chg_lb, m.d_chg_ub, max_chg, m.aux));
+  HIPCHK(hipMemcpyAsync(m.d_exact, exact.data(), nf * sizeof(int32_t), hipMemcpyHostToDevice, m.aux));
+  HIPCHK(launch_init_slot(v, m.d_new, m.d_exact, nf, o.warm_start != 0, m.eta, m.omega0, m.aux));
+  HIPCHK(launch_x_pass(v, m.d_new, nf, false, true, true, true, 0, m.aux));
+  HIPCHK(launch_node_pass(v, m.d_new, nf, false, true, true, true, 0, m.aux));
+  HIPCHK(launch_scalar_pass(v, m.d_new, nf, false, true, true, true, 0, o.check_every, m.aux));
+  // the new slots join the block after the one in flight: `stream` waits for their initialisation
+  HIPCHK(hipEventRecord(m.ev_aux, m.aux));
+  HIPCHK(hipStreamWaitEvent(m.stream, m.ev_aux, 0));
   m.act.insert(m.act.end(), fresh.begin(), fresh.end());
   HIPCHK(hipMemcpyAsync(m.d_slots, m.act.data(), m.act.size() * sizeof(int32_t), hipMemcpyHostToDevice, m.stream));
-  HIPCHK(hipStreamSynchronize(m.stream));
+  HIPCHK(hipStreamSynchronize(m.aux));   // (the uploads above read host vectors that end with this call)
   return NEP_OK;
 }
 
@@ -1161,8 +1179,8 @@ int solve_batch(Model &m, int B, const int32_t *slots, const double *lbi, const 
 // is the one whose objective and feasibility the certificate proved), else the PDHG iterate.
 int solution_z(Model &m, int slot, const double **z) {
   int32_t st = 0;
-  HIPCHK(hipMemcpyAsync(&st, &m.v.ctrl[slot].status, sizeof(int32_t), hipMemcpyDeviceToHost, m.stream));
-  HIPCHK(hipStreamSynchronize(m.stream));
+  HIPCHK(hipMemcpyAsync(&st, &m.v.ctrl[slot].status, sizeof(int32_t), hipMemcpyDeviceToHost, m.aux));
+  HIPCHK(hipStreamSynchronize(m.aux));
   *z = (st == NEP_LP_OPTIMAL ? m.v.zr : m.v.zi) + (size_t)slot * m.v.sint;
   return NEP_OK;
 }
@@ -1190,27 +1208,27 @@ int compact(Model &m, const T *vals, int rows, int cols, int64_t ld, double thr,
   }
   hipError_t e;
   if constexpr (sizeof(T) == 4)
-    e = launch_compact_f32(vals, rows, cols, ld, thr, round3, m.d_cnt, m.d_off, nullptr, nullptr, nullptr, true, m.stream);
+    e = launch_compact_f32(vals, rows, cols, ld, thr, round3, m.d_cnt, m.d_off, nullptr, nullptr, nullptr, true, m.aux);
   else
-    e = launch_compact_f64(vals, rows, cols, ld, thr, round3, m.d_cnt, m.d_off, nullptr, nullptr, nullptr, true, m.stream);
+    e = launch_compact_f64(vals, rows, cols, ld, thr, round3, m.d_cnt, m.d_off, nullptr, nullptr, nullptr, true, m.aux);
   HIPCHK(e);
   int32_t total = 0;
-  HIPCHK(hipMemcpyAsync(&total, m.d_off + rows, sizeof(int32_t), hipMemcpyDeviceToHost, m.stream));
-  HIPCHK(hipStreamSynchronize(m.stream));
+  HIPCHK(hipMemcpyAsync(&total, m.d_off + rows, sizeof(int32_t), hipMemcpyDeviceToHost, m.aux));
+  HIPCHK(hipStreamSynchronize(m.aux));
   *n_out = total;
   if (capacity < total || total == 0) return NEP_OK;   // size query (or nothing to write)
   if ((rc = ensure_entries(m, total))) return rc;
   if constexpr (sizeof(T) == 4)
     e = launch_compact_f32(vals, rows, cols, ld, thr, round3, m.d_cnt, m.d_off, m.d_erow, m.d_ecol, m.d_eval, false,
-                           m.stream);
+                           m.aux);
   else
     e = launch_compact_f64(vals, rows, cols, ld, thr, round3, m.d_cnt, m.d_off, m.d_erow, m.d_ecol, m.d_eval, false,
-                           m.stream);
+                           m.aux);
   HIPCHK(e);
-  if (orow) HIPCHK(hipMemcpyAsync(orow, m.d_erow, total * sizeof(int32_t), hipMemcpyDeviceToHost, m.stream));
-  if (ocol) HIPCHK(hipMemcpyAsync(ocol, m.d_ecol, total * sizeof(int32_t), hipMemcpyDeviceToHost, m.stream));
-  if (oval) HIPCHK(hipMemcpyAsync(oval, m.d_eval, total * sizeof(double), hipMemcpyDeviceToHost, m.stream));
-  HIPCHK(hipStreamSynchronize(m.stream));
+  if (orow) HIPCHK(hipMemcpyAsync(orow, m.d_erow, total * sizeof(int32_t), hipMemcpyDeviceToHost, m.aux));
+  if (ocol) HIPCHK(hipMemcpyAsync(ocol, m.d_ecol, total * sizeof(int32_t), hipMemcpyDeviceToHost, m.aux));
+  if (oval) HIPCHK(hipMemcpyAsync(oval, m.d_eval, total * sizeof(double), hipMemcpyDeviceToHost, m.aux));
+  HIPCHK(hipStreamSynchronize(m.aux));
   return NEP_OK;
 }
 
@@ -1223,10 +1241,10 @@ int flows(Model &m, int n, const int32_t *slots, float *out) {
   }
   int rc;
   if (!m.d_flows && (rc = dalloc(m, &m.d_flows, (size_t)m.max_batch * m.F * m.N))) return rc;
-  HIPCHK(hipMemcpyAsync(m.d_new, slots, n * sizeof(int32_t), hipMemcpyHostToDevice, m.stream));
-  HIPCHK(launch_node_flows(m.v, m.d_new, n, m.d_flows, m.stream));
-  HIPCHK(hipMemcpyAsync(out, m.d_flows, (size_t)n * m.F * m.N * sizeof(float), hipMemcpyDeviceToHost, m.stream));
-  HIPCHK(hipStreamSynchronize(m.stream));
+  HIPCHK(hipMemcpyAsync(m.d_new, slots, n * sizeof(int32_t), hipMemcpyHostToDevice, m.aux));
+  HIPCHK(launch_node_flows(m.v, m.d_new, n, m.d_flows, m.aux));
+  HIPCHK(hipMemcpyAsync(out, m.d_flows, (size_t)n * m.F * m.N * sizeof(float), hipMemcpyDeviceToHost, m.aux));
+  HIPCHK(hipStreamSynchronize(m.aux));
   return NEP_OK;
 }
 
@@ -1242,10 +1260,10 @@ int score_check(Model &m, int slot, double *out) {
   double *cpu_fj = m.d_score, *fpart = cpu_fj + nfj, *jpart = fpart + nf, *dout = jpart + nj;
   const double *z = nullptr;
   if ((rc = solution_z(m, slot, &z))) return rc;
-  HIPCHK(launch_score_check(m.v, slot, z, cpu_fj, fpart, jpart, m.d_node_cost, m.node_budget, dout, m.stream));
+  HIPCHK(launch_score_check(m.v, slot, z, cpu_fj, fpart, jpart, m.d_node_cost, m.node_budget, dout, m.aux));
   double raw[16] = {0};
-  HIPCHK(hipMemcpyAsync(raw, dout, 10 * sizeof(double), hipMemcpyDeviceToHost, m.stream));
-  HIPCHK(hipStreamSynchronize(m.stream));
+  HIPCHK(hipMemcpyAsync(raw, dout, 10 * sizeof(double), hipMemcpyDeviceToHost, m.aux));
+  HIPCHK(hipStreamSynchronize(m.aux));
   // NEP_SC_* layout (include/neptune_lp.h)
   out[0] = raw[0];                                   // network delay  sum W D x
   out[1] = raw[6];                                   // nodes used     #{n != 0}
@@ -1334,17 +1352,18 @@ int nep_lp_get_solution(void *model, int32_t slot, double *z_int, float *x_dense
   if (!model) return fail(NEP_ERR_ARG, "null model");
   Model &m = *static_cast<Model *>(model);
   if (slot < 0 || slot >= m.max_batch) return fail(NEP_ERR_ARG, "slot out of range");
+  if (m.busy[slot]) return fail(NEP_ERR_STATE, "slot is still iterating");
   if (z_int) {
     const double *z = nullptr;
     int rc = solution_z(m, slot, &z);
     if (rc) return rc;
-    HIPCHK(hipMemcpyAsync(z_int, z, m.il.n_int * sizeof(double), hipMemcpyDeviceToHost, m.stream));
+    HIPCHK(hipMemcpyAsync(z_int, z, m.il.n_int * sizeof(double), hipMemcpyDeviceToHost, m.aux));
   }
   if (x_dense) {
     std::vector<float> xb((size_t)m.R * m.NP);
     HIPCHK(hipMemcpyAsync(xb.data(), m.v.x + (size_t)slot * m.v.sx, xb.size() * sizeof(float), hipMemcpyDeviceToHost,
-                          m.stream));
-    HIPCHK(hipStreamSynchronize(m.stream));
+                          m.aux));
+    HIPCHK(hipStreamSynchronize(m.aux));
     const int N = m.N, F = m.F;
     for (int r = 0; r < m.R; ++r) {
       const int f = m.row_f[r], src = m.row_src[r];
@@ -1356,7 +1375,7 @@ int nep_lp_get_solution(void *model, int32_t slot, double *z_int, float *x_dense
       }
     }
   }
-  HIPCHK(hipStreamSynchronize(m.stream));
+  HIPCHK(hipStreamSynchronize(m.aux));
   return NEP_OK;
 }
 
@@ -1364,10 +1383,11 @@ int nep_lp_get_rows(void *model, int32_t slot, float *xbar, int32_t *row_f, int3
   if (!model) return fail(NEP_ERR_ARG, "null model");
   Model &m = *static_cast<Model *>(model);
   if (slot < 0 || slot >= m.max_batch) return fail(NEP_ERR_ARG, "slot out of range");
+  if (xbar && m.busy[slot]) return fail(NEP_ERR_STATE, "slot is still iterating");
   if (xbar) {
     HIPCHK(hipMemcpy2DAsync(xbar, m.N * sizeof(float), m.v.x + (size_t)slot * m.v.sx, m.NP * sizeof(float),
-                            m.N * sizeof(float), m.R, hipMemcpyDeviceToHost, m.stream));
-    HIPCHK(hipStreamSynchronize(m.stream));
+                            m.N * sizeof(float), m.R, hipMemcpyDeviceToHost, m.aux));
+    HIPCHK(hipStreamSynchronize(m.aux));
   }
   if (row_f) std::memcpy(row_f, m.row_f.data(), m.R * sizeof(int32_t));
   if (row_src) std::memcpy(row_src, m.row_src.data(), m.R * sizeof(int32_t));
@@ -1381,23 +1401,23 @@ int nep_lp_copy_state(void *model, int32_t src, int32_t dst) {
   if (m.busy[dst]) return fail(NEP_ERR_STATE, "destination slot is still iterating");
   if (src == dst) return NEP_OK;
   const DeviceView &v = m.v;
-  HIPCHK(hipMemcpyAsync(v.x + dst * v.sx, v.x + src * v.sx, v.sx * sizeof(float), hipMemcpyDeviceToDevice, m.stream));
+  HIPCHK(hipMemcpyAsync(v.x + dst * v.sx, v.x + src * v.sx, v.sx * sizeof(float), hipMemcpyDeviceToDevice, m.aux));
   HIPCHK(hipMemcpyAsync(v.theta + dst * m.R, v.theta + src * m.R, m.R * sizeof(float), hipMemcpyDeviceToDevice,
-                        m.stream));
+                        m.aux));
   HIPCHK(hipMemcpyAsync(v.zi + dst * v.sint, v.zi + src * v.sint, v.sint * sizeof(double), hipMemcpyDeviceToDevice,
-                        m.stream));
+                        m.aux));
   HIPCHK(hipMemcpyAsync(v.y + dst * v.sdual, v.y + src * v.sdual, v.sdual * sizeof(double), hipMemcpyDeviceToDevice,
-                        m.stream));
+                        m.aux));
   HIPCHK(hipMemcpyAsync(v.kty + dst * v.skty, v.kty + src * v.skty, v.skty * sizeof(float), hipMemcpyDeviceToDevice,
-                        m.stream));
+                        m.aux));
   // the certificate's repaired point travels with the status it belongs to: solution_z() of a copied
   // certified slot returns the source's repaired point, not the destination's stale one
   HIPCHK(hipMemcpyAsync(v.zr + dst * v.sint, v.zr + src * v.sint, v.sint * sizeof(double), hipMemcpyDeviceToDevice,
-                        m.stream));
+                        m.aux));
   HIPCHK(hipMemcpyAsync(v.rpart + dst * v.srpart, v.rpart + src * v.srpart, v.srpart * sizeof(double),
-                        hipMemcpyDeviceToDevice, m.stream));
-  HIPCHK(hipMemcpyAsync(v.ctrl + dst, v.ctrl + src, sizeof(Ctrl), hipMemcpyDeviceToDevice, m.stream));
-  HIPCHK(hipStreamSynchronize(m.stream));
+                        hipMemcpyDeviceToDevice, m.aux));
+  HIPCHK(hipMemcpyAsync(v.ctrl + dst, v.ctrl + src, sizeof(Ctrl), hipMemcpyDeviceToDevice, m.aux));
+  HIPCHK(hipStreamSynchronize(m.aux));
   return NEP_OK;
 }
 
@@ -1409,8 +1429,8 @@ int nep_lp_set_params(void *model, double tol, double cutoff) {
   m.prm_host[0] = m.run.tol;
   m.prm_host[1] = m.run.cutoff;
   m.prm_host[2] = m.run.gap_tol;
-  HIPCHK(hipMemcpyAsync(m.d_prm, m.prm_host, sizeof(m.prm_host), hipMemcpyHostToDevice, m.stream));
-  HIPCHK(hipStreamSynchronize(m.stream));
+  HIPCHK(hipMemcpyAsync(m.d_prm, m.prm_host, sizeof(m.prm_host), hipMemcpyHostToDevice, m.aux));
+  HIPCHK(hipStreamSynchronize(m.aux));
   return NEP_OK;
 }
 

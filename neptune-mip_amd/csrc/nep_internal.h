@@ -106,6 +106,7 @@ struct Ctrl {
   int32_t polish, polish_pending;       // pending: 1 = enter (duals saved, from 0), 2 = leave (duals restored)
   double polish_bound;
   int64_t polish_k0, polish_next;        // iteration polishing started; earliest iteration to start (-1: never)
+  double bound_res;                      // > 0: stop with NEP_LP_BOUND once the bound converged (nep_lp_opts)
 };
 
 // row-family offsets inside y / kz / rho / lo / hi
@@ -161,6 +162,7 @@ struct DeviceView {
   // NEP_OMEGA_SMOOTH override them
   double rs_suff, rs_nec, rs_art, omega_smooth;
   int64_t max_iters;
+  double bound_res;                      // submit option copied into each new slot's Ctrl (init_slot)
 };
 
 }  // namespace nep

@@ -1473,6 +1473,12 @@ __global__ __launch_bounds__(256) void scalar_pass(DeviceView v, const int32_t *
       restore_duals = 1;
       return;
     }
+    if (res <= ctrl->bound_res && pobj - b <= gap_tol * fmax(1.0, fabs(b))) {   // bound converged (B&B node)
+      ctrl->status = 5;   // NEP_LP_BOUND
+      ctrl->active = 0;
+      restore_duals = 1;
+      return;
+    }
   } else {
     ctrl->lagr = lagr;
     if (lagr > ctrl->best_lagr) ctrl->best_lagr = lagr;
@@ -1480,6 +1486,12 @@ __global__ __launch_bounds__(256) void scalar_pass(DeviceView v, const int32_t *
     ctrl->gap = gap;
     if (isfinite(lagr) && res <= tol && gap <= gap_tol * fmax(1.0, fabs(lagr))) {
       ctrl->status = 0; ctrl->active = 0; return;
+    }
+    // a B&B node's bound has converged (nep_lp_opts.bound_res): its residual need not reach tol, since
+    // the node branches on the bound, which is valid at any dual point
+    const double bl = ctrl->best_lagr;
+    if (isfinite(bl) && res <= ctrl->bound_res && pobj - bl <= gap_tol * fmax(1.0, fabs(bl))) {
+      ctrl->status = 5; ctrl->active = 0; return;   // NEP_LP_BOUND
     }
   }
   if (ctrl->best_lagr > cutoff) { ctrl->status = 3; ctrl->active = 0; return; }
@@ -1594,6 +1606,7 @@ __global__ void init_slot(DeviceView v, const int32_t *__restrict__ slots, const
     ctrl->active = 1;
     ctrl->exact = exact[blockIdx.y];
     ctrl->max_iters = v.max_iters;
+    ctrl->bound_res = v.bound_res;
     ctrl->restart_pending = 1;
     ctrl->polish = ctrl->polish_pending = 0;   // a warm start does not inherit its parent's polishing
     ctrl->polish_bound = -INFINITY;

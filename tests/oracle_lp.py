@@ -73,7 +73,7 @@ class OracleLP:
     # streaming form (nep_lp_submit / nep_lp_advance): HiGHS solves each submitted node at once; advance
     # hands back up to min_done finished nodes per call, in slot order, like the engine's blocks
     def submit(self, slots, lb=None, ub=None, tol=1e-7, cutoff=math.inf, max_iters=0, check_every=64,
-               warm_start=False, warm_omega_floor=0.0):
+               warm_start=False, warm_omega_floor=0.0, bound_res=0.0):
         slots = np.asarray(slots).reshape(-1)
         self._cutoff = cutoff
         r = self.solve(slots, lb, ub, tol=tol, cutoff=math.inf)
@@ -90,6 +90,9 @@ class OracleLP:
 
     def set_params(self, tol=1e-7, cutoff=math.inf):
         self._cutoff = cutoff
+
+    def diag(self, slot):
+        return {"pres": 0.0}
 
     def active(self):
         return len(getattr(self, "_queue", []))
@@ -152,7 +155,7 @@ class StreamingOracleLP(OracleLP):
     the pre-polish incumbent: round-2 ADVICE)."""
 
     def submit(self, slots, lb=None, ub=None, tol=1e-7, cutoff=math.inf, max_iters=0, check_every=64,
-               warm_start=False, warm_omega_floor=0.0):
+               warm_start=False, warm_omega_floor=0.0, bound_res=0.0):
         slots = np.asarray(slots).reshape(-1)
         self._cutoff = cutoff
         r = self.solve(slots, lb, ub, tol=tol, cutoff=math.inf)
@@ -171,6 +174,9 @@ class StreamingOracleLP(OracleLP):
             pobj = obj + (1e-9 * max(1.0, abs(obj)) if tol <= 1e-8 else 0.0)
             self._pend[int(s)] = [blocks, obj, pobj]
         return st
+
+    def diag(self, slot):
+        return {"pres": 0.0}
 
     def active(self):
         return len(getattr(self, "_pend", {}))

@@ -118,3 +118,60 @@ def check_step1_solution(data, variant, alpha, xb, row_f, row_src, z, lb=None, u
             obj += (1 - alpha) * xdelay / mwd
     worst = max(v for k, v in viol.items() if k != "C4")
     return viol, worst, obj
+
+
+def check_step2_solution(data, variant, alpha, mode, max_score, xb, row_f, row_src, z, lb=None, ub=None,
+                         soften=1.3, prev_delay=0.0, tol=1e-6, simplex_tol=2e-5):
+    """Independent fp64 host check of a step-2 engine solution: the step-1 rows C1-C7 (check_step1_solution,
+    on c and n) plus the step-2 rows of constraints_step2.py and the disruption objective
+    (objectives.py:55-63).  z = c, moved_from, moved_to [F*N each], allocated, deallocated (+ n[N]):
+      D1 (:5-9)    mf >= 0, mf - c >= -old          D2 (:12-16)  mt >= 0, mt + c >= old
+      D3 (:19-33)  a <= 0, sumOld - sum c >= a, d <= 0, sum c - sumOld >= d
+      D4 (:36-55)  delete: d + a + sumOld - sum c >= 0 ; create: d + a - sumOld + sum c >= 0
+      D5/D6/D7 (:57-88) the variant's score row (normalised by its right-hand side)
+    Returns (violations, worst, disruption objective recomputed from z)."""
+    W = np.asarray(data.workload_matrix, np.float64)
+    F, N = W.shape
+    FN = F * N
+    z = np.asarray(z, np.float64)
+    has_n = variant != "MinDelay"
+    c, mf, mt = z[:FN], z[FN:2 * FN], z[2 * FN:3 * FN]
+    a, d = float(z[3 * FN]), float(z[3 * FN + 1])
+    n = z[3 * FN + 2:3 * FN + 2 + N] if has_n else np.zeros(0)
+    z1 = np.concatenate([c, n])
+    box1 = [None, None]
+    for k, lim in enumerate((lb, ub)):
+        if lim is not None:
+            lim = np.asarray(lim, np.float64)
+            box1[k] = np.concatenate([lim[:FN], lim[3 * FN + 2:3 * FN + 2 + N] if has_n else np.zeros(0)])
+    viol, _, _ = check_step1_solution(data, variant if has_n else "MinDelay", alpha, xb, row_f, row_src, z1,
+                                      box1[0], box1[1], tol, simplex_tol)
+    old = np.asarray(data.old_allocations_matrix, np.float64).ravel()
+    so, sc = float(old.sum()), float(c.sum())
+    viol["D1"] = float(max(0.0, (-mf).max(), (-(mf - c) - old).max()))
+    viol["D2"] = float(max(0.0, (-mt).max(), (old - (mt + c)).max()))
+    viol["D3"] = float(max(0.0, a, a - (so - sc), d, d - (sc - so)) / max(1.0, so))
+    d4 = (d + a + so - sc) if mode == "delete" else (d + a - so + sc)
+    viol["D4"] = float(max(0.0, -d4) / max(1.0, so))
+    x = np.asarray(xb, np.float64)
+    D = np.asarray(data.node_delay_matrix, np.float64)
+    wsrc = np.where(row_src >= 0, W[row_f, np.maximum(row_src, 0)], 0.0)
+    dsrc = np.where(row_src[:, None] >= 0, D[np.maximum(row_src, 0)], 0.0)
+    if variant == "MinUtilization":
+        lhs, rhs = float(n.sum()), max_score * soften
+    elif variant == "MinDelay":
+        lhs, rhs = float((wsrc[:, None] * dsrc * x).sum()), soften * prev_delay
+    else:
+        md = np.maximum(np.asarray(data.max_delay_matrix, np.float64)[None, :], D.max(axis=0)[:, None])  # [i, f]
+        mdr = np.where(row_src >= 0, md[np.maximum(row_src, 0), row_f], 1.0)
+        lhs = alpha / N * float(n.sum()) + float((((1 - alpha) * wsrc / mdr)[:, None] * dsrc * x).sum())
+        rhs = max_score * soften
+    viol["score"] = float(max(0.0, lhs - rhs) / max(1.0, abs(rhs)))
+    if lb is not None:
+        viol["lb"] = float(max(0.0, np.nanmax(np.where(np.isfinite(lb), np.asarray(lb) - z, 0.0))))
+    if ub is not None:
+        viol["ub"] = float(max(0.0, np.nanmax(np.where(np.isfinite(ub), z - np.asarray(ub), 0.0))))
+    w = float(FN)
+    obj = w * float(mf.sum() + mt.sum()) + (w - 1) * a + (w + 1) * d
+    worst = max(v for k, v in viol.items() if k != "C4")
+    return viol, worst, obj

@@ -3,8 +3,10 @@ recorded models (root LPs of every step model, and seeded B&B-node fixings), wit
 
 A certified LP (NEP_LP_OPTIMAL) must be within 1e-6 max(1, |HiGHS|): the certificate evaluates the
 primal at a repaired, feasible point, so a certified value is an LP value, not only a
-bound.  Every step-1 LP must certify.  A step-2 LP that PDHG does not certify within the budget must
-return a valid bound within 1e-4 (DESIGN.md §4 'Known limit'); each such LP is printed."""
+bound.  Every LP must certify, except the step-2 node LPs listed in KNOWN_UNCERTIFIED (DESIGN.md §4
+'Known limit': their fixings force a routing column to carry >= 1 - eps and the PDHG routing stays
+~1e-6 short of it after 200k iterations); those must still return a bound within 1e-6 of HiGHS, and the
+test is reported XFAIL (not passed) while they stay uncertified."""
 import numpy as np
 import pytest
 
@@ -13,6 +15,14 @@ from gpu_cases import G, build_args, fixing_bounds, lp_cases
 pytestmark = pytest.mark.gpu
 TOL = 1e-6
 SOLVE_TOL = 5e-7      # certificate tolerance of the solves: below the 1e-6 parity bar
+
+
+# (golden case, model, LP index: 0 = root) -> why it does not certify (tools/step2_split_probe.py,
+# profiles/r03/step2_split_probe.log)
+KNOWN_UNCERTIFIED = {
+    ("payload", 1, 1): "moved_to fixed 0 on an old placement: the routing column stays 1.4e-6 short of 1 - eps",
+    ("syn_4x3_s0_r0.5_NeptuneMinUtilization", 1, 3): "forced placement: routing column 9e-7 short of 1 - eps",
+}
 
 
 def _gap(a, b):
@@ -34,22 +44,28 @@ def test_root_and_node_lps(name, k):
     ub = np.full((B, m.n_int), np.inf)
     for b, (l, u, _) in enumerate(nodes):
         lb[b + 1], ub[b + 1] = l, u
-    res = m.solve(np.arange(B), lb, ub, tol=SOLVE_TOL, max_iters=100000)
+    res = m.solve(np.arange(B), lb, ub, tol=SOLVE_TOL, max_iters=200000 if step >= 2 else 100000)
     refs = [rec["lp_objective"]] + [r for _, _, r in nodes]
+    known = []
     for b, ref in enumerate(refs):
         st, obj = int(res["status"][b]), float(res["obj"][b])
         if ref is None:
             assert st != LP_OPTIMAL, f"node {b}: HiGHS infeasible but engine says optimal obj={obj}"
             continue
         assert obj <= ref + TOL * max(1.0, abs(ref)), f"node {b}: bound {obj} above the LP optimum {ref}"
-        if st != LP_OPTIMAL and step >= 2:
-            # step 2 (DESIGN.md §4 'Known limit'): the bound stays valid and close; logged, and such
-            # an LP is never a B&B incumbent
-            assert st == LP_ITERATION_LIMIT and _gap(obj, ref) <= 1e-4, f"node {b}: status {st} bound {obj} vs {ref}"
-            print(f"UNCERTIFIED step-2 LP {name} model {k} node {b}: bound {obj} (HiGHS {ref})")
+        why = KNOWN_UNCERTIFIED.get((name, k, b))
+        if st != LP_OPTIMAL and why is not None:
+            # a known uncertified step-2 LP: its bound must still equal HiGHS within 1e-6 (it is never a
+            # B&B incumbent); reported as XFAIL below
+            assert st == LP_ITERATION_LIMIT and _gap(obj, ref) <= TOL, f"node {b}: status {st} bound {obj} vs {ref}"
+            print(f"UNCERTIFIED step-2 LP {name} model {k} node {b}: bound {obj} (HiGHS {ref}): {why}")
+            known.append(f"LP {b}: {why}")
             continue
         assert st == LP_OPTIMAL, f"node {b}: status {st} iters {res['iters'][b]} obj {obj} (HiGHS {ref})"
         assert _gap(obj, ref) <= TOL, f"node {b}: obj {obj} ref {ref} primal {res['primal_obj'][b]}"
+    m.close()
+    if known:
+        pytest.xfail("uncertified (bound within 1e-6 of HiGHS): " + "; ".join(known))
 
 
 @pytest.mark.parametrize("continuous", [False, True])

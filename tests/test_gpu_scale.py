@@ -37,41 +37,52 @@ def _solve_case(c, tol=SOLVE_TOL):
     return m, rr, res
 
 
-UNCERTIFIED = []
+# step-2 cases whose LPs PDHG does not certify at 1e-6 within the budget (DESIGN.md §4 'Known limit',
+# tools/step2_split_probe.py): case -> (largest bound gap measured, why).  Their bounds must stay valid
+# and within that gap; the test then reports XFAIL, not a pass.  Every other LP must certify.
+KNOWN_UNCERTIFIED = {
+    "syn64x32_MDU_s2delete": (1e-5, "the routing x stalls 1.2e-2 above the optimum (no small-block repair "
+                                    "closes it: best objective over (c, moved, a, d, n) at that x is the same)"),
+    "syn64x32_MDU_s2create": (3e-4, "the Lagrangian bound stalls below the optimum 2.13e-4 (the 1/M-priced "
+                                    "routing flow and its C5 duals are not resolved)"),
+}
 
 
-def _check_lp(c, what, st, obj, iters, ref):
-    """Step 1: certified and within 1e-6 of HiGHS.  Step 2 (DESIGN.md §4 'Known limit'): certified and
-    within 1e-6, or — when PDHG did not reach the certificate in the iteration budget — a VALID bound
-    (<= HiGHS + 1e-6); such LPs are printed with their gap and never become B&B incumbents."""
+def _check_lp(c, what, st, obj, iters, ref, known):
+    """Certified and within 1e-6 of HiGHS; or, for a KNOWN_UNCERTIFIED case, a VALID bound (<= HiGHS
+    + 1e-6) within the case's recorded gap — collected in `known` (never a B&B incumbent)."""
     from core.engine.lp import LP_ITERATION_LIMIT, LP_OPTIMAL
     if st == LP_OPTIMAL:
         assert gap(obj, ref) <= TOL, f"{what}: {obj} vs HiGHS {ref}"
         return
-    assert c["step"] != 1, f"{what}: status {st} after {iters} iterations (HiGHS {ref})"
+    assert c["name"] in KNOWN_UNCERTIFIED, f"{what}: status {st} after {iters} iterations (HiGHS {ref})"
     assert st == LP_ITERATION_LIMIT, f"{what}: status {st}"
     assert obj <= ref + TOL * max(1.0, abs(ref)), f"{what}: bound {obj} above the LP value {ref}"
-    UNCERTIFIED.append((c.get("variant"), c["step"], what, obj, ref))
+    assert gap(obj, ref) <= KNOWN_UNCERTIFIED[c["name"]][0], f"{what}: bound {obj} vs HiGHS {ref}"
+    known.append(f"{what} gap {gap(obj, ref):.2e}")
     print(f"UNCERTIFIED step-2 LP {what}: bound {obj} (HiGHS {ref}, gap {gap(obj, ref):.2e}) after {iters} iterations")
 
 
 @pytest.mark.parametrize("name", sorted(CASES))
 def test_scale_parity(name):
     from core.engine.lp import LP_OPTIMAL
-    c = CASES[name]
+    c = dict(CASES[name], name=name)
     m, rr, res = _solve_case(c)
+    known = []
     try:
         ref = c["root"]["lp_objective"]
-        _check_lp(c, "root", int(rr["status"][0]), float(rr["obj"][0]), rr["iters"][0], ref)
+        _check_lp(c, "root", int(rr["status"][0]), float(rr["obj"][0]), rr["iters"][0], ref, known)
         for b, nd in enumerate(c["nodes"]):
             st, obj = int(res["status"][b]), float(res["obj"][b])
             if nd["lp_objective"] is None:
                 assert st != LP_OPTIMAL, f"node {b}: HiGHS infeasible, engine optimal {obj}"
                 continue
-            _check_lp(c, f"node {b}", st, obj, res["iters"][b], nd["lp_objective"])
+            _check_lp(c, f"node {b}", st, obj, res["iters"][b], nd["lp_objective"], known)
         print(f"{name}: root {rr['iters'][0]} iterations, nodes {res['iters'].tolist()}")
     finally:
         m.close()
+    if known:
+        pytest.xfail(f"uncertified step-2 LPs ({KNOWN_UNCERTIFIED[name][1]}): " + ", ".join(known))
 
 
 def _full_size_check(payload, variant, fixings=0, seed=0):
@@ -128,3 +139,62 @@ def test_full_size_alibaba_1024x512(variant):
     from core.utils.synthetic import alibaba_payload
     rr = _full_size_check(alibaba_payload(1024, 512, seed=0), variant, fixings=4, seed=1)
     print("1024x512", variant, "root iterations", rr["iters"][0], "obj", rr["obj"][0])
+
+
+def test_full_size_alibaba_1024x512_step2_create():
+    """BASELINE config 5's shape, step 2 (create, MinDelayAndUtilization at the published step-1 score
+    0.005, gen_scale_golden.py:33): the root (optimum ~0: every function keeps its old placements) and 4
+    warm children whose fixings force moves, so their optimum is O(1) .. O(F N): open 2 new (f, j) (cost
+    1 each), close an old one (2 F N - 1 plus the opening it forces), empty a node (n = 0), move one
+    function.  Each LP certified after more than one iteration and re-checked on the host in fp64 against
+    every step-1 and step-2 row family, its disruption objective recomputed from z
+    (scale_util.check_step2_solution; constraints_step2.py, objectives.py:55-63)."""
+    from core.engine.lp import LPModel, LP_OPTIMAL, STEP2_CREATE
+    from core.utils import data_to_solver_input
+    from core.utils.synthetic import alibaba_payload
+    from scale_util import check_step2_solution
+    data = data_to_solver_input(alibaba_payload(1024, 512, seed=0), with_db=False)
+    F, N = data.workload_matrix.shape
+    FN = F * N
+    old = np.asarray(data.old_allocations_matrix, np.float64)
+    m = LPModel(data, "MinDelayAndUtilization", step=STEP2_CREATE, alpha=0.5, max_score=0.005,
+                soften_step1_sol=1.3, max_batch=5)
+    try:
+        rr = m.solve([0], tol=TOL, max_iters=400000)
+        assert int(rr["status"][0]) == LP_OPTIMAL, f"root: status {rr['status'][0]} after {rr['iters'][0]}"
+        rng = np.random.default_rng(3)
+        fs = [f for f in rng.permutation(F) if 0 < old[f].sum() < N][:4]
+        ones = [np.flatnonzero(old[f] == 1) for f in fs]
+        zeros = [np.flatnonzero(old[f] == 0) for f in fs]
+        n0 = 3 * FN + 2
+        j_node = int(np.flatnonzero(old.sum(axis=0) > 0)[0])
+        fix = [([fs[0] * N + zeros[0][0], fs[0] * N + zeros[0][1]], [1.0, 1.0]),     # open two new placements
+               ([fs[1] * N + ones[1][0]], [0.0]),                                     # close an old one
+               ([n0 + j_node], [0.0]),                                                # empty a node
+               ([fs[3] * N + ones[3][0], fs[3] * N + zeros[3][0]], [0.0, 1.0])]       # move a function
+        lb = np.full((4, m.n_int), -np.inf)
+        ub = np.full((4, m.n_int), np.inf)
+        for b, (idx, val) in enumerate(fix):
+            lb[b, idx] = ub[b, idx] = val
+            m.copy_state(0, b + 1)
+        r2 = m.solve(np.arange(1, 5), lb, ub, tol=TOL, max_iters=200000, warm_start=True)
+        print("1024x512 step-2 create: root", rr["iters"][0], "its obj", rr["obj"][0], "; children its",
+              r2["iters"].tolist(), "obj", r2["obj"].tolist())
+        boxes = [(None, None)] + [(lb[b], ub[b]) for b in range(4)]
+        for b in range(5):
+            st = int(rr["status"][0]) if b == 0 else int(r2["status"][b - 1])
+            obj = float(rr["obj"][0]) if b == 0 else float(r2["obj"][b - 1])
+            pobj = float(rr["primal_obj"][0]) if b == 0 else float(r2["primal_obj"][b - 1])
+            its = int(rr["iters"][0]) if b == 0 else int(r2["iters"][b - 1])
+            assert st == LP_OPTIMAL, f"LP {b}: status {st} after {its} iterations"
+            assert pobj - obj <= TOL * max(1.0, abs(obj)), (b, obj, pobj)
+            if b:
+                assert its > 1 and obj >= 0.5, f"child {b}: {its} iterations, objective {obj} (expected a forced move)"
+            xb, rf, rs = m.rows(b)
+            z, _ = m.solution(b, dense_x=False)
+            viol, worst, hobj = check_step2_solution(data, "MinDelayAndUtilization", 0.5, "create", 0.005, xb, rf, rs,
+                                                     z, *boxes[b])
+            assert viol["C4"] <= 2e-5 and worst <= 1e-5, (b, viol)
+            assert abs(hobj - pobj) <= 1e-6 * max(1.0, abs(pobj)), (b, hobj, pobj)
+    finally:
+        m.close()
