@@ -73,7 +73,7 @@ def parse(argv=None):
                     help="after the root certifies at --tol, continue it (warm, same slot) until its objective gap "
                          "is below this: the children warm-start from a well-converged root (0 = off)")
     ap.add_argument("--cold", action="store_true", help="cold-start every node LP")
-    ap.add_argument("--cpu-budget", type=float, default=45.0,
+    ap.add_argument("--cpu-budget", type=float, default=150.0,
                     help="seconds for the CPU baseline (0 = skip); the bench-size attempt gets what the fit leaves, "
                          ">= 30 s")
     ap.add_argument("--cpu-workers", type=int, default=16,

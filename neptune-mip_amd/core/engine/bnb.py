@@ -80,11 +80,15 @@ class BnBResult:
         # wall seconds by phase: device waits in advance, host work per finished LP, submits (incl.
         # warm-start copies), the drain after a stop, the end (routing fetch, polish, repair)
         self.timing = dict.fromkeys(("advance", "finish", "submit", "drain", "end"), 0.0)
+        self.timing["root"] = 0.0       # wall seconds until the root LP finished (it iterates alone)
+        self.advance_calls = 0
+        self.inflight_sum = 0           # LPs in flight summed over the advance calls (mean: / advance_calls)
 
     def as_dict(self):
         d = {k: getattr(self, k) for k in ("status", "objective", "bound", "nodes", "leaves", "lps", "certified",
                                            "lp_iterations", "unresolved", "seconds", "polished", "repaired",
                                            "lp_status", "lp_status_kind", "drained", "timing")}
+        d["inflight_mean"] = self.inflight_sum / max(1, self.advance_calls)
         d["resolved"] = sum(v for k, v in self.lp_status.items() if k not in ("limit", "numerical"))
         it = np.asarray(self.lp_iters, np.float64)
         d["lp_iters_p50_p90_p99_max"] = ([float(v) for v in np.percentile(it, [50, 90, 99, 100])] if it.size else None)
@@ -112,7 +116,7 @@ class BranchAndBound:
                  node_limit=20000, time_limit=None, upper_bound=math.inf, flow_tol=1e-4, log=None, comm=None,
                  warm=True, root_max_iters=200000, check_every=12, polish_tol=1e-8, polish_iters=20000,
                  seed_leaves=None, integer_bound=None, improve=None, repair=None, node_bound_res=1e-2,
-                 retry_res=1e-2):
+                 retry_res=math.inf):
         self.lp = lp
         self.N, self.F = lp.N, lp.F
         L = lp.layout()
@@ -170,7 +174,7 @@ class BranchAndBound:
         fx[node.idx] = True
         return fx
 
-    def _round(self, node, flow, zc=None, by_flow=True):
+    def _round(self, node, flow, zc=None, by_flow=True, min_flow=None):
         """Heuristic completion of a node (a leaf fixing every c and n), or None.
 
         Memory-aware greedy rounding of the node LP: the fixed c stay as fixed; the free c the LP
@@ -182,7 +186,9 @@ class BranchAndBound:
         re-optimises x.  (Opening the LP's near-integral c first is what keeps step 2's placement
         next to the old allocation: its LP c sits at old wherever no flow forces a move.)
         by_flow=False skips the flow pass: the fewest openings the LP's c allows (a leaf whose x
-        must then fit the CPU rows with those openings only)."""
+        must then fit the CPU rows with those openings only).  min_flow: the flow pass opens only the
+        (f, j) the LP already sends >= min_flow (an open (f, j) must receive >= 1 - eps, C2, so opening
+        a trickle forces a unit of flow onto j's CPU; at 512x256 such leaves end CPU-infeasible)."""
         F, N, c0, c1 = self.F, self.N, self.c0, self.c1
         fixed = np.full(F * N, -1.0)
         sel = (node.idx >= c0) & (node.idx < c1)
@@ -240,7 +246,8 @@ class BranchAndBound:
         half = np.flatnonzero(~closed & (zc >= 0.5))
         open_in_order(half[np.argsort(-zc[half], kind="stable")])
         if by_flow:
-            cand = np.flatnonzero(~closed & (c < 0.5) & (fl > self.flow_tol))
+            thr = self.flow_tol if min_flow is None else min_flow
+            cand = np.flatnonzero(~closed & (c < 0.5) & (fl > thr))
             open_in_order(cand[np.argsort(-fl[cand], kind="stable")])
         need = np.flatnonzero(cm.sum(axis=1) < 1)
         if need.size:
@@ -366,6 +373,7 @@ class BranchAndBound:
         if st == LP_OPTIMAL:
             res.certified += 1
         if not self.root_ready and node.depth == 0 and node.kind == NODE:
+            res.timing["root"] = time.time() - self.t0
             if self.warm and st not in (LP_INFEASIBLE, LP_CUTOFF):
                 self.lp.copy_state(slot, self.root_slot)   # every later node can start from the root
             self.root_ready = True
@@ -425,8 +433,8 @@ class BranchAndBound:
         flow = self.lp.flows([slot])[0]
         me = (slot, self.slot_gen[slot])
         z, _ = self.lp.solution(slot, dense_x=False)
-        for by_flow in (False, True):
-            leaf = self._round(node, flow, z[self.c0:self.c1], by_flow)
+        for by_flow, min_flow in ((False, None), (True, None), (True, 1.0 - 1e-6)):
+            leaf = self._round(node, flow, z[self.c0:self.c1], by_flow, min_flow)
             if leaf is not None:
                 key = np.packbits(leaf[1] > 0.5).tobytes()
                 if key not in self.seen_leaves:
@@ -511,7 +519,7 @@ class BranchAndBound:
 
     # ---------------------------------------------------------------------------------------
     def solve(self):
-        t0 = time.time()
+        t0 = self.t0 = time.time()
         self.res = res = BnBResult()
         lp = self.lp
         comm = self.comm
@@ -583,6 +591,8 @@ class BranchAndBound:
             # before the frontier is dealt every rank must stay identical: drain each batch whole.  Under a
             # time limit the sharded loop comes back after every block, so a stop is never held up by
             # long LPs (a leaf's retry runs the root budget)
+            res.advance_calls += 1
+            res.inflight_sum += len(self.inflight)
             r = lp.advance((0 if self.time_limit else 1) if sharded else len(self.inflight))
             t3 = time.perf_counter()
             tm["advance"] += t3 - t2

@@ -66,6 +66,11 @@ class NeptuneStepBase(Solver):
     def upper_bound(self):
         return math.inf
 
+    # B&B branching nodes stop once their bound has converged (core/engine/bnb.py, NEP_LP_BOUND); step 2
+    # keeps every node LP to its certificate: its disruption objective (weights F N) moves by orders of
+    # magnitude with the residual, so a node stopped at 1e-2 can branch on flows far from its LP optimum
+    node_bound_res = 1e-2
+
     def seed_leaves(self, layout):
         """Placements to try as leaves right after the root (a B&B primal start); none by default."""
         return []
@@ -119,7 +124,8 @@ class NeptuneStepBase(Solver):
                                  time_limit=self.time_limit,
                                  upper_bound=ub * (1 + 1e-6) + 1e-6 if math.isfinite(ub) else ub, log=self.log,
                                  seed_leaves=self.seed_leaves(model.layout()), integer_bound=self.integer_bound(model.layout()),
-                                 improve=self.improve(model.layout()), repair=self.routing_repair(model.layout()))
+                                 improve=self.improve(model.layout()), repair=self.routing_repair(model.layout()),
+                                 node_bound_res=self.node_bound_res)
             res = bnb.solve()
             layout = model.layout()
         finally:
@@ -247,6 +253,8 @@ class NeptuneStep1CPUMinDelayAndUtilization(NeptuneStep1CPUMinUtilization):
 
 
 class NeptuneStep2Base(NeptuneStepBase):
+    node_bound_res = 0.0   # every node LP to its certificate (see NeptuneStepBase.node_bound_res)
+
     def __init__(self, mode=str, soften_step1_sol=1.3, **kwargs):
         super().__init__(**kwargs)
         self.mode = mode

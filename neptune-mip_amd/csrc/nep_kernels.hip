@@ -1473,7 +1473,7 @@ __global__ __launch_bounds__(256) void scalar_pass(DeviceView v, const int32_t *
       restore_duals = 1;
       return;
     }
-    if (res <= ctrl->bound_res && pobj - b <= gap_tol * fmax(1.0, fabs(b))) {   // bound converged (B&B node)
+    if (ctrl->bound_res > 0.0 && res <= ctrl->bound_res && pobj - b <= gap_tol * fmax(1.0, fabs(b))) {   // B&B node
       ctrl->status = 5;   // NEP_LP_BOUND
       ctrl->active = 0;
       restore_duals = 1;
@@ -1484,13 +1484,17 @@ __global__ __launch_bounds__(256) void scalar_pass(DeviceView v, const int32_t *
     if (lagr > ctrl->best_lagr) ctrl->best_lagr = lagr;
     ctrl->pres = res;
     ctrl->gap = gap;
-    if (isfinite(lagr) && res <= tol && gap <= gap_tol * fmax(1.0, fabs(lagr))) {
+    // certified against the best bound seen so far (every Lagrangian bound of this LP is valid, the
+    // repaired point is this iteration's): the value reported is that bound
+    const double bl = ctrl->best_lagr;
+    if (isfinite(bl) && res <= tol && pobj - bl <= gap_tol * fmax(1.0, fabs(bl))) {
+      ctrl->lagr = bl;
+      ctrl->gap = pobj - bl;
       ctrl->status = 0; ctrl->active = 0; return;
     }
     // a B&B node's bound has converged (nep_lp_opts.bound_res): its residual need not reach tol, since
     // the node branches on the bound, which is valid at any dual point
-    const double bl = ctrl->best_lagr;
-    if (isfinite(bl) && res <= ctrl->bound_res && pobj - bl <= gap_tol * fmax(1.0, fabs(bl))) {
+    if (ctrl->bound_res > 0.0 && isfinite(bl) && res <= ctrl->bound_res && pobj - bl <= gap_tol * fmax(1.0, fabs(bl))) {
       ctrl->status = 5; ctrl->active = 0; return;   // NEP_LP_BOUND
     }
   }
@@ -1678,18 +1682,21 @@ static hipError_t launch_x_tw(const DeviceView &v, const int32_t *slots, int nsl
 // its x pass 1.9x faster with 16 waves (root LP 7.3 s -> 3.9 s) while 4 waves stay fastest from
 // ~4 slots on (0.47 vs 0.57 ms per launch at ~15 slots).  The column sums are then added in another
 // (still fixed) order, so an LP's last bits depend on how many slots iterated beside it.
-static int tile_waves(const DeviceView &v, int nslots) {
+// Only the certificate variant is held to 144 KB of LDS (fp64 column / CPU sums + constants: fp32, fp64,
+// repaired prices, pooled flow), i.e. to 8 waves at N = 512; the plain iterations of a lone root keep
+// 16 (2 x 16 x N fp32 accumulators: 66 KB at N = 512).
+static int tile_waves(const DeviceView &v, int nslots, bool check) {
   int tw = 4;
   while (tw < 16 && (int64_t)nslots * v.F * tw < 4096) tw *= 2;
-  // LDS of the certificate variant: fp64 column / CPU sums + constants (fp32, fp64, repaired prices, pooled flow)
-  while (tw > 4 && (size_t)(4 * tw + 2) * v.NP * sizeof(float) + 4 * v.NP * sizeof(double) > 144 * 1024) tw /= 2;
+  while (check && tw > 4 && (size_t)(4 * tw + 2) * v.NP * sizeof(float) + 4 * v.NP * sizeof(double) > 144 * 1024)
+    tw /= 2;
   return tw;
 }
 
 template <int CPL>
 static hipError_t launch_x_cpl(const DeviceView &v, const int32_t *slots, int nslots, bool check, bool init,
                                bool first, bool plain, int it, hipStream_t s) {
-  switch (tile_waves(v, nslots)) {
+  switch (tile_waves(v, nslots, check)) {
     case 4: return launch_x_tw<CPL, 4>(v, slots, nslots, check, init, first, plain, it, s);
     case 8: return launch_x_tw<CPL, 8>(v, slots, nslots, check, init, first, plain, it, s);
     case 16: return launch_x_tw<CPL, 16>(v, slots, nslots, check, init, first, plain, it, s);

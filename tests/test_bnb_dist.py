@@ -50,7 +50,8 @@ def _worker(rank, world, port, name, k, out, streaming=False):
     cls = StreamingOracleLP if streaming else OracleLP
     lp = cls(data, VARIANT[p["solver"]["type"]], step=step, max_batch=4 if streaming else 2, **kw)
     res = BranchAndBound(lp, data.workload_matrix, data.function_memory_matrix, data.node_memory_matrix,
-                         batch=2, node_limit=20000, comm=TorchComm()).solve()
+                         batch=2, node_limit=20000, comm=TorchComm(),
+                         time_limit=600.0 if streaming else None).solve()   # (a time limit: advance block by block)
     x = None if res.x is None else np.asarray(res.x).round(12).tolist()
     out[rank] = (res.status, res.objective, None if res.z is None else np.asarray(res.z).tolist(), res.nodes, x,
                  res.polished)

@@ -30,7 +30,7 @@ def _mdu_objective(data, alpha, x, z):
     return obj
 
 
-@pytest.mark.parametrize("n,f,seconds", [(64, 32, 25.0), (256, 128, 40.0), (512, 256, 45.0)])
+@pytest.mark.parametrize("n,f,seconds", [(64, 32, 25.0), (256, 128, 40.0), (512, 256, 60.0)])
 def test_product_bnb_time_limited(n, f, seconds):
     from core.engine.bnb import INFEASIBLE, BranchAndBound
     from core.engine.lp import LPModel

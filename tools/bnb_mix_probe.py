@@ -64,7 +64,8 @@ def main():
     print(f"{N}x{F}: {time.time() - t0:.1f}s status {res.status} lps {res.lps} certified {res.certified} "
           f"drained {res.drained} inc {res.objective} bound {res.bound}")
     print("by kind:", res.lp_status_kind)
-    print("timing:", {k: round(v, 2) for k, v in res.timing.items()})
+    print("timing:", {k: round(v, 2) for k, v in res.timing.items()}, "advance calls", res.advance_calls,
+          "LPs in flight (mean)", round(res.inflight_sum / max(1, res.advance_calls), 1))
     for kind in ("node", "leaf", "retry"):
         rk = [r for r in rec if r["kind"] == kind]
         if not rk:
