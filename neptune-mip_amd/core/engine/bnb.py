@@ -116,7 +116,7 @@ class BranchAndBound:
                  node_limit=20000, time_limit=None, upper_bound=math.inf, flow_tol=1e-4, log=None, comm=None,
                  warm=True, root_max_iters=200000, check_every=12, polish_tol=1e-8, polish_iters=20000,
                  seed_leaves=None, integer_bound=None, improve=None, repair=None, node_bound_res=1e-2,
-                 retry_res=math.inf):
+                 retry_res=math.inf, unit_flow_leaves=True):
         self.lp = lp
         self.N, self.F = lp.N, lp.F
         L = lp.layout()
@@ -154,6 +154,9 @@ class BranchAndBound:
         # at the node-LP limit is <= retry_res (a leaf the rounding made CPU-infeasible ends far above it
         # and would burn the root budget); otherwise its bound stays as an unresolved one
         self.retry_res = retry_res
+        # rounding leaves per branched node: fewest openings, every (f, j) with flow, and (unit_flow_leaves)
+        # every (f, j) with a unit of flow (_round's min_flow)
+        self.round_modes = ((False, None), (True, None)) + (((True, 1.0 - 1e-6),) if unit_flow_leaves else ())
         self.node_limit, self.time_limit = node_limit, time_limit
         self.ub0 = upper_bound
         self.flow_tol = flow_tol
@@ -433,7 +436,7 @@ class BranchAndBound:
         flow = self.lp.flows([slot])[0]
         me = (slot, self.slot_gen[slot])
         z, _ = self.lp.solution(slot, dense_x=False)
-        for by_flow, min_flow in ((False, None), (True, None), (True, 1.0 - 1e-6)):
+        for by_flow, min_flow in self.round_modes:
             leaf = self._round(node, flow, z[self.c0:self.c1], by_flow, min_flow)
             if leaf is not None:
                 key = np.packbits(leaf[1] > 0.5).tobytes()

@@ -70,6 +70,9 @@ class NeptuneStepBase(Solver):
     # keeps every node LP to its certificate: its disruption objective (weights F N) moves by orders of
     # magnitude with the residual, so a node stopped at 1e-2 can branch on flows far from its LP optimum
     node_bound_res = 1e-2
+    # the unit-flow rounding leaf (core/engine/bnb.py): step 1 only — on step 2 it mostly adds leaves whose
+    # placement leaves the routing infeasible, which the node LPs cannot prove, so the search ends LIMIT
+    unit_flow_leaves = True
 
     def seed_leaves(self, layout):
         """Placements to try as leaves right after the root (a B&B primal start); none by default."""
@@ -125,7 +128,7 @@ class NeptuneStepBase(Solver):
                                  upper_bound=ub * (1 + 1e-6) + 1e-6 if math.isfinite(ub) else ub, log=self.log,
                                  seed_leaves=self.seed_leaves(model.layout()), integer_bound=self.integer_bound(model.layout()),
                                  improve=self.improve(model.layout()), repair=self.routing_repair(model.layout()),
-                                 node_bound_res=self.node_bound_res)
+                                 node_bound_res=self.node_bound_res, unit_flow_leaves=self.unit_flow_leaves)
             res = bnb.solve()
             layout = model.layout()
         finally:
@@ -254,6 +257,7 @@ class NeptuneStep1CPUMinDelayAndUtilization(NeptuneStep1CPUMinUtilization):
 
 class NeptuneStep2Base(NeptuneStepBase):
     node_bound_res = 0.0   # every node LP to its certificate (see NeptuneStepBase.node_bound_res)
+    unit_flow_leaves = False
 
     def __init__(self, mode=str, soften_step1_sol=1.3, **kwargs):
         super().__init__(**kwargs)

@@ -519,7 +519,8 @@ void x_pass(DeviceView v, const int32_t *__restrict__ slots, int plain, int it, 
   const double *ybak = v.ybak + slot * v.sdual;
   const bool polishing = ctrl->polish != 0;
   const float cs = polishing ? 0.f : 1.f;
-  // (oS exists in step 2 only, which never polishes; the guard keeps the index in range regardless)
+  // (oS, the step-2 score row, exists in step 2 only; step-2 LPs polish too: its dual is kept in ybak[oS]
+  // by scalar_pass when polishing starts and read back here when it ends)
   const float ys = pol_enter ? 0.f
                              : ((pol_leave && v.step2) ? (float)ybak[v.dl.oS] : kty[(int64_t)F * NP + NP]);
 
@@ -1447,6 +1448,11 @@ __global__ __launch_bounds__(256) void scalar_pass(DeviceView v, const int32_t *
   const double gap = pobj - lagr;
   const double tol = v.prm[0], cutoff = v.prm[1], gap_tol = v.prm[2];
   ctrl->pobj = pobj;
+  // An exact LP (below) has the value pobj if it is feasible at all, so pobj bounds it from below
+  // whether or not this point is feasible yet (an infeasible LP has value +inf): a leaf whose fixed
+  // placement costs more than the incumbent is cut off at its first check instead of iterating on to
+  // feasibility.
+  if (ctrl->exact && isfinite(pobj)) ctrl->best_lagr = fmax(ctrl->best_lagr, pobj);
   if (ctrl->exact && isfinite(pobj) && res <= tol) {
     // The node box fixes every variable that carries cost (a leaf of a model whose routing has no
     // cost: step 2, or W == 0): every feasible point has the repaired point's objective, so a
@@ -1502,7 +1508,8 @@ __global__ __launch_bounds__(256) void scalar_pass(DeviceView v, const int32_t *
   if (ctrl->k >= ctrl->max_iters) { ctrl->status = 1; ctrl->active = 0; return; }
   if (!isfinite(pobj) || !isfinite(a.mvz) || !isfinite(a.mvy)) { ctrl->status = 4; ctrl->active = 0; return; }
 
-  // primal feasibility polishing (step 1): the best bound already meets the gap test against the
+  // primal feasibility polishing (step 1 and step 2; the step-2 duals D1/D2 are kept by x_pass, D3a/D3b/
+  // D4/score by this pass): the best bound already meets the gap test against the
   // repaired point's objective and only its primal residual is left — the tail of the node LPs,
   // whose CPU rows (C5) close last (tools/tail_probe.py).  From here the LP iterates on its
   // feasibility problem (objective off, duals restarted from 0) from the current point; it is

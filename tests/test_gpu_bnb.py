@@ -30,7 +30,7 @@ def _mdu_objective(data, alpha, x, z):
     return obj
 
 
-@pytest.mark.parametrize("n,f,seconds", [(64, 32, 25.0), (256, 128, 40.0), (512, 256, 60.0)])
+@pytest.mark.parametrize("n,f,seconds", [(64, 32, 25.0), (256, 128, 40.0), (512, 256, 90.0)])
 def test_product_bnb_time_limited(n, f, seconds):
     from core.engine.bnb import INFEASIBLE, BranchAndBound
     from core.engine.lp import LPModel
@@ -46,7 +46,8 @@ def test_product_bnb_time_limited(n, f, seconds):
     m = LPModel(data, "MinDelayAndUtilization", step=1, alpha=0.5, max_batch=34)
     try:
         res = BranchAndBound(m, data.workload_matrix, data.function_memory_matrix, data.node_memory_matrix,
-                             batch=32, tol=5e-7, time_limit=seconds, upper_bound=ub * (1 + 1e-6) + 1e-6,
+                             batch=32, tol=5e-7 if n < 512 else 1e-6, time_limit=seconds,
+                             root_max_iters=200000 if n < 512 else 400000, upper_bound=ub * (1 + 1e-6) + 1e-6,
                              repair=st1.routing_repair(m.layout())).solve()
     finally:
         m.close()
