@@ -116,7 +116,7 @@ class BranchAndBound:
                  node_limit=20000, time_limit=None, upper_bound=math.inf, flow_tol=1e-4, log=None, comm=None,
                  warm=True, root_max_iters=200000, check_every=12, polish_tol=1e-8, polish_iters=20000,
                  seed_leaves=None, integer_bound=None, improve=None, repair=None, node_bound_res=1e-2,
-                 retry_res=math.inf, unit_flow_leaves=True):
+                 retry_res=math.inf, unit_flow_leaves=True, node_max_iters=None):
         self.lp = lp
         self.N, self.F = lp.N, lp.F
         L = lp.layout()
@@ -154,6 +154,8 @@ class BranchAndBound:
         # at the node-LP limit is <= retry_res (a leaf the rounding made CPU-infeasible ends far above it
         # and would burn the root budget); otherwise its bound stays as an unresolved one
         self.retry_res = retry_res
+        # iteration limit of branching nodes (their bound is valid wherever they stop); leaves keep max_iters
+        self.node_max_iters = int(node_max_iters) if node_max_iters else max_iters
         # rounding leaves per branched node: fewest openings, every (f, j) with flow, and (unit_flow_leaves)
         # every (f, j) with a unit of flow (_round's min_flow)
         self.round_modes = ((False, None), (True, None)) + (((True, 1.0 - 1e-6),) if unit_flow_leaves else ())
@@ -332,7 +334,8 @@ class BranchAndBound:
                 if src != slot:
                     copies.append((src, slot))
                 warm = True
-            budget = self.root_max_iters if (node.kind == RETRY or not self.root_ready) else self.max_iters
+            budget = (self.root_max_iters if (node.kind == RETRY or not self.root_ready)
+                      else (self.node_max_iters if node.kind == NODE else self.max_iters))
             bres = self.node_bound_res if (node.kind == NODE and self.root_ready) else 0.0
             groups.setdefault((warm, budget, bres), []).append((slot, node))
         # warm-start copies: a slot that is both a parent state (source) and a new node's slot

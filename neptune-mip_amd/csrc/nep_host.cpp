@@ -95,6 +95,11 @@ struct Model {
   std::vector<int> Kr, Kc;
   std::vector<double> Kv, ftot;
   bool x_coef_nonneg = true;   // every x coefficient outside C1/C2 is >= 0 (W, cpr, D >= 0)
+  // step 2: the score / delay row's routing coefficients wsc[r] * D[src, j] (presolve: the row's smallest
+  // activity over the routing simplexes of a node's allowed destinations)
+  bool score_x = false;
+  std::vector<double> Dh;            // [N*N] delay matrix (step 2 with score_x only)
+  std::vector<uint8_t> allow;        // scratch [F*N]
   bool x_cost_free = true;     // no routing entry carries objective cost (step 2; W == 0)
   int32_t *d_exact = nullptr;  // per submitted node: the box fixes the objective (Ctrl::exact)
   // node presolve as a sparse change of the base box (presolve_setup / presolve_node)
@@ -285,7 +290,9 @@ int build(Model &m, const nep_model_desc &d) {
         wsc = (1.0 - d.alpha) * m.row_w[r] / std::max(d.max_delay[f], colmaxD[i]);
     }
     m.row_wsc[r] = (float)wsc;
+    if (wsc != 0.0) m.score_x = true;
   }
+  if (m.score_x) m.Dh.assign(D, D + (size_t)N * N);
   if (m.step2) {
     if (d.variant == NEP_MIN_DELAY) {
       score_rhs = d.soften_step1_sol * d.prev_network_delay;
@@ -736,6 +743,24 @@ static inline bool row_range_ok(const Model &m, int k, double amin, double amax)
   return true;
 }
 
+// the step-2 score / delay row's smallest activity over the routing simplexes: sum_r wsc[r] min over
+// the allowed destinations j of f_r of D[src_r, j] (allow: [F][ld] nonzero = allowed)
+static double score_row_xmin(const Model &m, const uint8_t *allow, int ld) {
+  const int N = m.N;
+  double xmin = 0.0;
+  for (int r = 0; r < m.R; ++r) {
+    const double w = m.row_wsc[r];
+    if (w == 0.0) continue;
+    const double *Dr = &m.Dh[(size_t)m.row_src[r] * N];
+    const uint8_t *al = allow + (size_t)m.row_f[r] * ld;
+    double mn = INF;
+    for (int j = 0; j < N; ++j)
+      if (al[j]) mn = std::min(mn, Dr[j]);
+    if (mn < INF) xmin += w * mn;
+  }
+  return xmin;
+}
+
 bool presolve_full(const Model &m, const double *lbi, const double *ubi, std::vector<double> &lb,
                    std::vector<double> &ub, std::vector<uint8_t> &mask) {
   const int n = m.il.n_int, N = m.N, F = m.F, NP = m.NP;
@@ -765,6 +790,7 @@ bool presolve_full(const Model &m, const double *lbi, const double *ubi, std::ve
   if (!ok) return false;
   std::vector<double> amin, amax;
   activity_ranges(m, lb, ub, mask, amin, amax);
+  if (m.score_x) amin[m.dl.oS] += score_row_xmin(m, mask.data(), NP);   // (see presolve_node)
   for (int k = 0; k < m.dl.n_dual; ++k)
     if (!row_range_ok(m, k, amin[k], amax[k])) return false;
   return true;
@@ -864,6 +890,22 @@ bool presolve_node(Model &m, const double *lbi, const double *ubi, std::vector<i
       m.dmin[r] += std::min(a * l, a * u) - std::min(a * bl, a * bu);
       m.dmax[r] += std::max(a * l, a * u) - std::max(a * bl, a * bu);
     }
+  }
+  if (ok && m.score_x) {
+    // The score / delay row (constraints_step2.py:57-88) over x: every routing row carries mass 1 on its
+    // allowed destinations, so its activity is at least sum_r wsc[r] min_{j allowed} D[src_r, j].  Closed
+    // placements can push that above the right-hand side (e.g. a step-1 delay of 0 admits only local
+    // serving): such a node is infeasible, which PDHG cannot prove (DESIGN.md §4 "Infeasibility").
+    m.allow.assign((size_t)F * N, 0);
+    for (int f = 0; f < F; ++f)
+      for (int j = 0; j < N; ++j) m.allow[(size_t)f * N + j] = m.base_mask[(size_t)f * NP + j];
+    for (size_t t = c0; t < ci.size(); ++t) {
+      const int k = ci[t];
+      if (k >= oc && k < oc + F * N) m.allow[k - oc] = cu[t] > 0.0;
+    }
+    const int rs = m.dl.oS;
+    touch(rs);
+    m.dmin[rs] += score_row_xmin(m, m.allow.data(), N);
   }
   for (int f : ftouched) {
     if (m.base_cnt[f] + m.fdelta[f] == 0) ok = false;   // every routing row of f empty

@@ -67,7 +67,7 @@ struct RowInfo {
 
 // per-function scalar partials (TS_LAGR_REP: the routing rows' Lagrangian terms at the repaired
 // column prices, DESIGN.md §4 "Dual repair")
-enum { TS_SCORE = 0, TS_POBJ, TS_LAGR, TS_MOVE, TS_DIST, TS_EMPTY, TS_LAGR_REP, NTS };
+enum { TS_SCORE = 0, TS_POBJ, TS_LAGR, TS_MOVE, TS_DIST, TS_EMPTY, TS_LAGR_REP, TS_LAGR0, NTS };
 // per-block scalar partials of the small variables
 enum {
   BS_SUMC_NEW = 0,   // sum over (f,j) of c'            (step-2 rows D3/D4)
@@ -81,6 +81,7 @@ enum {
   BS_LAGR_D,         // step 2: the disruption block's share of the Lagrangian (c, moved, a, d; D1-D4)
   BS_LAGR_REP,       // certificate: the small variables' / node rows' Lagrangian terms at the repaired duals
   BS_TLO, BS_THI,    // step 2: sum over (f,j) of the node box of c (the range of sum c)
+  BS_LAGR0,          // certificate: the Lagrangian with the objective off (the infeasibility test)
   BS_LK0,            // step 2: the disruption block kept exact, one sum per price lambda_k of sum c
   BS_LKR0 = BS_LK0 + 6,   //   (kNLam candidates; DESIGN.md §4 "Disruption block"), and the same at the
   NBS = BS_LKR0 + 6       //   repaired column prices (DESIGN.md §4 "Dual repair")

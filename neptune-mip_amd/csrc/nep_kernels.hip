@@ -96,6 +96,7 @@ struct SmallAcc {
   double lagr = 0, pobj = 0, res = 0, mvz = 0, mvy = 0, dsz = 0, dsy = 0;
   double lagrD = 0;   // Lagrangian terms of the step-2 disruption block (dblk calls)
   double lagrR = 0;   // certificate: Lagrangian terms at the repaired duals (DESIGN.md §4 "Dual repair")
+  double lagr0 = 0;   // certificate: every Lagrangian term with the objective off (DESIGN.md §4 "Infeasibility")
 };
 
 // ---------------------------------------------------------------------------------------------
@@ -322,7 +323,11 @@ __device__ __forceinline__ double dual_step_p(double *y, double *ya, double *kz,
     y[row] = ynew;
   }
   kz[row] = knew;
-  if (CHECK) (dblk ? a.lagrD : a.lagr) += row_lagr(yold, lo, hi);
+  if (CHECK) {
+    const double t = row_lagr(yold, lo, hi);
+    (dblk ? a.lagrD : a.lagr) += t;
+    a.lagr0 += t;
+  }
   return ynew;
 }
 template <bool CHECK, bool INIT>
@@ -352,6 +357,8 @@ __device__ __forceinline__ double primal_step_p(double *zi, double *zia, int k, 
     const double u = (nz - zanc) / g;
     a.dsz += u * u;
     (dblk ? a.lagrD : a.lagr) += rc > 0 ? p.lb * rc : p.ub * rc;
+    const double rc0 = rc - p.cost;   // (rc carries the cost except while polishing, when lagr0 is unused)
+    a.lagr0 += rc0 > 0 ? p.lb * rc0 : p.ub * rc0;
   }
   return nz;
 }
@@ -587,7 +594,7 @@ void x_pass(DeviceView v, const int32_t *__restrict__ slots, int plain, int it, 
 #pragma unroll
   for (int e = 0; e < E; ++e) cnt_f += __popcll(__ballot((mbits >> e) & 1u));
 
-  double s_score = 0.0, s_pobj = 0.0, s_lagr = 0.0, s_lagr_r = 0.0, s_move = 0.0, s_dist = 0.0;
+  double s_score = 0.0, s_pobj = 0.0, s_lagr = 0.0, s_lagr_r = 0.0, s_lagr0 = 0.0, s_move = 0.0, s_dist = 0.0;
   const double s_empty = (cnt_f == 0 && threadIdx.x == 0) ? (double)nrows : 0.0;
 
   for (int rr = wave; rr < nrows; rr += TW) {
@@ -644,7 +651,7 @@ void x_pass(DeviceView v, const int32_t *__restrict__ slots, int plain, int it, 
     if (CHECK) {
       // Lagrangian term of this row: min over the simplex of the reduced cost, in fp64, at the PDHG
       // duals and at the repaired column prices
-      double gmin = INFINITY, gmin_r = INFINITY;
+      double gmin = INFINITY, gmin_r = INFINITY, gmin0 = INFINITY;
 #pragma unroll
       for (int e = 0; e < E; ++e) {
         if ((mbits >> e) & 1u) {
@@ -652,11 +659,13 @@ void x_pass(DeviceView v, const int32_t *__restrict__ slots, int plain, int it, 
           const double g0 = (double)wobj * dc[e] - ((double)w * lCd[j] + (double)wsc * ysd * dc[e]);
           gmin = fmin(gmin, g0 - (double)m * lKd[j]);
           gmin_r = fmin(gmin_r, g0 - (double)m * lKr[j]);
+          gmin0 = fmin(gmin0, g0 - (double)wobj * dc[e] - (double)m * lKd[j]);   // objective off
         }
       }
       gmin = wave_min_d(gmin);
       gmin_r = wave_min_d(gmin_r);
-      if (lane == 0) { s_lagr += gmin; s_lagr_r += gmin_r; }
+      gmin0 = wave_min_d(gmin0);
+      if (lane == 0) { s_lagr += gmin; s_lagr_r += gmin_r; s_lagr0 += gmin0; }
     }
     // Projection onto {x >= 0, sum x = 1} over the allowed destinations: the threshold theta is
     // the root of f(t) = sum_j max(v_j - t, 0) - 1 (convex, decreasing).  Michelot's iteration is
@@ -1008,6 +1017,8 @@ void x_pass(DeviceView v, const int32_t *__restrict__ slots, int plain, int it, 
   vals[NTS + BS_LAGR_D] = a.lagrD;
   vals[TS_LAGR_REP] = s_lagr_r;
   vals[NTS + BS_LAGR_REP] = a.lagrR;
+  vals[TS_LAGR0] = s_lagr0;
+  vals[NTS + BS_LAGR0] = a.lagr0;
   vals[NTS + BS_TLO] = dtlo;
   vals[NTS + BS_THI] = dthi;
 #pragma unroll
@@ -1051,6 +1062,7 @@ __device__ __forceinline__ void write_bpart(double *bp, const SmallAcc &a, doubl
   vals[BS_DIST_Y] = a.dsy;
   vals[BS_LAGR_D] = a.lagrD;
   vals[BS_LAGR_REP] = a.lagrR;
+  vals[BS_LAGR0] = a.lagr0;
   vals[BS_TLO] = vals[BS_THI] = 0.0;
 #pragma unroll
   for (int q = 0; q < kNLam; ++q) vals[BS_LK0 + q] = vals[BS_LKR0 + q] = 0.0;
@@ -1428,6 +1440,14 @@ __global__ __launch_bounds__(256) void scalar_pass(DeviceView v, const int32_t *
   // the Lagrangian with every row dualised, or (step 2) the disruption block kept exact at the best
   // of the candidate prices (both are valid bounds)
   double lagr = a.lagr + a.lagrD;
+  // Infeasibility (Farkas): with the objective off the Lagrangian L0(y) is positively
+  // homogeneous in y and <= 0 at every y when the LP has a feasible point; L0(y) > 0 at a sign-feasible
+  // y proves the node LP infeasible (L(t y) >= t L0(y) + min cost -> +inf).  The margin is far above the
+  // fp64 rounding of the sums.  (Not while polishing: its passes carry no cost in rc.)
+  const double lagr0 = tot[TS_LAGR0] + tot[NTS + BS_LAGR0] + a.lagr0;
+  if (!ctrl->polish && isfinite(lagr0) && lagr0 > 1e-6 * fmax(1.0, fabs(lagr))) {
+    ctrl->status = 2; ctrl->active = 0; ctrl->lagr = INFINITY; return;
+  }
   if (v.step2) {
 #pragma unroll
     for (int q = 0; q < kNLam; ++q)

@@ -45,7 +45,8 @@ def main():
 
     B.BranchAndBound._finish = finish
     knobs = dict(node_bound_res=float(os.environ.get("NODE_BOUND_RES", "1e-3")),
-                 max_iters=int(os.environ.get("MAX_ITERS", "4096")))
+                 max_iters=int(os.environ.get("MAX_ITERS", "4096")),
+                 node_max_iters=int(os.environ.get("NODE_MAX_ITERS", "0")) or None)
     print("knobs", knobs)
     bb = B.BranchAndBound(m, data.workload_matrix, data.function_memory_matrix, data.node_memory_matrix, batch=32,
                           tol=1e-6, time_limit=secs, upper_bound=ub * (1 + 1e-6) + 1e-6,
