@@ -108,6 +108,7 @@ struct Ctrl {
   double polish_bound;
   int64_t polish_k0, polish_next;        // iteration polishing started; earliest iteration to start (-1: never)
   double bound_res;                      // > 0: stop with NEP_LP_BOUND once the bound converged (nep_lp_opts)
+  int32_t infeas_hits, pad_;             // consecutive certificate checks whose Farkas test held
 };
 
 // row-family offsets inside y / kz / rho / lo / hi

@@ -1445,8 +1445,12 @@ __global__ __launch_bounds__(256) void scalar_pass(DeviceView v, const int32_t *
   // y proves the node LP infeasible (L(t y) >= t L0(y) + min cost -> +inf).  The margin is far above the
   // fp64 rounding of the sums.  (Not while polishing: its passes carry no cost in rc.)
   const double lagr0 = tot[TS_LAGR0] + tot[NTS + BS_LAGR0] + a.lagr0;
+  // (two consecutive checks: the duals of an infeasible LP keep running off along the ray, so the test
+  // keeps holding; a one-off from rounding in the sums does not)
   if (!ctrl->polish && isfinite(lagr0) && lagr0 > 1e-6 * fmax(1.0, fabs(lagr))) {
-    ctrl->status = 2; ctrl->active = 0; ctrl->lagr = INFINITY; return;
+    if (++ctrl->infeas_hits >= 2) { ctrl->status = 2; ctrl->active = 0; ctrl->lagr = INFINITY; return; }
+  } else {
+    ctrl->infeas_hits = 0;
   }
   if (v.step2) {
 #pragma unroll
@@ -1638,6 +1642,7 @@ __global__ void init_slot(DeviceView v, const int32_t *__restrict__ slots, const
     ctrl->exact = exact[blockIdx.y];
     ctrl->max_iters = v.max_iters;
     ctrl->bound_res = v.bound_res;
+    ctrl->infeas_hits = 0;
     ctrl->restart_pending = 1;
     ctrl->polish = ctrl->polish_pending = 0;   // a warm start does not inherit its parent's polishing
     ctrl->polish_bound = -INFINITY;
