@@ -10,7 +10,7 @@ import numpy as np
 from oracle.formulation import build_model
 from oracle.solve import solve as oracle_solve
 
-LP_OPTIMAL, LP_ITERATION_LIMIT, LP_INFEASIBLE, LP_CUTOFF = 0, 1, 2, 3
+LP_OPTIMAL, LP_ITERATION_LIMIT, LP_INFEASIBLE, LP_CUTOFF, LP_BOUND = 0, 1, 2, 3, 5
 
 
 class OracleLP:
@@ -172,7 +172,7 @@ class StreamingOracleLP(OracleLP):
             blocks = 1 + zlib.crc32(key.tobytes()) % 3   # deterministic across ranks
             obj = float(r["obj"][b])
             pobj = obj + (1e-9 * max(1.0, abs(obj)) if tol <= 1e-8 else 0.0)
-            self._pend[int(s)] = [blocks, obj, pobj]
+            self._pend[int(s)] = [blocks, obj, pobj, bound_res > 0]   # bound_res: ends NEP_LP_BOUND
         return st
 
     def diag(self, slot):
@@ -193,7 +193,7 @@ class StreamingOracleLP(OracleLP):
                 break
         cut = getattr(self, "_cutoff", math.inf)
         obj = np.array([v[1] for _, v in done])
-        st = np.array([LP_CUTOFF if v[1] > cut else LP_OPTIMAL for _, v in done], np.int32)
+        st = np.array([LP_CUTOFF if v[1] > cut else (LP_BOUND if v[3] else LP_OPTIMAL) for _, v in done], np.int32)
         return {"slots": np.array([s for s, _ in done], np.int32), "obj": obj,
                 "primal_obj": np.array([v[2] for _, v in done]), "status": st,
                 "iters": np.full(len(done), 12, np.int64)}

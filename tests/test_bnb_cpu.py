@@ -72,3 +72,30 @@ def test_solver_flow_matches_reference(name, monkeypatch):
     if done and done[-1].get("mip_tied") is False:
         assert c == ref["cpu_allocations"]
         assert set(x) == set(ref["cpu_routing_rules"])
+
+
+STEP1 = [(name, k) for name, k in SMALL if k == 0][:10]
+
+
+@pytest.mark.parametrize("name,k", STEP1)
+def test_bnb_with_bound_converged_nodes(name, k):
+    """Branching nodes that end NEP_LP_BOUND (bound converged, primal not certified: nep_lp_opts.bound_res)
+    branch on their bound like certified ones; leaves still need certificates.  The streaming fake engine
+    returns LP_BOUND for every LP submitted with bound_res > 0: the search must still reach the recorded
+    MIP optimum, and only leaves may be counted certified."""
+    from core.engine.bnb import INFEASIBLE, OPTIMAL, BranchAndBound
+    from oracle_lp import StreamingOracleLP
+    p, data = _data(name)
+    rec = G[name]["models"][k]
+    variant = VARIANT[p["solver"]["type"]]
+    args = p["solver"].get("args", {})
+    lp = StreamingOracleLP(data, variant, step=1, max_batch=10, alpha=args.get("alpha", 0.5))
+    res = BranchAndBound(lp, data.workload_matrix, data.function_memory_matrix, data.node_memory_matrix,
+                         batch=8, node_limit=20000, node_bound_res=1e-2).solve()
+    if rec["status"] == 0:
+        assert res.status == OPTIMAL, res.as_dict()
+        assert _close(res.objective, rec["mip_objective"]), (res.objective, rec["mip_objective"])
+    else:
+        assert res.status == INFEASIBLE, res.as_dict()
+    assert res.lp_status_kind["node"]["certified"] <= 1      # (the root alone may certify)
+    assert res.lp_status["bound"] == res.lp_status_kind["node"]["bound"]
