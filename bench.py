@@ -247,7 +247,7 @@ def bnb_section(a, rank, world, dev, N, F):
     bnb = BranchAndBound(m, data.workload_matrix, data.function_memory_matrix, data.node_memory_matrix,
                          batch=a.batch, tol=a.tol, max_iters=a.max_iters, time_limit=a.bnb_seconds,
                          upper_bound=ub * (1 + 1e-6) + 1e-6, comm=comm, check_every=a.check_every,
-                         root_max_iters=a.root_max_iters)
+                         root_max_iters=a.root_max_iters, node_max_iters=a.max_iters // 4)
     m.reset_stats()
     t0 = time.perf_counter()
     res = bnb.solve()
