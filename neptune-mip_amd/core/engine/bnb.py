@@ -214,46 +214,50 @@ class BranchAndBound:
         zc = np.zeros(F * N) if zc is None else np.asarray(zc, np.float64).ravel()
         usedl, rooml, fmem = used.tolist(), room.tolist(), self.fn_mem.tolist()
 
-        def open_in_order(ks):
-            """Greedy first-fit of the candidates ks (flat (f, j), in priority order) into the node memories.
-            A destination's decisions depend only on its own earlier ones, so every destination whose
-            candidates all fit is decided at once (prefix sums); only the few that fill up are walked."""
+        def open_in_order(ks, key):
+            """Greedy first-fit of the candidates ks (flat (f, j), ascending) into the node memories in
+            decreasing `key` order (ties: lower index first).  A destination's decisions depend only on its
+            own earlier ones: every destination whose candidates all fit takes them all (no sort); only the
+            candidates of the few that fill up are sorted and walked."""
             if ks.size == 0:
                 return
             fj, jj = np.divmod(ks, N)
-            o = np.argsort(jj, kind="stable")
-            js, ks_o = jj[o], ks[o]
-            ms = self.fn_mem[fj[o]]
-            cs = np.cumsum(ms)
-            start = np.flatnonzero(np.r_[True, js[1:] != js[:-1]])
-            base = np.repeat(cs[start] - ms[start], np.diff(np.r_[start, len(js)]))
-            avail = np.asarray(rooml)[js] - np.asarray(usedl)[js]
-            fits = (cs - base) <= avail
-            seg_ok = np.logical_and.reduceat(fits, start)
-            okm = np.repeat(seg_ok, np.diff(np.r_[start, len(js)]))
-            opened = ks_o[okm].tolist()
-            np.add.at(used_acc := np.zeros(N), js[okm], ms[okm])
-            for j, u in zip(np.flatnonzero(used_acc).tolist(), used_acc[used_acc > 0].tolist()):
+            ms = self.fn_mem[fj]
+            tot = np.bincount(jj, weights=ms, minlength=N)
+            fit = tot <= np.asarray(rooml) - np.asarray(usedl)
+            allin = fit[jj]
+            opened = ks[allin].tolist()
+            some = fit & (tot > 0)
+            for j, u in zip(np.flatnonzero(some).tolist(), tot[some].tolist()):
                 usedl[j] += u
-            for s0, e0 in zip(start[~seg_ok].tolist(), (np.r_[start, len(js)][1:][~seg_ok]).tolist()):
-                j = int(js[s0])
-                seg_k, seg_m = ks_o[s0:e0].tolist(), ms[s0:e0]
-                tail_min = np.minimum.accumulate(seg_m[::-1])[::-1].tolist()   # smallest memory still to come
-                for q, (k, mq) in enumerate(zip(seg_k, seg_m.tolist())):
-                    left = rooml[j] - usedl[j]
-                    if left < tail_min[q]:
-                        break                                                # nothing left fits here
-                    if mq <= left:
-                        opened.append(k)
-                        usedl[j] += mq
+            rest = ~allin
+            if rest.any():
+                kr, jr, mr, keyr = ks[rest], jj[rest], ms[rest], key[rest]
+                o = np.lexsort((kr, -keyr, jr))          # by destination, then priority, then index
+                kr, jr, mr = kr[o].tolist(), jr[o].tolist(), mr[o].tolist()
+                q = 0
+                while q < len(kr):
+                    j = jr[q]
+                    e = q
+                    while e < len(kr) and jr[e] == j:
+                        e += 1
+                    tail_min = np.minimum.accumulate(np.asarray(mr[q:e])[::-1])[::-1].tolist()
+                    for t in range(q, e):
+                        left = rooml[j] - usedl[j]
+                        if left < tail_min[t - q]:
+                            break                                # nothing left fits here
+                        if mr[t] <= left:
+                            opened.append(kr[t])
+                            usedl[j] += mr[t]
+                    q = e
             c[opened] = 1.0
 
         half = np.flatnonzero(~closed & (zc >= 0.5))
-        open_in_order(half[np.argsort(-zc[half], kind="stable")])
+        open_in_order(half, zc[half])
         if by_flow:
             thr = self.flow_tol if min_flow is None else min_flow
             cand = np.flatnonzero(~closed & (c < 0.5) & (fl > thr))
-            open_in_order(cand[np.argsort(-fl[cand], kind="stable")])
+            open_in_order(cand, fl[cand])
         need = np.flatnonzero(cm.sum(axis=1) < 1)
         if need.size:
             # each function left without a destination: the open-able destination with the largest LP c,
