@@ -160,6 +160,10 @@ int nep_lp_set_params(void *model, double tol, double cutoff);
 /* flow[b][f][j] = sum_i x[i,f,j] of finished slots (host float, n x F x N), computed on the device:
  * the branch-and-bound's branching / rounding input (replaces copying the R x N routing rows). */
 int nep_lp_get_flows(void *model, int32_t n, const int32_t *slots, float *flows);
+/* API 6: the same flows and, in wflows, their part carried by workload sources only (W[f,i] > 0: the
+ * pooled zero-workload row excluded — its mass is free to go to any open placement); the B&B's
+ * rounding opens placements for workload, not for that free mass. */
+int nep_lp_get_flows_split(void *model, int32_t n, const int32_t *slots, float *flows, float *wflows);
 
 /* Wire format on the device (neptune/utils/output.py:23-39).  Routing entries of the aggregated rows
  * with x > threshold (0.001), value rounded as np.round(x, 3) when round3; allocation entries c[f,j] >

@@ -61,6 +61,7 @@ class Stats(ctypes.Structure):
 EXPORTS = ("nep_model_create", "nep_model_destroy", "nep_model_get_info", "nep_lp_solve_batch",
            "nep_lp_submit", "nep_lp_advance", "nep_lp_active",
            "nep_lp_get_solution", "nep_lp_get_rows", "nep_lp_copy_state", "nep_get_stats", "nep_reset_stats",
+           "nep_lp_get_flows_split",
            "nep_last_error", "nep_api_version", "nep_lp_get_diag", "nep_debug_build", "nep_debug_state",
            "nep_debug_presolve", "nep_lp_set_params", "nep_lp_get_flows", "nep_lp_routing_entries",
            "nep_lp_allocation_entries", "nep_lp_score_check")
@@ -103,6 +104,7 @@ def load_library(path=None):
     lib.nep_debug_presolve.argtypes = [ctypes.POINTER(ModelDesc), i32, _dp, _dp, pi32, pi32, _dp, _dp]
     lib.nep_lp_set_params.argtypes = [vp, ctypes.c_double, ctypes.c_double]
     lib.nep_lp_get_flows.argtypes = [vp, i32, pi32, ctypes.POINTER(ctypes.c_float)]
+    lib.nep_lp_get_flows_split.argtypes = [vp, i32, pi32, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float)]
     lib.nep_lp_routing_entries.argtypes = [vp, i32, ctypes.c_double, i32, i64, pi64, pi32, pi32, _dp]
     lib.nep_lp_allocation_entries.argtypes = [vp, i32, ctypes.c_double, i64, pi64, pi32, pi32]
     lib.nep_lp_score_check.argtypes = [vp, i32, _dp]
@@ -330,10 +332,17 @@ class LPModel:
         incumbent without resubmitting."""
         _check(self._lib, self._lib.nep_lp_set_params(self._h, float(tol), float(cutoff)), "nep_lp_set_params")
 
-    def flows(self, slots):
-        """flow[b, f, j] = sum_i x[i, f, j] of finished slots, reduced on the device (nep_lp_get_flows)."""
+    def flows(self, slots, split=False):
+        """flow[b, f, j] = sum_i x[i, f, j] of finished slots, reduced on the device (nep_lp_get_flows);
+        split=True: (flow, workload-source part of it) (nep_lp_get_flows_split)."""
         slots = np.ascontiguousarray(np.asarray(slots, dtype=np.int32).reshape(-1))
         out = np.zeros((len(slots), self.F, self.N), np.float32)
+        if split:
+            wout = np.zeros_like(out)
+            _check(self._lib, self._lib.nep_lp_get_flows_split(
+                self._h, len(slots), _ptr(slots, ctypes.c_int32), _ptr(out, ctypes.c_float),
+                _ptr(wout, ctypes.c_float)), "nep_lp_get_flows_split")
+            return out, wout
         _check(self._lib, self._lib.nep_lp_get_flows(self._h, len(slots), _ptr(slots, ctypes.c_int32),
                                                      _ptr(out, ctypes.c_float)), "nep_lp_get_flows")
         return out

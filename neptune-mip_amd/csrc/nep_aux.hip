@@ -21,16 +21,23 @@ namespace nep {
 // flows: one workgroup per (function f, slot b); thread = destination j, loop over f's rows
 // (coalesced across j).  fp64 accumulation of the pooled-row weights m_r.
 // ---------------------------------------------------------------------------------------------
+// wout (optional): the same sum over the rows of workload-carrying sources only (the pooled
+// zero-workload row excluded: its mass is free to go anywhere)
 __global__ __launch_bounds__(256) void node_flows(DeviceView v, const int32_t *__restrict__ slots,
-                                                  float *__restrict__ out) {
+                                                  float *__restrict__ out, float *__restrict__ wout) {
   const int f = blockIdx.x, b = blockIdx.y;
   const int slot = slots[b];
   const float *x = v.x + slot * v.sx;
   const int r0 = v.frow[f], r1 = v.frow[f + 1];
   for (int j = threadIdx.x; j < v.N; j += blockDim.x) {
-    double s = 0.0;
-    for (int r = r0; r < r1; ++r) s += (double)v.rows[r].m * (double)x[(int64_t)r * v.NP + j];
+    double s = 0.0, sw = 0.0;
+    for (int r = r0; r < r1; ++r) {
+      const double t = (double)v.rows[r].m * (double)x[(int64_t)r * v.NP + j];
+      s += t;
+      if (v.rows[r].src >= 0) sw += t;
+    }
     out[((int64_t)b * v.F + f) * v.N + j] = (float)s;
+    if (wout) wout[((int64_t)b * v.F + f) * v.N + j] = (float)sw;
   }
 }
 
@@ -236,8 +243,9 @@ __global__ __launch_bounds__(256) void score_final(DeviceView v, const double *_
 // ---------------------------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------------------------
-hipError_t launch_node_flows(const DeviceView &v, const int32_t *slots, int n, float *out, hipStream_t s) {
-  hipLaunchKernelGGL(node_flows, dim3(v.F, n), dim3(256), 0, s, v, slots, out);
+hipError_t launch_node_flows(const DeviceView &v, const int32_t *slots, int n, float *out, float *wout,
+                             hipStream_t s) {
+  hipLaunchKernelGGL(node_flows, dim3(v.F, n), dim3(256), 0, s, v, slots, out, wout);
   return hipGetLastError();
 }
 

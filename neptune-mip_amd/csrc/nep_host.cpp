@@ -32,7 +32,8 @@ hipError_t launch_node_bounds(const DeviceView &v, const int32_t *slots, int nsl
                               const double *cl, const double *cu, int max_chg, hipStream_t s);
 hipError_t launch_init_slot(const DeviceView &v, const int32_t *slots, const int32_t *exact, int nslots, bool warm,
                             double eta, double omega0, hipStream_t s);
-hipError_t launch_node_flows(const DeviceView &v, const int32_t *slots, int n, float *out, hipStream_t s);
+hipError_t launch_node_flows(const DeviceView &v, const int32_t *slots, int n, float *out, float *wout,
+                             hipStream_t s);
 hipError_t launch_compact_f32(const float *vals, int rows, int cols, int64_t ld, double thr, int round3,
                               int32_t *cnt, int32_t *off, int32_t *orow, int32_t *ocol, double *oval, bool count_only,
                               hipStream_t s);
@@ -1274,7 +1275,7 @@ int compact(Model &m, const T *vals, int rows, int cols, int64_t ld, double thr,
   return NEP_OK;
 }
 
-int flows(Model &m, int n, const int32_t *slots, float *out) {
+int flows(Model &m, int n, const int32_t *slots, float *out, float *wout = nullptr) {
   if (n <= 0) return NEP_OK;
   if (n > m.max_batch) return fail(NEP_ERR_ARG, "n > max_batch");
   for (int b = 0; b < n; ++b) {
@@ -1282,10 +1283,14 @@ int flows(Model &m, int n, const int32_t *slots, float *out) {
     if (m.busy[slots[b]]) return fail(NEP_ERR_STATE, "slot is still iterating");
   }
   int rc;
-  if (!m.d_flows && (rc = dalloc(m, &m.d_flows, (size_t)m.max_batch * m.F * m.N))) return rc;
+  const size_t plane = (size_t)m.max_batch * m.F * m.N;
+  if (!m.d_flows && (rc = dalloc(m, &m.d_flows, 2 * plane))) return rc;
   HIPCHK(hipMemcpyAsync(m.d_new, slots, n * sizeof(int32_t), hipMemcpyHostToDevice, m.aux));
-  HIPCHK(launch_node_flows(m.v, m.d_new, n, m.d_flows, m.aux));
+  HIPCHK(launch_node_flows(m.v, m.d_new, n, m.d_flows, wout ? m.d_flows + plane : nullptr, m.aux));
   HIPCHK(hipMemcpyAsync(out, m.d_flows, (size_t)n * m.F * m.N * sizeof(float), hipMemcpyDeviceToHost, m.aux));
+  if (wout)
+    HIPCHK(hipMemcpyAsync(wout, m.d_flows + plane, (size_t)n * m.F * m.N * sizeof(float), hipMemcpyDeviceToHost,
+                          m.aux));
   HIPCHK(hipStreamSynchronize(m.aux));
   return NEP_OK;
 }
@@ -1479,6 +1484,11 @@ int nep_lp_set_params(void *model, double tol, double cutoff) {
 int nep_lp_get_flows(void *model, int32_t n, const int32_t *slots, float *flows_out) {
   if (!model || (n > 0 && (!slots || !flows_out))) return fail(NEP_ERR_ARG, "null argument");
   return flows(*static_cast<Model *>(model), n, slots, flows_out);
+}
+
+int nep_lp_get_flows_split(void *model, int32_t n, const int32_t *slots, float *flows_out, float *wflows_out) {
+  if (!model || (n > 0 && (!slots || !flows_out || !wflows_out))) return fail(NEP_ERR_ARG, "null argument");
+  return flows(*static_cast<Model *>(model), n, slots, flows_out, wflows_out);
 }
 
 int nep_lp_routing_entries(void *model, int32_t slot, double threshold, int32_t round3, int64_t capacity,

@@ -27,6 +27,7 @@ class OracleLP:
                              mode="delete" if self.step == 2 else "create", alpha=alpha,
                              soften_step1_sol=soften_step1_sol, max_score=max_score, prev_x=prev_x)
         self.nx = self.N * self.N * self.F
+        self._W = np.asarray(data.workload_matrix, np.float64)
         self.n_int = self.m["A"].shape[1] - self.nx
         self.max_batch = max_batch
         self._sol = {}
@@ -107,12 +108,14 @@ class OracleLP:
         return {"slots": np.array([s for s, _ in done], np.int32), "obj": obj, "primal_obj": obj.copy(),
                 "status": st, "iters": np.zeros(len(done), np.int64)}
 
-    def flows(self, slots):
+    def flows(self, slots, split=False):
         out = np.zeros((len(slots), self.F, self.N), np.float32)
+        wout = np.zeros_like(out)
         for b, s in enumerate(np.asarray(slots).reshape(-1)):
-            x = self._sol[int(s)]
-            out[b] = x[:self.nx].reshape(self.F, self.N, self.N).sum(axis=1)
-        return out
+            x = self._sol[int(s)][:self.nx].reshape(self.F, self.N, self.N)
+            out[b] = x.sum(axis=1)
+            wout[b] = (x * (self._W > 0)[:, :, None]).sum(axis=1)
+        return (out, wout) if split else out
 
     def copy_state(self, src, dst):
         """Warm-start hand-off of the engine (nep_lp_copy_state); HiGHS solves from scratch, so this

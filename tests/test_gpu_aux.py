@@ -50,6 +50,12 @@ def test_flows_entries_and_checks(name, k):
             fl = m.flows([slot])[0]
             ref = x.sum(axis=0)                             # [f, j]
             assert np.allclose(fl, ref, rtol=1e-6, atol=1e-6)
+            # split flows (nep_lp_get_flows_split): the workload sources' part (W[f, i] > 0) of the same sum
+            fl2, wfl = m.flows([slot], split=True)
+            Wm = np.asarray(data.workload_matrix) > 0       # [f, i]
+            wref = (x * Wm.T[:, :, None]).sum(axis=0)
+            assert np.array_equal(fl2[0], fl)
+            assert np.allclose(wfl[0], wref, rtol=1e-6, atol=1e-6)
             # routing entries == reference wire format of the dense x
             row, dst, val = m.routing_entries(slot)
             xb, rf, rs = m.rows(slot)
