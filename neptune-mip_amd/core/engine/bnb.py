@@ -234,22 +234,10 @@ class BranchAndBound:
             if rest.any():
                 kr, jr, mr, keyr = ks[rest], jj[rest], ms[rest], key[rest]
                 o = np.lexsort((kr, -keyr, jr))          # by destination, then priority, then index
-                kr, jr, mr = kr[o].tolist(), jr[o].tolist(), mr[o].tolist()
-                q = 0
-                while q < len(kr):
-                    j = jr[q]
-                    e = q
-                    while e < len(kr) and jr[e] == j:
-                        e += 1
-                    tail_min = np.minimum.accumulate(np.asarray(mr[q:e])[::-1])[::-1].tolist()
-                    for t in range(q, e):
-                        left = rooml[j] - usedl[j]
-                        if left < tail_min[t - q]:
-                            break                                # nothing left fits here
-                        if mr[t] <= left:
-                            opened.append(kr[t])
-                            usedl[j] += mr[t]
-                    q = e
+                for k, j, mq in zip(kr[o].tolist(), jr[o].tolist(), mr[o].tolist()):
+                    if usedl[j] + mq <= rooml[j]:
+                        opened.append(k)
+                        usedl[j] += mq
             c[opened] = 1.0
 
         half = np.flatnonzero(~closed & (zc >= 0.5))
