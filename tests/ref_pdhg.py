@@ -294,11 +294,14 @@ def proj_simplex_rows(V, mask):
     return out
 
 
-def solve(m, lbi=None, ubi=None, tol=1e-7, max_iters=100000, check_every=64, verbose=False):
+def solve(m, lbi=None, ubi=None, tol=1e-7, max_iters=100000, check_every=64, verbose=False, inline_reflect=False):
     """Same algorithm as the kernels, fp64: blocks of `check_every` iterations; iteration 0 of a block
     is the certificate iteration (a plain PDHG step whose input dual is the previous block's plain
     output), restarts take effect at iteration 1, the last iteration is plain, the others are
     reflected Halpern steps w' = lam (2 T(w) - w) + (1 - lam) w_anchor.
+    inline_reflect: form the dual step's reflected activity as K(2ŵ - w) from the primal points
+    (what x_pass does for the per-(f, j) rows) instead of 2·Kŵ - kz with the tracked activity kz;
+    the two are the same operator (K is linear).
     Returns dict(status, obj, pobj, iters, x, z, y)."""
     ok, lb, ub, fmask = m.presolve(lbi, ubi)
     if not ok:
@@ -333,7 +336,7 @@ def solve(m, lbi=None, ubi=None, tol=1e-7, max_iters=100000, check_every=64, ver
             zn = np.clip(z - tau * m.gam ** 2 * rcz, lb, ub)
             act = m.K(xn, zn)
             s = sig * m.rho ** 2
-            V = y - s * (2 * act - kz)
+            V = y - s * (m.K(2 * xn - x, 2 * zn - z) if inline_reflect else 2 * act - kz)
             with np.errstate(invalid="ignore"):
                 a = V + s * m.hi
                 b = V + s * m.lo

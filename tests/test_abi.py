@@ -108,3 +108,18 @@ def test_request_unknown_solver_type_raises():
     p["solver"] = {"type": "NotASolver"}
     with pytest.raises(KeyError):
         solve_request(p)
+
+
+@pytest.mark.parametrize("name,k", CASES[:4])
+def test_inline_reflection_equals_tracked_activity(name, k):
+    """x_pass forms the C1/C2/D1/D2 reflected activities K(2ŵ - w) from the primal points instead of
+    tracking K w (kz / kza): the same PDHG operator, so the mirror reaches the same answer either way."""
+    from ref_pdhg import RefModel, solve
+    data, variant, step, kw = build_args(name, k)
+    ref = RefModel(data, variant, step=step, **kw)
+    a = solve(ref, tol=1e-6, max_iters=20000, check_every=16)
+    b = solve(ref, tol=1e-6, max_iters=20000, check_every=16, inline_reflect=True)
+    assert a["status"] == b["status"]
+    if a["status"] == 0:
+        assert abs(a["obj"] - b["obj"]) <= 1e-5 * max(1.0, abs(a["obj"]))
+        assert abs(a["iters"] - b["iters"]) <= 0.1 * a["iters"] + 16
