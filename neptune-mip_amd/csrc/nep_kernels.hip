@@ -9,8 +9,10 @@
 // ("plain" iterations take w' = T(w): the certificate iteration and the one before it, so the
 // certificate's dual is a T output and satisfies the row sign constraints).
 // K·[x̂, ẑ] is produced in the same passes that write the iterate (column sums, CPU sums, score
-// row); the iterate's activity K w is kept in `kz` (and the anchor's in `kza`, K is linear), so
-// K(2ẑ − z) = 2·Kẑ − Kz costs no extra pass.
+// row).  The per-(f, j) rows C1/C2/D1/D2 form the reflected activity K(2ŵ − w) in the pass itself
+// (x_pass sums m (2x̂ − x̄) per column and holds the old and new c / moved in registers); the node
+// and scalar rows keep the iterate's activity K w in `kz` (the anchor's in `kza`, K is linear), so
+// K(2ŵ − w) = 2·Kŵ − Kw costs no extra pass there either.
 //
 // Launches per iteration: x_pass (one workgroup per (function f, LP slot): all routing rows of f,
 // then the per-(f,j) variables c / moved_from / moved_to and rows C1/C2/D1/D2 of that f) and
@@ -26,6 +28,13 @@
 #include <cmath>
 
 #include "nep_internal.h"
+
+// NEP_INLINE_REFLECT (build flag, default off until the whole GPU suite has run on it):
+// the C1/C2/D1/D2 duals take the reflected activity K(2ŵ - w) formed in x_pass instead of the tracked
+// activities kz / kza (48 B per (f, j) and LP-iteration less)
+#ifndef NEP_INLINE_REFLECT
+#define NEP_INLINE_REFLECT 0
+#endif
 
 namespace nep {
 
@@ -339,6 +348,36 @@ __device__ __forceinline__ double dual_step(const DeviceView &v, double *y, doub
   return dual_step_p<CHECK, INIT>(y, ya, kz, kza, row, act, p, sigma, copy_anchor, halp, lam, a, dblk);
 }
 
+// Dual half-step of a row whose reflected activity K(2ŵ - w) the caller forms itself from values it
+// already holds (C1/C2: the reflected column sum of x and 2ĉ - c; D1/D2: the small variables), so the
+// per-(f, j) activities kz / kza are neither read nor written (48 B per (f, j) and LP-iteration).
+template <bool CHECK, bool INIT>
+__device__ __forceinline__ double dual_step_refl(const DeviceView &v, double *y, double *ya, int row, double refl,
+                                                 double yold, double sigma, bool copy_anchor, bool halp, double lam,
+                                                 SmallAcc &a, bool dblk = false) {
+  const double lo = v.lo[row], hi = v.hi[row];
+  double ynew = yold;
+  if (!INIT) {
+    const double rr = v.rho[row];
+    const double yanc = copy_anchor ? yold : ya[row];
+    if (copy_anchor) ya[row] = yanc;
+    const double yT = dual_prox(yold, sigma * rr * rr, refl, lo, hi);
+    const double t = (yT - yold) / rr;
+    a.mvy += t * t;
+    if (CHECK) { const double u = (yT - yanc) / rr; a.dsy += u * u; }
+    ynew = halp ? lam * (2.0 * yT - yold) + (1.0 - lam) * yanc : yT;
+    y[row] = ynew;
+  } else {
+    ya[row] = yold;
+  }
+  if (CHECK) {
+    const double t = row_lagr(yold, lo, hi);
+    (dblk ? a.lagrD : a.lagr) += t;
+    a.lagr0 += t;
+  }
+  return ynew;
+}
+
 // Primal half-step of one small variable.  Stores the new iterate, returns the T output ẑ (the
 // value every row activity and the certificate use).  rc = cost - Kᵀy.
 template <bool CHECK>
@@ -544,6 +583,10 @@ void x_pass(DeviceView v, const int32_t *__restrict__ slots, int plain, int it, 
   double *lKd = reinterpret_cast<double *>(lC + NP), *lCd = lKd + NP;
   double *lKr = lCd + NP;   // certificate: the repaired column prices s*[j] of f (DESIGN.md §4 "Dual repair")
   double *lPm = lKr + NP;   // certificate: the pooled row's flow m * x̂[pooled, j] (fp64; DESIGN.md §4 "Pooled shift")
+  // The C1/C2 duals need the reflected activity K(2ŵ - w) only: the plain iterations accumulate the
+  // reflected column sums m (2x̂ - x) in lS itself; the certificate ones, which keep the sums of x̂ in
+  // fp64 for the repaired point, accumulate them beside it (lR, fp32 [TW][NP])
+  float *lR = reinterpret_cast<float *>(lPm + NP);
   // the price of sum c the step-2 repair aims at (pre-update duals of D3a / D3b / D4)
   double lam_rep = 0.0;
   if (CHECK && v.step2) {
@@ -582,6 +625,7 @@ void x_pass(DeviceView v, const int32_t *__restrict__ slots, int plain, int it, 
         double2 *pd = reinterpret_cast<double2 *>(lSd + wave * NP + j0);
         double2 *pe = reinterpret_cast<double2 *>(lWd + wave * NP + j0);
         pd[0] = pd[1] = pe[0] = pe[1] = make_double2(0.0, 0.0);
+        if (NEP_INLINE_REFLECT) *reinterpret_cast<float4 *>(lR + wave * NP + j0) = make_float4(0.f, 0.f, 0.f, 0.f);
       } else {
         *reinterpret_cast<float4 *>(lS + wave * NP + j0) = make_float4(0.f, 0.f, 0.f, 0.f);
         *reinterpret_cast<float4 *>(lW + wave * NP + j0) = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -756,13 +800,21 @@ void x_pass(DeviceView v, const int32_t *__restrict__ slots, int plain, int it, 
     for (int q = 0; q < CPL; ++q) {
       const int j0 = 4 * (lane + kWave * q);
       if (j0 < NP) {
-        float o[4];
+        float o[4], rf[4];
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
           const int e = 4 * q + t;
-          o[t] = halp ? lam * (2.f * xn[e] - xc[e]) + (1.f - lam) * xav[e] : xn[e];
+          rf[t] = 2.f * xn[e] - xc[e];   // reflected point 2x̂ - x
+          o[t] = halp ? lam * rf[t] + (1.f - lam) * xav[e] : xn[e];
         }
         st_x4(xrow + j0, f32x4{o[0], o[1], o[2], o[3]}, nt);
+        // column sums m x̂, or the reflected m (2x̂ - x) (plain iterations: lS; certificate iterations: lR)
+        if (NEP_INLINE_REFLECT) {
+          float4 *pr = reinterpret_cast<float4 *>((CHECK ? lR : lS) + wave * NP + j0);
+          float4 c = *pr;
+          c.x += m * rf[0]; c.y += m * rf[1]; c.z += m * rf[2]; c.w += m * rf[3];
+          *pr = c;
+        }
       }
     }
     if (restart) {
@@ -809,6 +861,11 @@ void x_pass(DeviceView v, const int32_t *__restrict__ slots, int plain, int it, 
           a0.x += md * xq[0]; a0.y += md * xq[1]; a1.x += md * xq[2]; a1.y += md * xq[3];
           b0.x += wd * xq[0]; b0.y += wd * xq[1]; b1.x += wd * xq[2]; b1.y += wd * xq[3];
           pd[0] = a0; pd[1] = a1; pe[0] = b0; pe[1] = b1;
+        } else if (NEP_INLINE_REFLECT) {
+          float4 *pw = reinterpret_cast<float4 *>(lW + wave * NP + j0);
+          float4 b = *pw;
+          b.x += w * xq[0]; b.y += w * xq[1]; b.z += w * xq[2]; b.w += w * xq[3];
+          *pw = b;
         } else {
           float4 *ps = reinterpret_cast<float4 *>(lS + wave * NP + j0);
           float4 *pw = reinterpret_cast<float4 *>(lW + wave * NP + j0);
@@ -886,11 +943,13 @@ void x_pass(DeviceView v, const int32_t *__restrict__ slots, int plain, int it, 
   for (int q = 0; q < kNLam; ++q) { lamk[q] = 0.0; dlk[q] = dlkr[q] = 0.0; }
   if (CHECK && v.step2) dblock_lambdas(v, y, lamk);
   for (int j = threadIdx.x; j < N; j += kWave * TW) {
-    float Sf = 0.f, Uf = 0.f;
+    float Sf = 0.f, Uf = 0.f;   // (plain iterations: Sf is the reflected column sum)
     double Sd = 0.0, Ud = 0.0;
     if (CHECK) {
       Sd = lSd[j];   // reduced (and pooled-shifted) above
       Ud = lWd[j];
+#pragma unroll
+      for (int wv = 0; wv < TW && NEP_INLINE_REFLECT; ++wv) Sf += lR[wv * NP + j];
     } else {
 #pragma unroll
       for (int wv = 0; wv < TW; ++wv) {
@@ -898,7 +957,8 @@ void x_pass(DeviceView v, const int32_t *__restrict__ slots, int plain, int it, 
         Uf += lW[wv * NP + j];
       }
     }
-    const double S = CHECK ? Sd : (double)Sf;
+    const double S = CHECK ? Sd : (double)Sf;   // column sum of x̂ (tracked-activity build)
+    const double Sr = (double)Sf;               // reflected column sum of m (2x̂ - x) (NEP_INLINE_REFLECT)
     const double U = CHECK ? Ud * (double)v.cpr[(int64_t)f * NP + j] : (double)(Uf * v.cpr[(int64_t)f * NP + j]);
     const int idx = f * N + j;
     // (polishing: at its first iteration every dual counts as 0 — this f's rows C1/C2 are kept in
@@ -949,19 +1009,35 @@ void x_pass(DeviceView v, const int32_t *__restrict__ slots, int plain, int it, 
       }
       kty_c += -yd1 + yd2 - yD3a + yD3b + v.sigma4 * yD4;
     }
+    const double c_old = NEP_INLINE_REFLECT ? zi[il.oc + idx] : 0.0;
     const double cn = primal_step<CHECK>(v, zi, zia, lb, ub, il.oc + idx, csd * v.cost_int[il.oc + idx] - kty_c, taud,
                                          copy_anchor, halp, lamd, a, v.step2);
-    const double y1n = dual_step<CHECK, INIT>(v, y, ya, kz, kza, dl.o1 + idx, S - v.M * cn, y1, sigma, copy_anchor,
-                                              halp, lamd, a);
-    const double y2n = dual_step<CHECK, INIT>(v, y, ya, kz, kza, dl.o2 + idx, S - cn, y2, sigma, copy_anchor, halp,
-                                              lamd, a);
-    if (v.step2) {
+    const double c2 = 2.0 * cn - c_old;   // reflected c
+    double y1n, y2n;
+    if (NEP_INLINE_REFLECT) {
+      y1n = dual_step_refl<CHECK, INIT>(v, y, ya, dl.o1 + idx, Sr - v.M * c2, y1, sigma, copy_anchor, halp, lamd, a);
+      y2n = dual_step_refl<CHECK, INIT>(v, y, ya, dl.o2 + idx, Sr - c2, y2, sigma, copy_anchor, halp, lamd, a);
+    } else {
+      y1n = dual_step<CHECK, INIT>(v, y, ya, kz, kza, dl.o1 + idx, S - v.M * cn, y1, sigma, copy_anchor, halp, lamd, a);
+      y2n = dual_step<CHECK, INIT>(v, y, ya, kz, kza, dl.o2 + idx, S - cn, y2, sigma, copy_anchor, halp, lamd, a);
+    }
+    if (v.step2 && !NEP_INLINE_REFLECT) {
       const double mfn = primal_step<CHECK>(v, zi, zia, lb, ub, il.omf + idx, csd * v.cost_int[il.omf + idx] - yd1, taud,
                                             copy_anchor, halp, lamd, a, true);
       const double mtn = primal_step<CHECK>(v, zi, zia, lb, ub, il.omt + idx, csd * v.cost_int[il.omt + idx] - yd2, taud,
                                             copy_anchor, halp, lamd, a, true);
       dual_step<CHECK, INIT>(v, y, ya, kz, kza, dl.oD1 + idx, mfn - cn, yd1, sigma, copy_anchor, halp, lamd, a, true);
       dual_step<CHECK, INIT>(v, y, ya, kz, kza, dl.oD2 + idx, mtn + cn, yd2, sigma, copy_anchor, halp, lamd, a, true);
+    } else if (v.step2) {
+      const double mf_old = zi[il.omf + idx], mt_old = zi[il.omt + idx];
+      const double mfn = primal_step<CHECK>(v, zi, zia, lb, ub, il.omf + idx, csd * v.cost_int[il.omf + idx] - yd1, taud,
+                                            copy_anchor, halp, lamd, a, true);
+      const double mtn = primal_step<CHECK>(v, zi, zia, lb, ub, il.omt + idx, csd * v.cost_int[il.omt + idx] - yd2, taud,
+                                            copy_anchor, halp, lamd, a, true);
+      dual_step_refl<CHECK, INIT>(v, y, ya, dl.oD1 + idx, (2.0 * mfn - mf_old) - c2, yd1, sigma, copy_anchor, halp,
+                                  lamd, a, true);
+      dual_step_refl<CHECK, INIT>(v, y, ya, dl.oD2 + idx, (2.0 * mtn - mt_old) + c2, yd2, sigma, copy_anchor, halp,
+                                  lamd, a, true);
     }
     kty[(int64_t)f * NP + j] = (float)(y1n + y2n);
     np_[j] = cn;                 // node_pass forms the memory share mem_f * c itself
@@ -1696,7 +1772,7 @@ static hipError_t launch_x_tw(const DeviceView &v, const int32_t *slots, int nsl
                               bool first, bool plain, int it, hipStream_t s) {
   dim3 grid(8 * ((v.F * nslots + 7) / 8)), block(kWave * TW);
   const size_t lds = (size_t)(2 * TW + 2) * v.NP * sizeof(float) +
-                    (check ? (size_t)2 * TW * v.NP * sizeof(float) + 4 * v.NP * sizeof(double) : 0);
+                    (check ? (size_t)(NEP_INLINE_REFLECT ? 3 : 2) * TW * v.NP * sizeof(float) + 4 * v.NP * sizeof(double) : 0);
   const int pl = plain ? 1 : 0;
   // non-temporal routing streams only when the iterating slots' x + anchor exceed ~160 MB (see ld_x4)
   const int nt = (double)nslots * 2.0 * (double)v.sx * sizeof(float) > 160e6 ? 1 : 0;
@@ -1720,7 +1796,7 @@ static hipError_t launch_x_tw(const DeviceView &v, const int32_t *slots, int nsl
 static int tile_waves(const DeviceView &v, int nslots, bool check) {
   int tw = 4;
   while (tw < 16 && (int64_t)nslots * v.F * tw < 4096) tw *= 2;
-  while (check && tw > 4 && (size_t)(4 * tw + 2) * v.NP * sizeof(float) + 4 * v.NP * sizeof(double) > 144 * 1024)
+  while (check && tw > 4 && (size_t)((NEP_INLINE_REFLECT ? 5 : 4) * tw + 2) * v.NP * sizeof(float) + 4 * v.NP * sizeof(double) > 144 * 1024)
     tw /= 2;
   return tw;
 }
