@@ -11,8 +11,8 @@
 //   aent  [R][kAnchorK] (j, value) pairs of the anchor rows held sparse
 //   mask  [F][NP] u8    destination j allowed for function f at this node (c_ub[f,j] > 0)
 //   zi    [n_int] f64   small primal: c, (mf, mt, a, d), n        + anchor zia, bounds lb/ub
-//   y     [n_dual] f64  duals of the dualised rows   + anchor ya, activity kz (iterate) / kza (anchor) — the
-//                       activities of the node and scalar rows only (C1/C2/D1/D2 reflect in x_pass)
+//   y     [n_dual] f64  duals of the dualised rows   + anchor ya, activity kz (iterate) / kza (anchor) (built with
+//                       NEP_INLINE_REFLECT, C1/C2/D1/D2 reflect in x_pass and leave theirs unused)
 //   kty   [F*NP + NP + 4] f32  packed duals the x pass needs: y1+y2 per (f,j), y5 per j, yS
 //   tpart [F][NTS] f64  per-function scalars of the rows (score row, objective, Lagrangian, movement)
 //   npart [F][2][NP] f64 per-(function, node) shares of the node rows: c (memory = mem_f * c), CPU

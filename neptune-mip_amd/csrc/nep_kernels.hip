@@ -9,10 +9,10 @@
 // ("plain" iterations take w' = T(w): the certificate iteration and the one before it, so the
 // certificate's dual is a T output and satisfies the row sign constraints).
 // K·[x̂, ẑ] is produced in the same passes that write the iterate (column sums, CPU sums, score
-// row).  The per-(f, j) rows C1/C2/D1/D2 form the reflected activity K(2ŵ − w) in the pass itself
-// (x_pass sums m (2x̂ − x̄) per column and holds the old and new c / moved in registers); the node
-// and scalar rows keep the iterate's activity K w in `kz` (the anchor's in `kza`, K is linear), so
-// K(2ŵ − w) = 2·Kŵ − Kw costs no extra pass there either.
+// row); the iterate's activity K w is kept in `kz` (the anchor's in `kza`, K is linear), so
+// K(2ŵ − w) = 2·Kŵ − Kw costs no extra pass.  Built with NEP_INLINE_REFLECT, the per-(f, j) rows
+// C1/C2/D1/D2 form K(2ŵ − w) in x_pass itself instead (column sums of m (2x̂ − x̄), old and new c /
+// moved in registers) and skip their kz / kza.
 //
 // Launches per iteration: x_pass (one workgroup per (function f, LP slot): all routing rows of f,
 // then the per-(f,j) variables c / moved_from / moved_to and rows C1/C2/D1/D2 of that f) and
