@@ -131,23 +131,33 @@ def _dnf_probe(N, F, seed, fix, seconds):
             % ([PKG, REPO], N, F, seed, N, N, F, seed, F, N, fix, fix, seconds))
     t0 = time.perf_counter()
     out = {"seconds_budget": seconds, "stage": "model build"}
-    try:
-        r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=seconds + 5)
-        lines = r.stdout.splitlines()
-        for ln in lines:
+
+    def parse(text):
+        # (a child killed at the budget still reports the stage it reached: its stdout up to the kill)
+        if isinstance(text, bytes):
+            text = text.decode(errors="replace")
+        for ln in (text or "").splitlines():
             if ln.startswith("built"):
                 out["stage"] = "HiGHS LP"
                 out["build_s"] = float(ln.split()[-1])
             if ln.startswith("solved"):
                 _, st, obj, sec = ln.split()
                 out.update(lp_status=int(st), lp_seconds=float(sec))
-        out["finished"] = out.get("lp_status") == 0
-    except subprocess.TimeoutExpired:
-        out["finished"] = False
+    try:
+        r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=seconds + 5)
+        parse(r.stdout)
+    except subprocess.TimeoutExpired as e:
+        parse(e.stdout)
+    out["finished"] = out.get("lp_status") == 0
     out["wall_s"] = time.perf_counter() - t0
+    if "build_s" in out:
+        # HiGHS seconds reached: the wall after the build, or its own time_limit status when it returned
+        out["highs_s"] = out.get("lp_seconds", out["wall_s"] - out["build_s"])
     if not out["finished"]:
         out["note"] = (f"DNF > {seconds:.0f} s: the {N}x{F} node LP ({N * N * F:,} routing columns) reached "
-                       f"'{out['stage']}' and had not finished")
+                       f"'{out['stage']}' and had not finished"
+                       + (f" (model built in {out['build_s']:.1f} s, then {out['highs_s']:.1f} s of HiGHS)"
+                          if "build_s" in out else ""))
     return out
 
 
@@ -202,6 +212,7 @@ def cpu_baseline(N, F, seed, fix, budget, workers):
     n_l, f_l, t_l, _ = pts[-1]
     scale = ((N * N * F) / (n_l * n_l * f_l)) ** p_exp
     # pool throughput at the largest measured size
+    # (os.cpu_count() on the GPU box is the whole machine's; its share for this job is 16 CPUs)
     w = max(1, min(workers, os.cpu_count() or 1))
     m, bnds = model_and_bounds(n_l, f_l, w, seed + 1)
     sts, _, wall, w_used = lp_batch_cpu(m, bnds, workers=w)
@@ -218,6 +229,7 @@ def cpu_baseline(N, F, seed, fix, budget, workers):
                  p_exp, min(3, len(pts)), t_l * scale, N, F, w_used, len(sts), n_l, f_l, wall, pool_lps, scale,
                  N, F, N, F, dnf.get("note", "one node LP solved by HiGHS in %.1f s" % dnf.get("lp_seconds", 0.0))))
     return {"value": value, "unit": "LP-relaxations/s", "cores": w_used, "kind": "port", "sample": sample,
+            "host_cpu_count": os.cpu_count(), "worker_processes": w_used,
             "extrapolated": True, "pool_lp_per_s_at": {"nodes": n_l, "functions": f_l, "value": pool_lps},
             "dnf_at_bench_size": dnf,
             "measured": [{"nodes": a, "functions": b, "seconds": t, "status": s} for a, b, t, s in pts]}

@@ -92,7 +92,7 @@ class SparseRouting:
                            minlength=self.N)
 
 
-def repair_cpu(x, W, cpr, cores, c_open, coef=None, floor=1.0, max_moves=100000):
+def repair_cpu(x, W, cpr, cores, c_open, coef=None, floor=1.0, max_moves=100000, score_room=None):
     """Make a leaf's routing meet the reference checker's CPU rows at an ABSOLUTE tolerance.
 
     The engine certifies C5 relative to the row norm; the reference's offline checker
@@ -108,6 +108,10 @@ def repair_cpu(x, W, cpr, cores, c_open, coef=None, floor=1.0, max_moves=100000)
     c_open  [F, N] bool: the leaf's c
     coef    coef(f, i, j) -> the per-unit objective (or score-row) coefficient of x[i, f, j]
             (broadcasting arrays); None: every move costs 0
+    score_room  step 2: how far the score / delay row (constraints_step2.py:57-88) may still rise,
+            rhs + 1e-6 - activity (the reference checker's tolerance, efttc/utils/constraints_step2.py:
+            55-95), with `coef` that row's x coefficients: a move is admissible only while the summed
+            coefficient change of all moves stays within it (None: no such row)
     Returns (SparseRouting, sum of t * (coef(j') - coef(j)) over the moves, ok); ok = False when an
     overloaded node has no admissible move left (the routing is returned as far as repaired)."""
     F, N = x.F, x.N
@@ -155,9 +159,15 @@ def repair_cpu(x, W, cpr, cores, c_open, coef=None, floor=1.0, max_moves=100000)
             dc = np.zeros((ks.size, N)) if coef is None else \
                 np.asarray(coef(fk[:, None], ik[:, None], jj[None, :]), np.float64) - \
                 np.asarray(coef(fk, ik, np.full(ks.size, j)), np.float64)[:, None]
+            tt = np.minimum(cap2, ((cpu[j] - lim[j]) / relief)[:, None])     # the move each candidate would make
+            if score_room is not None:
+                adm &= (dc <= 0.0) | (tt * dc <= max(0.0, score_room - delta))
+                if not adm.any():
+                    ok = False
+                    break
             score = np.where(adm, dc / relief[:, None], np.inf)
             a, jd = np.unravel_index(int(np.argmin(score)), score.shape)
-            t = min(float(cap2[a, jd]), (cpu[j] - lim[j]) / relief[a])
+            t = float(tt[a, jd])
             k, f, i = int(ks[a]), int(fk[a]), int(ik[a])
             val[k] -= t
             key = (int(row[k]), int(jd))

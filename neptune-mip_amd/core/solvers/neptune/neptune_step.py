@@ -108,13 +108,19 @@ class NeptuneStepBase(Solver):
 
         def repair(x, z):
             c_open = np.asarray(z[c0:c1], np.float64).reshape(F, N) > 0.5
+            room = self.score_room(x, z, layout)
             x2, dpref, ok = repair_cpu(x, d.workload_matrix, d.core_per_req_matrix, d.node_cores_matrix, c_open,
-                                       coef=pref)
+                                       coef=pref, score_room=room)
             dobj = 0.0
             if obj is not None and x2 is not x:
                 dobj = dpref if obj is pref else _routing_delta(x, x2, obj)
             return x2, dobj, ok
         return repair
+
+    def score_room(self, x, z, layout):
+        """Step 2: rhs + 1e-6 - activity of the score / delay row at (x, z), the room the CPU repair's
+        moves may use (None: no such row over x)"""
+        return None
 
     def solve(self):
         self.init_objective()
@@ -461,6 +467,25 @@ class NeptuneStep2Base(NeptuneStepBase):
             md = np.maximum(np.asarray(d.max_delay_matrix, np.float64)[:, None], D.max(axis=0)[None, :])   # [f, i]
             return None, _delay_coef(d, (1 - self.alpha) * W / md)
         return None, None
+
+    def score_room(self, x, z, layout):
+        # D6 (MinDelay, constraints_step2.py:57-69): sum D W x <= soften * prev delay; D7 (MDU, :76-88):
+        # alpha / N sum n + sum (1 - alpha) W D / max(maxdelay, max_k D[k, i]) x <= soften * max_score;
+        # the checker allows + 1e-6 (efttc/utils/constraints_step2.py:68, :95).  D5 (MU) has no x.
+        _, pref = self.routing_coef()
+        if pref is None:
+            return None
+        d = self.data
+        i, f, j, v = x.entries() if hasattr(x, "entries") else SparseRouting.from_dense(x).entries()
+        act = float(np.sum(np.asarray(pref(f, i, j), np.float64) * v))
+        if self.VARIANT == "MinDelay":
+            rhs = self.soften_step1_sol * self.model_kwargs().get("prev_network_delay", 0.0)
+        else:
+            rhs = float(getattr(d, "max_score", 0.0) or 0.0) * self.soften_step1_sol
+            nr = layout.get("n")
+            if nr is not None:
+                act += self.alpha / len(d.nodes) * float(np.sum(np.asarray(z[nr[0]:nr[1]], np.float64)))
+        return rhs + 1e-6 - act
 
     def results(self):
         # neptune_step2.py:43-51: no side effects on data (the prints are logs only)

@@ -86,6 +86,7 @@ struct Model {
   IntLayout il{};
   std::vector<int> row_f, row_src, frow;
   std::vector<float> row_m, row_w, row_wobj, row_wsc;
+  std::vector<double> row_wsc_d;    // the score-row weights in fp64 (presolve's proofs; row_wsc is the kernels' fp32)
   std::vector<RowInfo> rows;
   std::vector<double> W;            // [F*N]
   std::vector<double> nat_lb, nat_ub, cost_int;
@@ -126,6 +127,7 @@ struct Model {
   double *d_prm = nullptr;      // {tol, cutoff} of the LPs in flight (DeviceView::prm)
   double prm_host[3] = {0, 0, 0};   // tol, cutoff, gap tol of the LPs in flight
   int32_t *d_slots = nullptr;   // the slots currently iterating (mirror of `act`)
+  int32_t *h_act = nullptr;     // pinned staging of `act` for the d_slots upload (launch_block only)
   int32_t *d_new = nullptr;     // slots being initialised by nep_lp_submit
   double *d_base_lb = nullptr, *d_base_ub = nullptr;
   uint8_t *d_base_mask = nullptr;
@@ -163,6 +165,7 @@ struct Model {
     if (stream) (void)hipStreamSynchronize(stream);
     if (aux) (void)hipStreamSynchronize(aux);
     if (h_ctrl) (void)hipHostFree(h_ctrl);
+    if (h_act) (void)hipHostFree(h_act);
     for (void *p : allocs) (void)hipFree(p);
     for (hipGraphExec_t g : block_graph)
       if (g) (void)hipGraphExecDestroy(g);
@@ -281,16 +284,19 @@ int build(Model &m, const nep_model_desc &d) {
     for (int i = 0; i < N; ++i) colmaxD[i] = std::max(colmaxD[i], D[(size_t)k * N + i]);
   m.row_wobj.resize(m.R);
   m.row_wsc.resize(m.R);
+  m.row_wsc_d.assign(m.R, 0.0);
   for (int r = 0; r < m.R; ++r) {
     m.row_wobj[r] = (float)(kobj * m.row_w[r]);
     double wsc = 0.0;
     if (m.step2 && m.row_src[r] >= 0) {
       const int f = m.row_f[r], i = m.row_src[r];
-      if (d.variant == NEP_MIN_DELAY) wsc = m.row_w[r];
+      const double wd = m.W[(size_t)f * N + i];
+      if (d.variant == NEP_MIN_DELAY) wsc = wd;
       else if (d.variant == NEP_MIN_DELAY_AND_UTILIZATION)
-        wsc = (1.0 - d.alpha) * m.row_w[r] / std::max(d.max_delay[f], colmaxD[i]);
+        wsc = (1.0 - d.alpha) * wd / std::max(d.max_delay[f], colmaxD[i]);
     }
     m.row_wsc[r] = (float)wsc;
+    m.row_wsc_d[r] = wsc;
     if (wsc != 0.0) m.score_x = true;
   }
   if (m.score_x) m.Dh.assign(D, D + (size_t)N * N);
@@ -667,6 +673,8 @@ int setup_dense(Model &m, const nep_model_desc &d) {
     void *h = nullptr;
     if (hipHostMalloc(&h, sizeof(Ctrl) * B) != hipSuccess) return fail(NEP_ERR_NOMEM, "hipHostMalloc (Ctrl)");
     m.h_ctrl = static_cast<Ctrl *>(h);
+    if (hipHostMalloc(&h, sizeof(int32_t) * B) != hipSuccess) return fail(NEP_ERR_NOMEM, "hipHostMalloc (act)");
+    m.h_act = static_cast<int32_t *>(h);
   }
   if ((rc = dalloc(m, &m.d_prm, 3))) return rc;
   v.prm = m.d_prm;
@@ -750,7 +758,7 @@ static double score_row_xmin(const Model &m, const uint8_t *allow, int ld) {
   const int N = m.N;
   double xmin = 0.0;
   for (int r = 0; r < m.R; ++r) {
-    const double w = m.row_wsc[r];
+    const double w = m.row_wsc_d[r];   // fp64: a proof of infeasibility must not rest on fp32 rounding
     if (w == 0.0) continue;
     const double *Dr = &m.Dh[(size_t)m.row_src[r] * N];
     const uint8_t *al = allow + (size_t)m.row_f[r] * ld;
@@ -1029,8 +1037,7 @@ int submit(Model &m, int n, const int32_t *slots, const double *lbi, const doubl
   // the new slots join the block after the one in flight: `stream` waits for their initialisation
   HIPCHK(hipEventRecord(m.ev_aux, m.aux));
   HIPCHK(hipStreamWaitEvent(m.stream, m.ev_aux, 0));
-  m.act.insert(m.act.end(), fresh.begin(), fresh.end());
-  HIPCHK(hipMemcpyAsync(m.d_slots, m.act.data(), m.act.size() * sizeof(int32_t), hipMemcpyHostToDevice, m.stream));
+  m.act.insert(m.act.end(), fresh.begin(), fresh.end());   // (d_slots follows at the next launch_block)
   HIPCHK(hipStreamSynchronize(m.aux));   // (the uploads above read host vectors that end with this call)
   return NEP_OK;
 }
@@ -1086,6 +1093,12 @@ int launch_block(Model &m) {
   const int na = (int)m.act.size();
   const int sample_it = (ce >= 4 && m.blocks % 4 == 0) ? 2 : -1;
   m.blocks += 1;
+  // the iterating slots for the kernels (read at run time, so the cached graphs replay for any set):
+  // staged through pinned memory, rewritten only here — every earlier upload has completed, since a
+  // block is launched only once the previous one was waited for (advance) — so no queued copy reads a
+  // host buffer that the caller's next submit may reallocate (round-3 ADVICE)
+  std::copy(m.act.begin(), m.act.end(), m.h_act);
+  HIPCHK(hipMemcpyAsync(m.d_slots, m.h_act, na * sizeof(int32_t), hipMemcpyHostToDevice, m.stream));
   bool eager = sample_it >= 0 || !m.graphs_ok;
   if (!eager) {
     hipGraphExec_t g = nullptr;
@@ -1160,9 +1173,6 @@ int advance(Model &m, int min_done, int32_t *n_done, int32_t *done, double *obj,
       for (int s : m.act)
         if (!fin[s]) still.push_back(s);
       m.act.swap(still);
-      if (!m.act.empty())
-        HIPCHK(hipMemcpyAsync(m.d_slots, m.act.data(), m.act.size() * sizeof(int32_t), hipMemcpyHostToDevice,
-                              m.stream));
     }
     // the next block runs while the caller handles the finished slots — unless more than
     // pipe_max_done slots just finished and the call returns: then the caller's refill joins the
@@ -1446,6 +1456,9 @@ int nep_lp_copy_state(void *model, int32_t src, int32_t dst) {
   Model &m = *static_cast<Model *>(model);
   if (src < 0 || dst < 0 || src >= m.max_batch || dst >= m.max_batch) return fail(NEP_ERR_ARG, "slot out of range");
   if (m.busy[dst]) return fail(NEP_ERR_STATE, "destination slot is still iterating");
+  // (the copy runs on the aux stream, not ordered after the block in flight: an iterating source would
+  // be read while the block rewrites it)
+  if (m.busy[src]) return fail(NEP_ERR_STATE, "source slot is still iterating");
   if (src == dst) return NEP_OK;
   const DeviceView &v = m.v;
   HIPCHK(hipMemcpyAsync(v.x + dst * v.sx, v.x + src * v.sx, v.sx * sizeof(float), hipMemcpyDeviceToDevice, m.aux));

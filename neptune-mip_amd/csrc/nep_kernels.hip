@@ -914,7 +914,18 @@ void x_pass(DeviceView v, const int32_t *__restrict__ slots, int plain, int it, 
       lWd[j] = Ud;
     }
     __syncthreads();
-    if (wave == 0) pooled_shift(v, slot, f, lSd, lPm, lane);
+    if (wave == 0) {
+      pooled_shift(v, slot, f, lSd, lPm, lane);
+      // the certificate's point is the STORED iterate (this plain iteration's x̂): the pooled row takes
+      // the shifted flows, so the routing a caller reads back (nep_lp_get_rows / routing entries) is
+      // the point the certificate checked, not one kShiftMax short of it on a column.  Unshifted
+      // entries rewrite the same value: (float)((m * x̂) / m) == x̂ exactly (the product is exact in fp64).
+      const int rp = r0 + nrows - 1;
+      if (nrows > 0 && v.rows[rp].src < 0) {
+        const double mp = v.rows[rp].m;
+        for (int j = lane; j < N; j += kWave) x[(int64_t)rp * NP + j] = (float)(lPm[j] / mp);
+      }
+    }
     __syncthreads();
   }
 

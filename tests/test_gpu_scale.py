@@ -20,6 +20,7 @@ from scale_util import case_model_args, check_step1_solution, gap, node_bounds, 
 pytestmark = pytest.mark.gpu
 TOL = 1e-6
 SOLVE_TOL = 5e-7      # certificate tolerance of the solves: below the 1e-6 parity bar
+C4_TOL = 2e-5         # fp32 routing rows: |sum_j x - 1| of the stored state (see _full_size_check)
 CASES = scale_cases()
 
 
@@ -109,17 +110,21 @@ def _full_size_check(payload, variant, fixings=0, seed=0):
             boxes += [(lb[b], ub[b]) for b in range(fixings)]
         for b in range(B):
             st = int(rr["status"][0]) if b == 0 else int(r2["status"][b - 1])
-            if st != LP_OPTIMAL:
-                continue
+            its = int(rr["iters"][0]) if b == 0 else int(r2["iters"][b - 1])
+            assert st == LP_OPTIMAL, f"LP {b}: status {st} after {its} iterations (every full-size LP must certify)"
             obj = float(rr["obj"][0]) if b == 0 else float(r2["obj"][b - 1])
             pobj = float(rr["primal_obj"][0]) if b == 0 else float(r2["primal_obj"][b - 1])
             xb, rf, rs = m.rows(b)
             z, _ = m.solution(b, dense_x=False)
             viol, worst, hobj = check_step1_solution(data, variant, alpha, xb, rf, rs, z, *boxes[b])
+            print(f"LP {b}: {its} iterations, host fp64 re-check: worst row violation {worst:.2e} (C4 {viol['C4']:.2e})",
+                  {k: f"{v:.1e}" for k, v in viol.items()})
             assert obj <= pobj + 1e-12, (obj, pobj)
             assert pobj - obj <= TOL * max(1.0, abs(obj)), (obj, pobj)
-            assert viol["C4"] <= 2e-5, viol
-            assert worst <= 1e-5, viol
+            # C4 (sum_j x = 1) is the fp32 routing state itself: the projection's fp32 threshold leaves each
+            # row sum within a few fp32 ulps of the row's values (C4_TOL); every other row family at 1e-6
+            assert viol["C4"] <= C4_TOL, viol
+            assert worst <= TOL, viol
             assert abs(hobj - pobj) <= 1e-6 * max(1.0, abs(pobj)), (hobj, pobj)
         return rr
     finally:
@@ -194,7 +199,8 @@ def test_full_size_alibaba_1024x512_step2_create():
             z, _ = m.solution(b, dense_x=False)
             viol, worst, hobj = check_step2_solution(data, "MinDelayAndUtilization", 0.5, "create", 0.005, xb, rf, rs,
                                                      z, *boxes[b])
-            assert viol["C4"] <= 2e-5 and worst <= 1e-5, (b, viol)
+            print(f"LP {b}: host fp64 re-check: worst {worst:.2e} (C4 {viol['C4']:.2e})")
+            assert viol["C4"] <= C4_TOL and worst <= TOL, (b, viol)
             assert abs(hobj - pobj) <= 1e-6 * max(1.0, abs(pobj)), (b, hobj, pobj)
     finally:
         m.close()

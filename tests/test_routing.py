@@ -141,3 +141,29 @@ def test_repair_cpu_noop_and_infeasible():
     tiny = x.cpu_usage(W, cpr) * (1 - 1e-3)                  # every node overloaded: nowhere to move
     _, _, ok = repair_cpu(x, W, cpr, tiny, c_open)
     assert not ok
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_repair_cpu_keeps_step2_score_row(seed):
+    """Step 2 (round-3 ADVICE): with the score / delay row's coefficients as `coef` and its room
+    rhs + 1e-6 - activity (constraints_step2.py:57-88; the checker's tolerance,
+    efttc/utils/constraints_step2.py:68, :95), the moves never raise the row beyond that room; with no
+    room left only moves that lower it are taken, and ok = False when none is admissible."""
+    from core.engine.routing import repair_cpu
+    x, W, cpr, cores, c_open = _overloaded(seed)
+    N = x.N
+    D = np.random.default_rng(seed + 7).integers(1, 40, size=(N, N)).astype(float)
+    coef = lambda f, i, j: W[f, i] * D[i, j]
+    d0 = np.asarray(x)
+    x_free, delta_free, ok_free = repair_cpu(x, W, cpr, cores, c_open, coef=coef)
+    assert ok_free
+    room = 0.5 * max(delta_free, 0.0)
+    x2, delta, ok = repair_cpu(x, W, cpr, cores, c_open, coef=coef, score_room=room)
+    d1 = np.asarray(x2)
+    ref = float(np.einsum("ifj,fi,ij->", d1 - d0, W, D))
+    assert abs(delta - ref) <= 1e-12 * max(1.0, abs(ref))
+    assert delta <= room + 1e-12                                 # the row's room is respected
+    if ok:
+        assert np.all(np.einsum("ifj,fi,fj->j", d1, W, cpr) <= cores)
+    _, delta0, _ = repair_cpu(x, W, cpr, cores, c_open, coef=coef, score_room=0.0)
+    assert delta0 <= 1e-12                                        # no room: only non-increasing moves
