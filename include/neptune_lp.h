@@ -32,12 +32,23 @@
 extern "C" {
 #endif
 
-#define NEP_API_VERSION 6
+#define NEP_API_VERSION 7
 
 /* variants: neptune.py:41-66 (NeptuneMinDelay / MinUtilization / MinDelayAndUtilization) */
 enum { NEP_MIN_DELAY = 0, NEP_MIN_UTILIZATION = 1, NEP_MIN_DELAY_AND_UTILIZATION = 2 };
 /* steps: neptune_step1.py (step 1), neptune_step2.py mode="delete" / "create" */
 enum { NEP_STEP1 = 1, NEP_STEP2_DELETE = 2, NEP_STEP2_CREATE = 3 };
+/* API 7, nep_model_desc.relaxation: which LP the model iterates.
+ *   NEP_RELAX_REFERENCE  the reference's own LP relaxation (constraints_step1.py / constraints_step2.py rows
+ *                        as built, big-M pairs included): the LP SCIP solves at a B&B node
+ *   NEP_RELAX_FACILITY   step 1 (MinUtilization / MinDelayAndUtilization) only: a STRENGTHENED relaxation
+ *                        for branch-and-bound bounds: x[i,f,j] <= c[f,j] for every routing
+ *                        row and c[f,j] <= n[j] (valid for every integral placement: constraints_step1.py:5-15,
+ *                        :69-78 with c, n binary) replace the big-M pairs C1/C2 and C6/C7, which they imply
+ *                        for integral c, n (C2 and C7, the eps floors, are relaxed).  Same variables, z_int and
+ *                        objective; C3 memory, C4, C5 CPU and C8 kept.  Its bound is valid for the MIP, not
+ *                        equal to the reference LP's */
+enum { NEP_RELAX_REFERENCE = 0, NEP_RELAX_FACILITY = 1 };
 
 enum { NEP_OK = 0, NEP_ERR_ARG = -1, NEP_ERR_HIP = -2, NEP_ERR_NOMEM = -3, NEP_ERR_STATE = -4 };
 
@@ -75,6 +86,7 @@ typedef struct {
   double node_budget;          /* (input_to_data.py:187: 300) */
   const double *max_delay;     /* [F] max_delay_matrix (input_to_data.py:136: 1000) */
   const double *old_allocations; /* [F*N] step 2 only (0/1) */
+  int32_t relaxation;          /* API 7: NEP_RELAX_REFERENCE (0) or NEP_RELAX_FACILITY */
 } nep_model_desc;
 
 typedef struct {

@@ -26,6 +26,14 @@ Warm starts: every node LP after the root starts from its parent's final PDHG st
 parent's slot still holds it (slots are reused least-recently-finished first), else from the
 root's, kept in a reserved slot (SCIP warm-starts its node LPs from the parent basis the same way).
 
+Strengthened bounds (round 4): with `bound_lp` (an LPModel of the facility relaxation,
+NEP_RELAX_FACILITY: x[i,f,j] <= c[f,j] and c[f,j] <= n[j] in place of the big-M pairs, valid for every
+integral placement) the branching nodes' LPs run on that model and give the search its bounds, flows and
+rounding input; leaves (every c and n fixed) still run on the reference model `lp`, whose certified LP is
+the incumbent (its point is feasible for the reference's rows, C2's eps floors included).  The two models
+iterate on their own HIP streams side by side; leaves warm-start from the reference root LP's state,
+solved beside the first bound LPs.
+
 Multi-GPU (core/engine/comm.py, one rank per GPU): every rank runs the same search
 redundantly until the open-node frontier holds `world * batch` nodes, then keeps the frontier nodes
 whose canonical position is its rank modulo `world` and searches those subtrees alone.  Every loop
@@ -47,8 +55,8 @@ from .lp import LP_BOUND, LP_CUTOFF, LP_INFEASIBLE, LP_ITERATION_LIMIT, LP_OPTIM
 OPTIMAL, INFEASIBLE, LIMIT = "OPTIMAL", "INFEASIBLE", "LIMIT"
 _STATUS_NAME = {LP_OPTIMAL: "certified", LP_ITERATION_LIMIT: "limit", LP_INFEASIBLE: "infeasible",
                 LP_CUTOFF: "cutoff", LP_BOUND: "bound"}
-NODE, LEAF, RETRY = 0, 1, 2
-_KIND_NAME = {NODE: "node", LEAF: "leaf", RETRY: "retry"}
+NODE, LEAF, RETRY, REFROOT = 0, 1, 2, 3
+_KIND_NAME = {NODE: "node", LEAF: "leaf", RETRY: "retry", REFROOT: "refroot"}
 
 
 class BnBResult:
@@ -74,7 +82,7 @@ class BnBResult:
         # node-LP mix: finished LPs per engine status (+ presolve-infeasible submits) and their iterations
         self.lp_status = {"certified": 0, "bound": 0, "limit": 0, "infeasible": 0, "cutoff": 0, "numerical": 0,
                           "presolve_infeasible": 0}
-        self.lp_status_kind = {k: dict.fromkeys(self.lp_status, 0) for k in ("node", "leaf", "retry")}
+        self.lp_status_kind = {k: dict.fromkeys(self.lp_status, 0) for k in ("node", "leaf", "retry", "refroot")}
         self.lp_iters = []
         self.drained = 0         # LPs still iterating at a stop decision (stopped at their next check)
         # wall seconds by phase: device waits in advance, host work per finished LP, submits (incl.
@@ -102,11 +110,30 @@ class _Node:
         self.bound, self.idx, self.val, self.kind, self.parent, self.depth = bound, idx, val, kind, parent, depth
 
 
+class _Engine:
+    """One LP model's slots: a free list of working slots, a reserved slot for its root LP's state (the
+    warm-start source of nodes whose parent's state is gone) and, on the leaf engine, one for the incumbent's;
+    per-slot generations tell a parent's state from a later occupant's."""
+
+    def __init__(self, lp, reserve, name):
+        self.lp, self.name = lp, name
+        self.reserved = reserve if lp.max_batch > reserve else 0
+        self.root_slot = lp.max_batch - 1
+        self.inc_slot = lp.max_batch - 2
+        self.gen = [0] * lp.max_batch
+        self.free = deque(range(lp.max_batch - self.reserved))
+        self.root_ready = False
+        self.inflight = 0
+
+
 class BranchAndBound:
     """Streaming best-first B&B.
 
     lp            core.engine.lp.LPModel of the step model (max_batch >= batch + 2: `batch` working
                   slots, one for the root's state, one for the incumbent's)
+    bound_lp      optional LPModel of the strengthened relaxation (NEP_RELAX_FACILITY) the branching nodes
+                  are bounded with (max_batch >= batch + 1: one slot for its root's state); None: every node
+                  LP runs on `lp`
     workload      W [F, N] (unused since the flows are reduced on the device; kept for the API)
     fn_mem/node_mem  memory data for the rounding heuristic's capacity check (C3)
     upper_bound   a-priori bound on any feasible objective: LPs whose Lagrangian exceeds it stop early
@@ -116,8 +143,9 @@ class BranchAndBound:
                  node_limit=20000, time_limit=None, upper_bound=math.inf, flow_tol=1e-4, log=None, comm=None,
                  warm=True, root_max_iters=200000, check_every=12, polish_tol=1e-8, polish_iters=20000,
                  seed_leaves=None, integer_bound=None, improve=None, repair=None, node_bound_res=1e-2,
-                 retry_res=math.inf, unit_flow_leaves=True, node_max_iters=None):
+                 retry_res=math.inf, unit_flow_leaves=True, node_max_iters=None, bound_lp=None, bound_gap=1e-4):
         self.lp = lp
+        self.two = bound_lp is not None
         self.N, self.F = lp.N, lp.F
         L = lp.layout()
         self.c0, self.c1 = L["c"]
@@ -126,7 +154,11 @@ class BranchAndBound:
         self.node_mem = np.asarray(node_mem, np.float64).reshape(self.N)
         self.reserved = 2 if lp.max_batch >= 3 else 0
         self.batch = max(1, min(int(batch), lp.max_batch - self.reserved))
-        self.warm = bool(warm) and self.reserved == 2
+        self.warm = bool(warm) and self.reserved == 2 and (bound_lp is None or bound_lp.max_batch >= 2)
+        self.bound_lp = bound_lp
+        # the bound model's LPs stop once their own gap (repaired point vs best bound) is within bound_gap:
+        # a node needs its bound, which is valid at any dual point; the leaves keep the certificate tolerance
+        self.bound_gap = bound_gap
         self.root_slot = lp.max_batch - 1
         self.inc_slot = lp.max_batch - 2
         self.tol, self.gap, self.max_iters = tol, gap, max_iters
@@ -286,7 +318,7 @@ class BranchAndBound:
             val.append(nv)
         return np.concatenate(idx), np.concatenate(val)
 
-    def _branch_var(self, node, flow, slot):
+    def _branch_var(self, node, flow, slot, lp=None):
         """n[j] receiving flow (largest inflow), then c[f,j] carrying flow (largest), then any free
         n / c by LP value (ties: lowest index).  None when every branching variable is fixed."""
         fixed = self._fixed(node)
@@ -305,77 +337,91 @@ class BranchAndBound:
             free = np.concatenate([free, np.flatnonzero(~fixed[self.n_range[0]:self.n_range[1]]) + self.n_range[0]])
         if free.size == 0:
             return None
-        z, _ = self.lp.solution(slot, dense_x=False)
+        z, _ = (lp or self.lp).solution(slot, dense_x=False)
         zf = z[free]
         return int(free[np.argmax(zf)])
 
     # ---------------------------------------------------------------------------------------
     def _submit(self, items, inc):
-        """items: [(slot, node)].  One nep_lp_submit per (warm, iteration budget) group."""
-        lp, n_int = self.lp, self.lp.n_int
+        """items: [(engine, slot, node)].  One nep_lp_submit per (engine, warm, iteration budget) group."""
         groups = {}
-        copies = []
-        for slot, node in items:
+        copies = {}
+        for eng, slot, node in items:
             warm = False
-            if self.warm and self.root_ready:
-                src = self.root_slot
+            if self.warm and eng.root_ready:
+                src = eng.root_slot
                 if node.parent is not None:
-                    ps, pg = node.parent
-                    if self.slot_gen[ps] == pg:
+                    pe, ps, pg = node.parent
+                    if pe is eng and eng.gen[ps] == pg:
                         src = ps
                 if src != slot:
-                    copies.append((src, slot))
+                    copies.setdefault(eng.name, (eng, []))[1].append((src, slot))
                 warm = True
-            budget = (self.root_max_iters if (node.kind == RETRY or not self.root_ready)
+            budget = (self.root_max_iters if (node.kind in (RETRY, REFROOT) or not eng.root_ready)
                       else (self.node_max_iters if node.kind == NODE else self.max_iters))
-            bres = self.node_bound_res if (node.kind == NODE and self.root_ready) else 0.0
-            groups.setdefault((warm, budget, bres), []).append((slot, node))
+            # (the bound model's root is a branching node like the others: it stops once its bound converged)
+            bres = self.node_bound_res if (node.kind == NODE and (eng.root_ready or self.two)) else 0.0
+            groups.setdefault((eng.name, warm, budget, bres), (eng, []))[1].append((slot, node))
         # warm-start copies: a slot that is both a parent state (source) and a new node's slot
         # (destination) is read before it is overwritten; a cycle falls back to the root's state
-        while copies:
-            srcs = {c[0] for c in copies}
-            k = next((i for i, (_, d) in enumerate(copies) if d not in srcs), None)
-            if k is None:
-                src, dst = copies[0]
-                copies[0] = (self.root_slot, dst)
-                continue
-            src, dst = copies.pop(k)
-            lp.copy_state(src, dst)
+        for eng, cps in copies.values():
+            while cps:
+                srcs = {c[0] for c in cps}
+                k = next((i for i, (_, d) in enumerate(cps) if d not in srcs), None)
+                if k is None:
+                    src, dst = cps[0]
+                    cps[0] = (eng.root_slot, dst)
+                    continue
+                src, dst = cps.pop(k)
+                eng.lp.copy_state(src, dst)
         cutoff = min(inc, self.ub0)
-        for (warm, budget, bres), its in groups.items():
+        for (_, warm, budget, bres), (eng, its) in groups.items():
+            n_int = eng.lp.n_int
             slots = np.array([s for s, _ in its], np.int32)
             lb = np.full((len(its), n_int), -np.inf)
             ub = np.full((len(its), n_int), np.inf)
             for b, (_, node) in enumerate(its):
                 lb[b, node.idx] = node.val
                 ub[b, node.idx] = node.val
-            st = lp.submit(slots, lb, ub, tol=self.tol, cutoff=cutoff if math.isfinite(cutoff) else math.inf,
-                           max_iters=budget, check_every=self.check_every, warm_start=warm, bound_res=bres)
+            gap_tol = self.bound_gap if (self.two and eng is self.B) else 0.0
+            st = eng.lp.submit(slots, lb, ub, tol=self.tol, cutoff=cutoff if math.isfinite(cutoff) else math.inf,
+                               max_iters=budget, check_every=self.check_every, warm_start=warm, bound_res=bres,
+                               gap_tol=gap_tol)
             for b, (slot, node) in enumerate(its):
-                self.slot_gen[slot] += 1
+                eng.gen[slot] += 1
                 self.res.lps += 1
                 if int(st[b]) == LP_INFEASIBLE:
                     self.res.lp_status["presolve_infeasible"] += 1
                     self.res.lp_status_kind[_KIND_NAME[node.kind]]["presolve_infeasible"] += 1
-                    self.free.append(slot)
+                    eng.free.append(slot)
                 else:
-                    self.inflight[slot] = node
+                    self.inflight[(eng.name, slot)] = node
+                    eng.inflight += 1
 
-    def _finish(self, slot, node, st, obj, pobj, iters, inc):
-        """Process one finished node LP; returns the (possibly improved) incumbent value."""
+    def _finish(self, eng, slot, node, st, obj, pobj, iters, inc):
+        """Process one finished node LP (of engine `eng`); returns the (possibly improved) incumbent value."""
         res = self.res
+        lp = eng.lp
+        eng.inflight -= 1
         res.lp_iterations += iters
         res.lp_iters.append(iters)
         res.lp_status[_STATUS_NAME.get(st, "numerical")] += 1
         res.lp_status_kind[_KIND_NAME[node.kind]][_STATUS_NAME.get(st, "numerical")] += 1
+        if node.kind == REFROOT:
+            # the reference root LP: its state warm-starts the leaves (their LPs run on this model)
+            if self.warm and st not in (LP_INFEASIBLE, LP_CUTOFF):
+                lp.copy_state(slot, eng.root_slot)
+            eng.root_ready = True
+            eng.free.append(slot)
+            return inc
         if st == LP_OPTIMAL:
             res.certified += 1
-        if not self.root_ready and node.depth == 0 and node.kind == NODE:
+        if not eng.root_ready and node.depth == 0 and node.kind == NODE:
             res.timing["root"] = time.time() - self.t0
             if self.warm and st not in (LP_INFEASIBLE, LP_CUTOFF):
-                self.lp.copy_state(slot, self.root_slot)   # every later node can start from the root
-            self.root_ready = True
-            me0 = (slot, self.slot_gen[slot])
+                lp.copy_state(slot, eng.root_slot)   # every later node can start from the root
+            eng.root_ready = True
+            me0 = (eng, slot, eng.gen[slot])
             for idx, val in self.seed_leaves:
                 idx, val = np.asarray(idx), np.asarray(val, np.float64)
                 lb = self._ibound(idx, val)
@@ -385,7 +431,7 @@ class BranchAndBound:
                         self.seen_leaves.add(key)
                         self.pending.append(_Node(lb, idx, val, LEAF, me0, 1))
         if st in (LP_INFEASIBLE, LP_CUTOFF):
-            self.free.append(slot)
+            eng.free.append(slot)
             return inc
         bound = max(node.bound, obj)
         if node.kind != NODE:
@@ -395,17 +441,18 @@ class BranchAndBound:
                     inc = pobj
                     res.objective = pobj
                     self.inc_node = node
-                    res.z, _ = self.lp.solution(slot, dense_x=False)
+                    res.z, _ = lp.solution(slot, dense_x=False)
                     if self.warm:
-                        self.lp.copy_state(slot, self.inc_slot)   # its x is fetched once, at the end
-                        res.incumbent_slot = self.inc_slot
+                        lp.copy_state(slot, eng.inc_slot)   # its x is fetched once, at the end
+                        res.incumbent_slot = eng.inc_slot
                     else:
                         if res.incumbent_slot is not None and res.incumbent_slot in self.keep:
                             self.keep.discard(res.incumbent_slot)
-                            self.free.append(res.incumbent_slot)
+                            eng.free.append(res.incumbent_slot)
                         res.incumbent_slot = slot
                         self.keep.add(slot)
-                    self.lp.set_params(self.tol, min(inc, self.ub0))
+                    for e in self.engines:
+                        e.lp.set_params(self.tol, min(inc, self.ub0))
                     self.log(f"incumbent {pobj:.10g} (lps {res.lps}, nodes {res.nodes})")
                     if self.improve is not None:
                         for idx, val in self.improve(node.idx, node.val, pobj):
@@ -414,23 +461,23 @@ class BranchAndBound:
                                 self.seen_leaves.add(key)
                                 # a neighbour is no descendant of this leaf: its bound is its own
                                 self.pending.appendleft(_Node(self._ibound(idx, val), idx,
-                                                              np.asarray(val, np.float64), LEAF, (slot, self.slot_gen[slot]),
-                                                              node.depth))
-            elif node.kind == LEAF and self.lp.diag(slot)["pres"] <= self.retry_res:
-                self.retry.append(_Node(bound, node.idx, node.val, RETRY, (slot, self.slot_gen[slot]), node.depth))
+                                                              np.asarray(val, np.float64), LEAF,
+                                                              (eng, slot, eng.gen[slot]), node.depth))
+            elif node.kind == LEAF and lp.diag(slot)["pres"] <= self.retry_res:
+                self.retry.append(_Node(bound, node.idx, node.val, RETRY, (eng, slot, eng.gen[slot]), node.depth))
             else:
                 res.unresolved += 1
                 self.unresolved_bounds.append(bound)
             if slot not in self.keep:
-                self.free.append(slot)
+                eng.free.append(slot)
             return inc
         if bound >= inc - self._gap_abs(inc):
-            self.free.append(slot)
+            eng.free.append(slot)
             return inc
         res.nodes += 1
-        flow = self.lp.flows([slot])[0]
-        me = (slot, self.slot_gen[slot])
-        z, _ = self.lp.solution(slot, dense_x=False)
+        flow = lp.flows([slot])[0]
+        me = (eng, slot, eng.gen[slot])
+        z, _ = lp.solution(slot, dense_x=False)
         for by_flow, min_flow in self.round_modes:
             leaf = self._round(node, flow, z[self.c0:self.c1], by_flow, min_flow)
             if leaf is not None:
@@ -440,7 +487,7 @@ class BranchAndBound:
                     lb = max(bound, self._ibound(*leaf))
                     if lb < inc - self._gap_abs(inc):
                         self.pending.append(_Node(lb, leaf[0], leaf[1], LEAF, me, node.depth + 1))
-        var = self._branch_var(node, flow, slot)
+        var = self._branch_var(node, flow, slot, lp)
         if var is not None:
             for v in (1.0, 0.0):
                 idx = np.append(node.idx, var)
@@ -451,7 +498,7 @@ class BranchAndBound:
                 kind = LEAF if len(idx) >= self._nb else NODE
                 heapq.heappush(self.heap, (cb, -(node.depth + 1), next(self.seq),
                                            _Node(cb, idx, val, kind, me, node.depth + 1)))
-        self.free.append(slot)        # most recently finished last: its state survives longest
+        eng.free.append(slot)        # most recently finished last: its state survives longest
         return inc
 
     def _polish(self, res):
@@ -530,13 +577,20 @@ class BranchAndBound:
         self.retry = deque()         # uncertified leaves, re-solved once with the root budget
         self.unresolved_bounds = []
         self.seen_leaves = set()
-        self.inflight = {}
+        self.inflight = {}           # (engine name, slot) -> node
         self.keep = set()
         self.inc_node = None
-        nwork = lp.max_batch - self.reserved
-        self.free = deque(range(nwork))
-        self.slot_gen = [0] * lp.max_batch
-        self.root_ready = False
+        L = _Engine(lp, self.reserved, "leaf")
+        B = L if not self.two else _Engine(self.bound_lp, 1 if self.warm else 0, "bound")
+        self.L, self.B = L, B
+        self.engines = [L] if not self.two else [B, L]
+        # two models: the reference root LP (the leaves' warm-start state) runs beside the first bound LPs
+        self.refroot = None
+        if self.two:
+            if self.warm:
+                self.refroot = _Node(-math.inf, np.zeros(0, np.int64), np.zeros(0), REFROOT, None, 0)
+            else:
+                L.root_ready = True
         sharded = comm.world == 1
         self.presplit = (0, 0, 0)
         limit_hit = False
@@ -551,7 +605,8 @@ class BranchAndBound:
                 self.presplit = (res.nodes, res.lps, res.certified)
                 sharded = True
             stop = res.nodes >= self.node_limit or bool(self.time_limit and time.time() - t0 > self.time_limit)
-            open_n = len(self.heap) + len(self.pending) + len(self.retry) + len(self.inflight)
+            busy = sum(1 for n in self.inflight.values() if n.kind != REFROOT)
+            open_n = len(self.heap) + len(self.pending) + len(self.retry) + busy
             if comm.world > 1:
                 # every rank takes the same stop / termination decision in the same loop iteration: one
                 # collective carries the incumbent (MIN), the stop flags (OR) and the open counts (SUM)
@@ -564,20 +619,40 @@ class BranchAndBound:
                 break
             # fill the free slots: retries, rounding leaves, then best-first open nodes
             items = []
-            while self.free and (self.retry or self.pending or self.heap):
-                if self.retry:
-                    node = self.retry.popleft()
-                elif self.pending:
-                    node = self.pending.popleft()
-                    if node.bound >= inc - self._gap_abs(inc):
-                        continue
-                else:
+            if not self.two:
+                while L.free and (self.retry or self.pending or self.heap):
+                    if self.retry:
+                        node = self.retry.popleft()
+                    elif self.pending:
+                        node = self.pending.popleft()
+                        if node.bound >= inc - self._gap_abs(inc):
+                            continue
+                    else:
+                        _, _, _, node = heapq.heappop(self.heap)
+                        if node.bound >= inc - self._gap_abs(inc):
+                            continue
+                    items.append((L, L.free.popleft(), node))
+                    if not L.root_ready:
+                        break                 # the root runs alone (its state warm-starts everything after)
+            else:
+                if self.refroot is not None and L.free:
+                    items.append((L, L.free.popleft(), self.refroot))
+                    self.refroot = None
+                while B.free and self.heap:
                     _, _, _, node = heapq.heappop(self.heap)
                     if node.bound >= inc - self._gap_abs(inc):
                         continue
-                items.append((self.free.popleft(), node))
-                if not self.root_ready:
-                    break                 # the root runs alone (its state warm-starts everything after)
+                    if node.kind != NODE:          # a leaf from branching: the reference model's
+                        self.pending.append(node)
+                        continue
+                    items.append((B, B.free.popleft(), node))
+                    if not B.root_ready:
+                        break
+                while L.root_ready and L.free and (self.retry or self.pending):
+                    node = self.retry.popleft() if self.retry else self.pending.popleft()
+                    if node.kind == LEAF and node.bound >= inc - self._gap_abs(inc):
+                        continue
+                    items.append((L, L.free.popleft(), node))
             tm = res.timing
             t1 = time.perf_counter()
             if items:
@@ -588,30 +663,40 @@ class BranchAndBound:
                 continue
             # before the frontier is dealt every rank must stay identical: drain each batch whole.  Under a
             # time limit the sharded loop comes back after every block, so a stop is never held up by
-            # long LPs (a leaf's retry runs the root budget)
+            # long LPs (a leaf's retry runs the root budget).  Two models: one block of each per loop (each
+            # pipelines its next block before returning, so both streams keep iterating)
             res.advance_calls += 1
-            res.inflight_sum += len(self.inflight)
-            r = lp.advance((0 if self.time_limit else 1) if sharded else len(self.inflight))
-            t3 = time.perf_counter()
-            tm["advance"] += t3 - t2
-            for i, slot in enumerate(r["slots"].tolist()):
-                node = self.inflight.pop(slot)
-                inc = self._finish(slot, node, int(r["status"][i]), float(r["obj"][i]), float(r["primal_obj"][i]),
-                                   int(r["iters"][i]), inc)
-            tm["finish"] += time.perf_counter() - t3
+            res.inflight_sum += busy
+            for eng in self.engines:
+                if eng.inflight <= 0:
+                    continue
+                if self.two:
+                    r = eng.lp.advance(0 if sharded else eng.inflight)
+                else:
+                    r = eng.lp.advance((0 if self.time_limit else 1) if sharded else eng.inflight)
+                t3 = time.perf_counter()
+                tm["advance"] += t3 - t2
+                for i, slot in enumerate(r["slots"].tolist()):
+                    node = self.inflight.pop((eng.name, slot))
+                    inc = self._finish(eng, slot, node, int(r["status"][i]), float(r["obj"][i]),
+                                       float(r["primal_obj"][i]), int(r["iters"][i]), inc)
+                t2 = time.perf_counter()
+                tm["finish"] += t2 - t3
         # drain what still iterates (a stop decision): a cutoff of -inf stops every LP in flight at its next
         # certificate check (one block), with its best Lagrangian bound, which stays valid for its node
         t_end = time.perf_counter()
-        open_bounds = [n.bound for n in self.inflight.values()]
-        res.drained = len(self.inflight)
-        if lp.active() > 0:
-            lp.set_params(self.tol, -math.inf)
-        while lp.active() > 0:
-            r = lp.advance(lp.active())
-            for i, slot in enumerate(r["slots"].tolist()):
-                node = self.inflight.pop(slot, None)
-                if node is not None and int(r["status"][i]) != LP_INFEASIBLE:
-                    open_bounds.append(max(node.bound, float(r["obj"][i])))
+        open_bounds = [n.bound for n in self.inflight.values() if n.kind != REFROOT]
+        res.drained = len(open_bounds)
+        for eng in self.engines:
+            if eng.lp.active() > 0:
+                eng.lp.set_params(self.tol, -math.inf)
+        for eng in self.engines:
+            while eng.lp.active() > 0:
+                r = eng.lp.advance(eng.lp.active())
+                for i, slot in enumerate(r["slots"].tolist()):
+                    node = self.inflight.pop((eng.name, slot), None)
+                    if node is not None and node.kind != REFROOT and int(r["status"][i]) != LP_INFEASIBLE:
+                        open_bounds.append(max(node.bound, float(r["obj"][i])))
         res.timing["drain"] = time.perf_counter() - t_end
         t_end = time.perf_counter()
         open_bounds += [h[0] for h in self.heap] + [n.bound for n in self.pending] + [n.bound for n in self.retry]

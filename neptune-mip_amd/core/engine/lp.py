@@ -18,7 +18,8 @@ STEP1, STEP2_DELETE, STEP2_CREATE = 1, 2, 3
 LP_OPTIMAL, LP_ITERATION_LIMIT, LP_INFEASIBLE, LP_CUTOFF, LP_NUMERICAL, LP_BOUND = 0, 1, 2, 3, 4, 5
 VARIANTS = {"MinDelay": MIN_DELAY, "MinUtilization": MIN_UTILIZATION,
             "MinDelayAndUtilization": MIN_DELAY_AND_UTILIZATION}
-API_VERSION = 6
+API_VERSION = 7
+RELAX_REFERENCE, RELAX_FACILITY = 0, 1
 
 _dp = ctypes.POINTER(ctypes.c_double)
 
@@ -34,7 +35,7 @@ class ModelDesc(ctypes.Structure):
                 ("big_m", ctypes.c_double), ("epsilon", ctypes.c_double),
                 ("delay", _dp), ("workload", _dp), ("core_per_req", _dp), ("function_memory", _dp),
                 ("node_memory", _dp), ("node_cores", _dp), ("node_cost", _dp), ("node_budget", ctypes.c_double),
-                ("max_delay", _dp), ("old_allocations", _dp)]
+                ("max_delay", _dp), ("old_allocations", _dp), ("relaxation", ctypes.c_int32)]
 
 
 class LpOpts(ctypes.Structure):
@@ -141,19 +142,22 @@ def _arrays(data, N, F):
     )
 
 
-def _desc(k, N, F, variant, step, alpha, soften, max_score, prev_delay, budget):
+def _desc(k, N, F, variant, step, alpha, soften, max_score, prev_delay, budget, relaxation=RELAX_REFERENCE):
     return ModelDesc(N, F, variant, step, float(alpha), float(soften), float(max_score), float(prev_delay), 1e6,
                      1e-6, _ptr(k["delay"]), _ptr(k["workload"]), _ptr(k["cpr"]), _ptr(k["fmem"]), _ptr(k["nmem"]),
-                     _ptr(k["ncores"]), _ptr(k["ncost"]), float(budget), _ptr(k["maxd"]), _ptr(k["old"]))
+                     _ptr(k["ncores"]), _ptr(k["ncost"]), float(budget), _ptr(k["maxd"]), _ptr(k["old"]),
+                     int(relaxation))
 
 
-def debug_build(data, variant, step=STEP1, alpha=0.5, soften_step1_sol=1.3, max_score=0.0, prev_network_delay=0.0):
+def debug_build(data, variant, step=STEP1, alpha=0.5, soften_step1_sol=1.3, max_score=0.0, prev_network_delay=0.0,
+                relaxation=RELAX_REFERENCE):
     """Host-only model build (no GPU needed): returns eta, rho, gam, rownorm, dims."""
     lib = load_library()
     N, F = len(data.nodes), len(data.functions)
     v = VARIANTS[variant] if isinstance(variant, str) else int(variant)
     k = _arrays(data, N, F)
-    d = _desc(k, N, F, v, int(step), alpha, soften_step1_sol, max_score, prev_network_delay, data.node_budget)
+    d = _desc(k, N, F, v, int(step), alpha, soften_step1_sol, max_score, prev_network_delay, data.node_budget,
+              relaxation)
     dims = np.zeros(4, np.int32)
     eta = np.zeros(1)
     _check(lib, lib.nep_debug_build(ctypes.byref(d), _ptr(eta), None, None, None, _ptr(dims, ctypes.c_int32)),
@@ -191,15 +195,16 @@ class LPModel:
     """One structured LP family (a reference step model) with `max_batch` device slots."""
 
     def __init__(self, data, variant, step=STEP1, alpha=0.5, soften_step1_sol=1.3, max_score=0.0,
-                 prev_network_delay=0.0, max_batch=1):
+                 prev_network_delay=0.0, max_batch=1, relaxation=RELAX_REFERENCE):
         self._lib = load_library()
         self.N = len(data.nodes)
         self.F = len(data.functions)
         self.variant = VARIANTS[variant] if isinstance(variant, str) else int(variant)
         self.step = int(step)
         self._keep = _arrays(data, self.N, self.F)
+        self.relaxation = int(relaxation)
         d = _desc(self._keep, self.N, self.F, self.variant, self.step, alpha, soften_step1_sol, max_score,
-                  prev_network_delay, data.node_budget)
+                  prev_network_delay, data.node_budget, self.relaxation)
         h = ctypes.c_void_p()
         _check(self._lib, self._lib.nep_model_create(ctypes.byref(d), int(max_batch), None, ctypes.byref(h)),
                "nep_model_create")

@@ -82,6 +82,17 @@ class NeptuneStepBase(Solver):
         """Placements to try as leaves right after the root (a B&B primal start); none by default."""
         return []
 
+    # the branching nodes' bounds come from the facility relaxation (NEP_RELAX_FACILITY: x <= c, c <= n in place
+    # of the big-M pairs; include/neptune_lp.h, DESIGN.md §7) where it exists — step 1 with n (MinUtilization,
+    # MinDelayAndUtilization); leaves stay on the reference model
+    strengthen = True
+
+    def bound_model(self, data, max_batch):
+        if not self.strengthen or self.step_id() != _lp.STEP1 or self.VARIANT == "MinDelay":
+            return None
+        return make_lp(data, self.VARIANT, self.step_id(), max_batch, relaxation=_lp.RELAX_FACILITY,
+                       **self.model_kwargs())
+
     def integer_bound(self, layout=None):
         """bound(idx, val): a lower bound on the objective of every integral completion of a node's
         fixings (+inf: none exists), or None."""
@@ -129,7 +140,9 @@ class NeptuneStepBase(Solver):
         # `batch` node LPs in flight + one slot for the root's state + one for the incumbent's
         # (core/engine/bnb.py)
         model = make_lp(data, self.VARIANT, self.step_id(), self.batch + 2, **self.model_kwargs())
+        bmodel = None
         try:
+            bmodel = self.bound_model(data, self.batch + 1)
             ub = self.upper_bound()
             bnb = BranchAndBound(model, data.workload_matrix, data.function_memory_matrix, data.node_memory_matrix,
                                  batch=self.batch, tol=self.lp_tol, max_iters=self.lp_max_iters,
@@ -139,11 +152,14 @@ class NeptuneStepBase(Solver):
                                  seed_leaves=self.seed_leaves(model.layout()), integer_bound=self.integer_bound(model.layout()),
                                  improve=self.improve(model.layout()), repair=self.routing_repair(model.layout()),
                                  node_bound_res=self.node_bound_res, unit_flow_leaves=self.unit_flow_leaves,
-                                 node_max_iters=max(1, int(self.lp_max_iters * self.node_iters_fraction)))
+                                 node_max_iters=max(1, int(self.lp_max_iters * self.node_iters_fraction)),
+                                 bound_lp=bmodel)
             res = bnb.solve()
             layout = model.layout()
         finally:
             model.close()
+            if bmodel is not None:
+                bmodel.close()
         self.result = res
         if res.objective is not None:
             self._value = float(res.objective)

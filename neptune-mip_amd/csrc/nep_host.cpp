@@ -80,6 +80,8 @@ struct Coo {
 struct Model {
   // problem
   int N = 0, F = 0, NP = 0, variant = 0, step = 1, has_n = 0, step2 = 0;
+  int fac = 0;                      // NEP_RELAX_FACILITY (include/neptune_lp.h)
+  std::vector<double> rhoL;         // fac: row scale of the x[r, j] <= c[f, j] rows, per (f, j)
   double alpha = 0.5, M = 1e6, eps = 1e-6, sigma4 = -1, cost_n = 0, score_n_coef = 0, w_dis = 0;
   int R = 0, JB = 0, CPL = 1, max_batch = 1;
   DualLayout dl{};
@@ -219,6 +221,10 @@ int build(Model &m, const nep_model_desc &d) {
   m.step = d.step;
   m.step2 = d.step != NEP_STEP1;
   m.has_n = d.variant != NEP_MIN_DELAY;
+  if (d.relaxation != NEP_RELAX_REFERENCE && d.relaxation != NEP_RELAX_FACILITY) return fail(NEP_ERR_ARG, "bad relaxation");
+  m.fac = d.relaxation == NEP_RELAX_FACILITY;
+  if (m.fac && (m.step2 || !m.has_n))
+    return fail(NEP_ERR_ARG, "the facility relaxation is a step-1 MinUtilization / MinDelayAndUtilization model");
   m.alpha = d.alpha;
   m.M = d.big_m > 0 ? d.big_m : 1e6;
   m.eps = d.epsilon > 0 ? d.epsilon : 1e-6;
@@ -362,12 +368,13 @@ int build(Model &m, const nep_model_desc &d) {
   // dual layout + row bounds
   DualLayout &dl = m.dl;
   int o = 0;
-  dl.o1 = o; o += FN;
-  dl.o2 = o; o += FN;
+  dl.o1 = dl.o2 = dl.oQ = -1;
+  if (!m.fac) { dl.o1 = o; o += FN; dl.o2 = o; o += FN; }
   dl.o3 = o; o += N;
   dl.o5 = o; o += N;
   dl.o6 = dl.o7 = dl.oD1 = dl.oD2 = dl.oD3a = dl.oD3b = dl.oD4 = dl.oS = -1;
-  if (m.has_n) { dl.o6 = o; o += N; dl.o7 = o; o += N; }
+  if (m.fac) { dl.oQ = o; o += FN; }   // c[f, j] - n[j] <= 0
+  else if (m.has_n) { dl.o6 = o; o += N; dl.o7 = o; o += N; }
   if (m.step2) {
     dl.oD1 = o; o += FN;
     dl.oD2 = o; o += FN;
@@ -376,14 +383,15 @@ int build(Model &m, const nep_model_desc &d) {
   dl.n_dual = o;
   m.lo.assign(o, -INF);
   m.hi.assign(o, INF);
-  for (int k = 0; k < FN; ++k) {
+  for (int k = 0; k < FN && !m.fac; ++k) {
     m.hi[dl.o1 + k] = 0.0;
     m.lo[dl.o2 + k] = -m.eps;
   }
+  for (int k = 0; k < FN && m.fac; ++k) m.hi[dl.oQ + k] = 0.0;
   for (int j = 0; j < N; ++j) {
     m.hi[dl.o3 + j] = d.node_memory[j];
     m.hi[dl.o5 + j] = d.node_cores[j];
-    if (m.has_n) { m.hi[dl.o6 + j] = 0.0; m.lo[dl.o7 + j] = -m.eps; }
+    if (m.has_n && !m.fac) { m.hi[dl.o6 + j] = 0.0; m.lo[dl.o7 + j] = -m.eps; }
   }
   if (m.step2) {
     for (int k = 0; k < FN; ++k) {
@@ -411,6 +419,12 @@ int build(Model &m, const nep_model_desc &d) {
   for (int f = 0; f < F; ++f)
     for (int j = 0; j < N; ++j) {
       const int k = f * N + j;
+      if (m.fac) {   // C3 and c[f, j] - n[j] <= 0 (the x <= c rows are structured: rhoL, below)
+        K.add(dl.o3 + j, il.oc + k, m.mem_f[f]);
+        K.add(dl.oQ + k, il.oc + k, 1.0);
+        K.add(dl.oQ + k, il.on + j, -1.0);
+        continue;
+      }
       K.add(dl.o1 + k, il.oc + k, -m.M);
       K.add(dl.o2 + k, il.oc + k, -1.0);
       K.add(dl.o3 + j, il.oc + k, m.mem_f[f]);
@@ -430,7 +444,7 @@ int build(Model &m, const nep_model_desc &d) {
         K.add(dl.oD4, il.oc + k, m.sigma4);
       }
     }
-  if (m.has_n)
+  if (m.has_n && !m.fac)
     for (int j = 0; j < N; ++j) {
       K.add(dl.o6 + j, il.on + j, -m.M);
       K.add(dl.o7 + j, il.on + j, -1.0);
@@ -478,6 +492,12 @@ int build(Model &m, const nep_model_desc &d) {
   // non-x columns; x columns keep scale 1 so every routing row stays a plain simplex.
   m.rho.assign(o, 1.0);
   m.gam.assign(il.n_int, 1.0);
+  // facility relaxation: the rows x[r, j] - c[f, j] <= 0 of every routing row r of f (x entry 1, unscaled;
+  // c entry -gam_c): one scale per (f, j), and nrow_f entries in c[f, j]'s column
+  std::vector<int> nrow_f(F, 0);
+  for (int r = 0; r < m.R; ++r) nrow_f[m.row_f[r]] += 1;
+  if (m.fac) m.rhoL.assign(FN, 1.0);
+  std::vector<double> rnL(m.fac ? FN : 0);
   std::vector<double> rn(o), cn(il.n_int);
   for (int sweep = 0; sweep < 11; ++sweep) {
     const bool pc = sweep == 10;
@@ -488,8 +508,17 @@ int build(Model &m, const nep_model_desc &d) {
       if (pc) { rn[K.r[e]] += a; cn[K.c[e]] += a; }
       else { rn[K.r[e]] = std::max(rn[K.r[e]], a); cn[K.c[e]] = std::max(cn[K.c[e]], a); }
     }
+    for (int k = 0; k < (m.fac ? FN : 0); ++k) {
+      const double gc = m.gam[il.oc + k], a = m.rhoL[k] * gc;
+      rnL[k] = pc ? m.rhoL[k] * (1.0 + gc) : m.rhoL[k] * std::max(1.0, gc);
+      const int f = k / N;
+      if (pc) cn[il.oc + k] += nrow_f[f] * a;
+      else cn[il.oc + k] = std::max(cn[il.oc + k], a);
+    }
     for (int k = 0; k < o; ++k)
       if (rn[k] > 0) m.rho[k] /= std::sqrt(rn[k]);
+    for (int k = 0; k < (m.fac ? FN : 0); ++k)
+      if (rnL[k] > 0) m.rhoL[k] /= std::sqrt(rnL[k]);
     for (int k = 0; k < il.n_int; ++k)
       if (cn[k] > 0) m.gam[k] /= std::sqrt(cn[k]);
   }
@@ -517,8 +546,10 @@ int build(Model &m, const nep_model_desc &d) {
         const double *xr = &zx[(size_t)r * N];
         double srow = 0.0;
         for (int j = 0; j < N; ++j) {
-          yv[dl.o1 + f * N + j] += mr * xr[j];
-          yv[dl.o2 + f * N + j] += mr * xr[j];
+          if (!m.fac) {
+            yv[dl.o1 + f * N + j] += mr * xr[j];
+            yv[dl.o2 + f * N + j] += mr * xr[j];
+          }
           yv[dl.o5 + j] += wr * cpr[(size_t)f * N + j] * xr[j];
           if (m.step2 && src >= 0 && sc != 0.0) srow += sc * D[(size_t)src * N + j] * xr[j];
         }
@@ -533,12 +564,25 @@ int build(Model &m, const nep_model_desc &d) {
         const double mr = m.row_m[r], wr = m.row_w[r], sc = m.row_wsc[r];
         double *gr = &gx[(size_t)r * N];
         for (int j = 0; j < N; ++j) {
-          double g = mr * (yv[dl.o1 + f * N + j] + yv[dl.o2 + f * N + j]) + wr * cpr[(size_t)f * N + j] * yv[dl.o5 + j];
+          double g = wr * cpr[(size_t)f * N + j] * yv[dl.o5 + j];
+          if (!m.fac) g += mr * (yv[dl.o1 + f * N + j] + yv[dl.o2 + f * N + j]);
           if (m.step2 && src >= 0 && sc != 0.0) g += sc * D[(size_t)src * N + j] * yv[dl.oS];
           gr[j] = g;
         }
       }
       std::fill(gs.begin(), gs.end(), 0.0);
+      if (m.fac)   // the x <= c rows, scaled: t = rhoL (x - gam_c z_c); x gets rhoL t, z_c gets -rhoL t (gam_c: below)
+        for (int r = 0; r < m.R; ++r) {
+          const int f = m.row_f[r];
+          const double *xr = &zx[(size_t)r * N];
+          double *gr = &gx[(size_t)r * N];
+          for (int j = 0; j < N; ++j) {
+            const int k = f * N + j;
+            const double t = m.rhoL[k] * (xr[j] - m.gam[il.oc + k] * zs[il.oc + k]);
+            gr[j] += m.rhoL[k] * t;
+            gs[il.oc + k] -= m.rhoL[k] * t;
+          }
+        }
       for (size_t e = 0; e < K.v.size(); ++e) gs[K.c[e]] += K.v[e] * yv[K.r[e]];
       for (int k = 0; k < il.n_int; ++k) gs[k] *= m.gam[k];
       double dot = 0.0;
@@ -593,7 +637,7 @@ int setup_device(Model &m, int max_batch, void *stream) {
   HIPCHK(hipEventCreateWithFlags(&m.ev_aux, hipEventDisableTiming));
   DeviceView &v = m.v;
   v.N = m.N; v.NP = m.NP; v.F = m.F; v.R = m.R; v.JB = m.JB; v.CPL = m.CPL;
-  v.has_n = m.has_n; v.step2 = m.step2; v.variant = m.variant;
+  v.has_n = m.has_n; v.step2 = m.step2; v.variant = m.variant; v.fac = m.fac;
   v.M = m.M; v.eps = m.eps; v.sigma4 = m.sigma4; v.cost_n = m.cost_n; v.score_n_coef = m.score_n_coef;
   v.w_dis = m.w_dis;
   v.dl = m.dl; v.il = m.il;
@@ -645,7 +689,7 @@ int setup_dense(Model &m, const nep_model_desc &d) {
   v.skty = (int64_t)F * NP + NP + 4;
   v.stpart = (int64_t)F * NTS;
   v.sbpart = (int64_t)(F + m.JB) * NBS;
-  v.snpart = (int64_t)F * 2 * NP;
+  v.snpart = (int64_t)F * (m.fac ? 3 : 2) * NP;   // fac: c, CPU share, reflected c (2ĉ - c) per (f, j)
   v.srpart = (int64_t)F * 2 * NP;
   if ((rc = dalloc(m, &v.x, (size_t)B * v.sx))) return rc;
   if ((rc = dalloc(m, &v.xa, (size_t)B * v.sx))) return rc;
@@ -667,6 +711,18 @@ int setup_dense(Model &m, const nep_model_desc &d) {
   if ((rc = dalloc(m, &v.tpart, (size_t)B * v.stpart))) return rc;
   if ((rc = dalloc(m, &v.bpart, (size_t)B * v.sbpart))) return rc;
   if ((rc = dalloc(m, &v.npart, (size_t)B * v.snpart))) return rc;
+  if (m.fac) {
+    v.slsum = (int64_t)F * NP;
+    if ((rc = dalloc(m, &v.lam, (size_t)B * v.sx))) return rc;
+    if ((rc = dalloc(m, &v.lama, (size_t)B * v.sx))) return rc;
+    if ((rc = dalloc(m, &v.lsum, (size_t)B * v.slsum))) return rc;
+    std::vector<float> rl((size_t)F * NP, 0.f);
+    for (int f = 0; f < F; ++f)
+      for (int j = 0; j < N; ++j) rl[(size_t)f * NP + j] = (float)m.rhoL[(size_t)f * N + j];
+    if ((rc = upload(m, &v.rho_l, rl))) return rc;
+    HIPCHK(hipMemsetAsync(v.lam, 0, sizeof(float) * B * v.sx, m.stream));
+    HIPCHK(hipMemsetAsync(v.lsum, 0, sizeof(float) * B * v.slsum, m.stream));
+  }
   if ((rc = dalloc(m, &v.rpart, (size_t)B * v.srpart))) return rc;
   if ((rc = dalloc(m, &v.ctrl, (size_t)B))) return rc;
   {
@@ -725,7 +781,7 @@ static void activity_ranges(const Model &m, const std::vector<double> &lb, const
   const int N = m.N, F = m.F, NP = m.NP, o = m.dl.n_dual;
   amin.assign(o, 0.0);
   amax.assign(o, 0.0);
-  for (int f = 0; f < F; ++f)
+  for (int f = 0; f < F && m.dl.o1 >= 0; ++f)   // (C1/C2: not in the facility relaxation)
     for (int j = 0; j < N; ++j) {
       const double fx = mask[(size_t)f * NP + j] ? m.ftot[f] : 0.0;
       amax[m.dl.o1 + f * N + j] += fx;
@@ -887,6 +943,7 @@ bool presolve_node(Model &m, const double *lbi, const double *ubi, std::vector<i
         m.fdelta[f] += now - was;
         const double dfx = (now - was) * m.ftot[f];
         for (int r : {m.dl.o1 + f * N + j, m.dl.o2 + f * N + j}) {
+          if (m.dl.o1 < 0) break;
           touch(r);
           m.dmax[r] += dfx;
         }
@@ -980,7 +1037,7 @@ int submit(Model &m, int n, const int32_t *slots, const double *lbi, const doubl
   DeviceView &v = m.v;
   v.warm_omega_floor = o.warm_omega_floor;
   v.warm_omega_cap = o.warm_omega_cap;
-  v.polish_after = o.polish_after < 0 ? -1 : (int64_t)o.polish_after;
+  v.polish_after = (o.polish_after < 0 || m.fac) ? -1 : (int64_t)o.polish_after;   // (fac: no polishing)
   v.max_iters = o.max_iters;
   v.bound_res = o.bound_res;
   // tol / cutoff of every LP in flight: device memory, read by the (graph-replayed) blocks
@@ -1002,7 +1059,7 @@ int submit(Model &m, int n, const int32_t *slots, const double *lbi, const doubl
     fresh.push_back(s);
     // the box fixes the objective when the routing carries no cost and every c and n is fixed (a
     // leaf): mf / mt / allocated / deallocated then follow from c at their cheapest (the repair)
-    bool ex = m.x_cost_free;
+    bool ex = m.x_cost_free && !m.fac;
     const double *L = lbi ? lbi + (size_t)b * ni : nullptr, *U = ubi ? ubi + (size_t)b * ni : nullptr;
     const int n_fix_end = m.has_n ? m.il.on + m.N : m.il.oc + m.F * m.N;
     for (int k = m.il.oc; ex && k < m.il.oc + m.F * m.N; ++k)
@@ -1372,7 +1429,9 @@ int nep_model_get_info(void *model, nep_model_info *info) {
   info->max_batch = m.max_batch;
   info->x_entries = (int64_t)m.R * m.N;
   // B_iter = 4 (2P + 2FN + 2N + 2m), P = x entries iterated, m = dual rows
-  info->bytes_per_iter = 4 * (2 * (int64_t)m.R * m.N + 2 * (int64_t)m.F * m.N + 2 * (int64_t)m.N + 2 * (int64_t)m.dl.n_dual);
+  // (facility relaxation: the x <= c rows are dualised rows too, one per routing entry: m += R N)
+  info->bytes_per_iter = 4 * (2 * (int64_t)m.R * m.N + 2 * (int64_t)m.F * m.N + 2 * (int64_t)m.N +
+                              2 * ((int64_t)m.dl.n_dual + (m.fac ? (int64_t)m.R * m.N : 0)));
   info->step_size = m.eta;
   return NEP_OK;
 }
@@ -1477,6 +1536,11 @@ int nep_lp_copy_state(void *model, int32_t src, int32_t dst) {
   HIPCHK(hipMemcpyAsync(v.rpart + dst * v.srpart, v.rpart + src * v.srpart, v.srpart * sizeof(double),
                         hipMemcpyDeviceToDevice, m.aux));
   HIPCHK(hipMemcpyAsync(v.ctrl + dst, v.ctrl + src, sizeof(Ctrl), hipMemcpyDeviceToDevice, m.aux));
+  if (m.fac) {   // the x <= c duals and their per-(f, j) sums travel with the state
+    HIPCHK(hipMemcpyAsync(v.lam + dst * v.sx, v.lam + src * v.sx, v.sx * sizeof(float), hipMemcpyDeviceToDevice, m.aux));
+    HIPCHK(hipMemcpyAsync(v.lsum + dst * v.slsum, v.lsum + src * v.slsum, v.slsum * sizeof(float),
+                          hipMemcpyDeviceToDevice, m.aux));
+  }
   HIPCHK(hipStreamSynchronize(m.aux));
   return NEP_OK;
 }

@@ -115,6 +115,7 @@ struct Ctrl {
 // row-family offsets inside y / kz / rho / lo / hi
 struct DualLayout {
   int o1, o2, o3, o5, o6, o7, oD1, oD2, oD3a, oD3b, oD4, oS;
+  int oQ;                                // facility relaxation: c[f, j] <= n[j] rows (F*N); else -1
   int n_dual;
 };
 // small-primal offsets inside zi
@@ -127,6 +128,7 @@ struct DeviceView {
   // sizes
   int N, NP, F, R, JB, CPL;
   int has_n, step2, variant;
+  int fac;                               // NEP_RELAX_FACILITY model (nep_fac.hip): x <= c, c <= n, no big-M pairs
   double M, eps, sigma4, cost_n, score_n_coef, w_dis;
   DualLayout dl;
   IntLayout il;
@@ -150,6 +152,11 @@ struct DeviceView {
   double *tpart, *bpart, *npart;
   double *rpart;                         // [F][2][NP] certificate: repaired c shares of the node rows (mem, c)
   Ctrl *ctrl;
+  // facility relaxation (fac): the duals of x[r, j] - c[f, j] <= 0, one per routing entry ([R][NP] f32 like x),
+  // their Halpern anchor, and per (f, j) their sum over the rows of f (c's reduced cost, next iteration)
+  float *lam, *lama, *lsum;
+  const float *rho_l;                    // [F][NP] row scale of those rows (the same for every row of f at j)
+  int64_t slsum;
   int64_t sx, smask, sint, sdual, skty, stpart, sbpart, snpart, srpart;   // per-slot strides (elements)
   // check/solve parameters.  tol / cutoff / gap tol live in device memory (prm[0..2], written by every
   // nep_lp_submit) because the iteration blocks are replayed from captured HIP graphs: a value

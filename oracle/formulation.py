@@ -214,3 +214,36 @@ def build_model(data, variant, step=1, mode="delete", alpha=0.5, soften_step1_so
         lb[L.alloc] = lb[L.dealloc] = -float(F * N)
         ub[L.alloc] = ub[L.dealloc] = 0.0
     return dict(A=A, lo=lo, hi=hi, c=obj, lb=lb, ub=ub, integrality=integ, layout=L, maximize=False, offset=0.0)
+
+
+def facility_relaxation(m, data):
+    """The B&B's strengthened relaxation (engine NEP_RELAX_FACILITY, include/neptune_lp.h) of a
+    step-1 MinUtilization / MinDelayAndUtilization model `m` (build_model's dict): the big-M pairs C1/C2
+    (constraints_step1.py:5-15) and C6/C7 (:69-78) are replaced by x[i,f,j] <= c[f,j] for every (i, f, j) and
+    c[f,j] <= n[j] — valid for every integral placement (c = 0 forces the column's flow to 0 through C1; n = 0
+    forces c = 0 through C6), and implying C1 and C6 for integral c, n; C2 / C7 (the eps floors) are relaxed.
+    Test infrastructure: its HiGHS value is what the engine's facility LPs are checked against."""
+    L = m["layout"]
+    assert L.step == 1 and L.has_n, "step-1 MinUtilization / MinDelayAndUtilization only"
+    N, F = L.N, L.F
+    A = m["A"].tocsr()
+    nrow = A.shape[0]
+    keep = np.ones(nrow, bool)
+    keep[:2 * F * N] = False                                    # C1/C2, interleaved per (f, j), built first
+    coo = A.tocoo()
+    big = (coo.col >= L.n0) & (coo.col < L.n0 + N) & ((coo.data == -float(BIG_M)) | (coo.data == -1.0))
+    keep[np.unique(coo.row[big])] = False                       # C6/C7 (the rows with -M n / -n)
+    A, lo, hi = A[keep], m["lo"][keep], m["hi"][keep]
+    nv = A.shape[1]
+    k = F * N * N
+    r = np.arange(k)
+    xc = sp.csr_matrix((np.concatenate([np.ones(k), -np.ones(k)]),
+                        (np.concatenate([r, r]), np.concatenate([np.arange(k), L.c0 + (r // (N * N)) * N + r % N]))),
+                       shape=(k, nv))
+    q = np.arange(F * N)
+    cn = sp.csr_matrix((np.concatenate([np.ones(F * N), -np.ones(F * N)]),
+                        (np.concatenate([q, q]), np.concatenate([L.c0 + q, L.n0 + q % N]))), shape=(F * N, nv))
+    A2 = sp.vstack([A, xc, cn]).tocsr()
+    lo2 = np.concatenate([lo, np.full(k + F * N, -INF)])
+    hi2 = np.concatenate([hi, np.zeros(k + F * N)])
+    return dict(m, A=A2, lo=lo2, hi=hi2)

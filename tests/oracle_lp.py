@@ -15,7 +15,7 @@ LP_OPTIMAL, LP_ITERATION_LIMIT, LP_INFEASIBLE, LP_CUTOFF, LP_BOUND = 0, 1, 2, 3,
 
 class OracleLP:
     def __init__(self, data, variant, step=1, alpha=0.5, soften_step1_sol=1.3, max_score=0.0,
-                 prev_network_delay=0.0, max_batch=1):
+                 prev_network_delay=0.0, max_batch=1, relaxation=0):
         self.N, self.F = len(data.nodes), len(data.functions)
         self.variant = variant
         self.step = int(step)
@@ -26,6 +26,9 @@ class OracleLP:
         self.m = build_model(data, variant, step=1 if self.step == 1 else 2,
                              mode="delete" if self.step == 2 else "create", alpha=alpha,
                              soften_step1_sol=soften_step1_sol, max_score=max_score, prev_x=prev_x)
+        if relaxation:   # the B&B's facility relaxation (engine NEP_RELAX_FACILITY)
+            from oracle.formulation import facility_relaxation
+            self.m = facility_relaxation(self.m, data)
         self.nx = self.N * self.N * self.F
         self._W = np.asarray(data.workload_matrix, np.float64)
         self.n_int = self.m["A"].shape[1] - self.nx
@@ -74,7 +77,7 @@ class OracleLP:
     # streaming form (nep_lp_submit / nep_lp_advance): HiGHS solves each submitted node at once; advance
     # hands back up to min_done finished nodes per call, in slot order, like the engine's blocks
     def submit(self, slots, lb=None, ub=None, tol=1e-7, cutoff=math.inf, max_iters=0, check_every=64,
-               warm_start=False, warm_omega_floor=0.0, bound_res=0.0):
+               warm_start=False, warm_omega_floor=0.0, bound_res=0.0, gap_tol=0.0):
         slots = np.asarray(slots).reshape(-1)
         self._cutoff = cutoff
         r = self.solve(slots, lb, ub, tol=tol, cutoff=math.inf)
@@ -158,7 +161,7 @@ class StreamingOracleLP(OracleLP):
     the pre-polish incumbent: round-2 ADVICE)."""
 
     def submit(self, slots, lb=None, ub=None, tol=1e-7, cutoff=math.inf, max_iters=0, check_every=64,
-               warm_start=False, warm_omega_floor=0.0, bound_res=0.0):
+               warm_start=False, warm_omega_floor=0.0, bound_res=0.0, gap_tol=0.0):
         slots = np.asarray(slots).reshape(-1)
         self._cutoff = cutoff
         r = self.solve(slots, lb, ub, tol=tol, cutoff=math.inf)

@@ -123,3 +123,22 @@ def test_inline_reflection_equals_tracked_activity(name, k):
     if a["status"] == 0:
         assert abs(a["obj"] - b["obj"]) <= 1e-5 * max(1.0, abs(a["obj"]))
         assert abs(a["iters"] - b["iters"]) <= 0.1 * a["iters"] + 16
+
+
+def test_facility_relaxation_build():
+    """nep_debug_build of the B&B's facility relaxation (NEP_RELAX_FACILITY, API 7): its dual rows are C3, C5
+    and c[f,j] <= n[j] (2N + FN; the x <= c rows are per routing entry, outside the dual vector), the integer
+    vector is step 1's (c, n), and it exists only for step-1 models with n (MinUtilization / MDU)."""
+    from core.engine.lp import EngineUnavailable, RELAX_FACILITY, STEP2_CREATE, debug_build
+    from core.utils import data_to_solver_input
+    from core.utils.synthetic import synthetic_payload
+    N, F = 16, 8
+    data = data_to_solver_input(synthetic_payload(N, F, seed=0), with_db=False)
+    ref = debug_build(data, "MinDelayAndUtilization")
+    got = debug_build(data, "MinDelayAndUtilization", relaxation=RELAX_FACILITY)
+    assert got["n_dual"] == 2 * N + F * N and got["n_int"] == F * N + N == ref["n_int"]
+    assert got["R"] == ref["R"] and 0.0 < got["eta"] < float("inf")
+    assert np.all(np.isfinite(got["rho"])) and np.all(got["rho"] > 0) and np.all(got["gam"] > 0)
+    for variant, step in (("MinDelay", 1), ("MinDelayAndUtilization", STEP2_CREATE)):
+        with pytest.raises(EngineUnavailable):
+            debug_build(data, variant, step=step, relaxation=RELAX_FACILITY, max_score=1.0)

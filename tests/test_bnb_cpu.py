@@ -99,3 +99,31 @@ def test_bnb_with_bound_converged_nodes(name, k):
         assert res.status == INFEASIBLE, res.as_dict()
     assert res.lp_status_kind["node"]["certified"] <= 1      # (the root alone may certify)
     assert res.lp_status["bound"] == res.lp_status_kind["node"]["bound"]
+
+
+STEP1_N = [(n, k) for n, k in SMALL if k == 0 and VARIANT[payload(n)["solver"]["type"]] != "MinDelay"]
+
+
+@pytest.mark.parametrize("name,k", STEP1_N)
+def test_bnb_two_models_matches_recorded_mip(name, k):
+    """Round 4: the branching nodes bounded by the facility relaxation (a second model,
+    oracle/formulation.py facility_relaxation: x <= c, c <= n in place of the big-M pairs), the leaves solved
+    on the reference model: the search still reaches the MIP optimum HiGHS found on the reference's own
+    recorded model (the relaxation is valid for every integral placement, so no optimum is cut off), with
+    streaming out-of-order finishes on both models."""
+    from core.engine.bnb import INFEASIBLE, OPTIMAL, BranchAndBound
+    from oracle_lp import StreamingOracleLP
+    p, data = _data(name)
+    rec = G[name]["models"][k]
+    variant = VARIANT[p["solver"]["type"]]
+    alpha = p["solver"].get("args", {}).get("alpha", 0.5)
+    lp = StreamingOracleLP(data, variant, step=1, max_batch=10, alpha=alpha)
+    blp = StreamingOracleLP(data, variant, step=1, max_batch=9, alpha=alpha, relaxation=1)
+    res = BranchAndBound(lp, data.workload_matrix, data.function_memory_matrix, data.node_memory_matrix,
+                         batch=8, node_limit=20000, bound_lp=blp).solve()
+    if rec["status"] == 0:
+        assert res.status == OPTIMAL, res.as_dict()
+        assert _close(res.objective, rec["mip_objective"]), (res.objective, rec["mip_objective"])
+    else:
+        assert res.status == INFEASIBLE, res.as_dict()
+    assert res.lp_status_kind["refroot"]["certified"] + res.lp_status_kind["refroot"]["cutoff"] <= 1

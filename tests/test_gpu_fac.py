@@ -1,0 +1,80 @@
+"""GPU parity of the facility relaxation (engine NEP_RELAX_FACILITY, include/neptune_lp.h): the
+strengthened step-1 LP the branch-and-bound bounds its nodes with — x[i,f,j] <= c[f,j] and c[f,j] <= n[j] in
+place of the big-M pairs (constraints_step1.py:5-15, :69-78) — certified by the engine and equal, within
+1e-6, to HiGHS on the same relaxation built from the reference formulation (oracle/formulation.py
+facility_relaxation).  Root LPs and B&B-style children (n and c fixings), warm-started from the root as the
+search does; every LP must certify."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-6
+
+
+def _gap(a, b):
+    return abs(a - b) / max(1.0, abs(b))
+
+
+def _fixings(F, N, rng, k):
+    """k children: close a node, open a node, fix a placement open, fix a placement closed."""
+    out = []
+    for b in range(k):
+        kind = b % 4
+        if kind == 0:
+            out.append(([F * N + int(rng.integers(N))], [0.0]))
+        elif kind == 1:
+            out.append(([F * N + int(rng.integers(N))], [1.0]))
+        elif kind == 2:
+            out.append(([int(rng.integers(F * N))], [1.0]))
+        else:
+            idx = rng.choice(F * N, size=2, replace=False)
+            out.append((idx.tolist(), [0.0, 0.0]))
+    return out
+
+
+@pytest.mark.parametrize("N,F,variant", [(16, 8, "MinDelayAndUtilization"), (24, 12, "MinDelayAndUtilization"),
+                                         (32, 16, "MinDelayAndUtilization"), (64, 32, "MinDelayAndUtilization"),
+                                         (32, 16, "MinUtilization")])
+def test_facility_relaxation_matches_highs(N, F, variant):
+    from core.engine.lp import LPModel, LP_OPTIMAL, RELAX_FACILITY
+    from core.utils import data_to_solver_input
+    from core.utils.synthetic import synthetic_payload
+    from oracle.formulation import build_model, facility_relaxation
+    from oracle.inputs import data_to_solver_input as oracle_input
+    from oracle.solve import solve
+    p = synthetic_payload(N, F, seed=0)
+    alpha = p["solver"]["args"]["alpha"]
+    data = data_to_solver_input(p, with_db=False)
+    od = oracle_input(p, with_db=False)
+    ref_model = facility_relaxation(build_model(od, variant, step=1, alpha=alpha), od)
+    fix = _fixings(F, N, np.random.default_rng(N + F), 4)
+    B = len(fix)
+    m = LPModel(data, variant, step=1, alpha=alpha, max_batch=B + 1, relaxation=RELAX_FACILITY)
+    try:
+        root = B
+        rr = m.solve([root], tol=5e-7, max_iters=100000)
+        lb = np.full((B, m.n_int), -np.inf)
+        ub = np.full((B, m.n_int), np.inf)
+        for b, (idx, val) in enumerate(fix):
+            lb[b, idx] = ub[b, idx] = val
+            m.copy_state(root, b)
+        res = m.solve(np.arange(B), lb, ub, tol=5e-7, max_iters=100000, warm_start=True)
+        nx = N * N * F
+        got = [(int(rr["status"][0]), float(rr["obj"][0]), int(rr["iters"][0]))]
+        got += [(int(res["status"][b]), float(res["obj"][b]), int(res["iters"][b])) for b in range(B)]
+        for b, (st, obj, its) in enumerate(got):
+            rl, ru = ref_model["lb"].copy(), ref_model["ub"].copy()
+            if b > 0:
+                idx, val = fix[b - 1]
+                rl[nx + np.asarray(idx)] = val
+                ru[nx + np.asarray(idx)] = val
+            hst, ref, _ = solve(ref_model, relax=True, lb=rl, ub=ru)
+            print(f"{N}x{F} {variant} LP {b}: status {st} obj {obj:.10g} HiGHS {ref} after {its} iterations")
+            if ref is None:
+                assert st != LP_OPTIMAL, f"LP {b}: HiGHS infeasible, engine optimal {obj}"
+                continue
+            assert obj <= ref + TOL * max(1.0, abs(ref)), f"LP {b}: bound {obj} above the LP value {ref}"
+            assert st == LP_OPTIMAL, f"LP {b}: status {st} after {its} iterations (HiGHS {ref})"
+            assert _gap(obj, ref) <= TOL, f"LP {b}: {obj} vs HiGHS {ref}"
+    finally:
+        m.close()
