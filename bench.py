@@ -73,6 +73,12 @@ def parse(argv=None):
                     help="after the root certifies at --tol, continue it (warm, same slot) until its objective gap "
                          "is below this: the children warm-start from a well-converged root (0 = off)")
     ap.add_argument("--cold", action="store_true", help="cold-start every node LP")
+    ap.add_argument("--stream", default="auto", choices=("auto", "replay", "children"),
+                    help="the timed node-LP stream: the product B&B's recorded nodes (replay, tests/golden/"
+                         "bnb_trace_<N>x<F>_s<seed>.json) or root children with --fix random fixings; auto: "
+                         "replay when the trace exists")
+    ap.add_argument("--children-steps", type=int, default=24,
+                    help="with the replay stream: steps of the children stream timed after it (secondary figure)")
     ap.add_argument("--cpu-budget", type=float, default=150.0,
                     help="seconds for the CPU baseline (0 = skip); the bench-size attempt gets what the fit leaves, "
                          ">= 30 s")
@@ -86,9 +92,15 @@ def parse(argv=None):
     return ap.parse_args(argv)
 
 
-def workload_name(a):
+def children_workload_name(a):
     return (f"synthetic_{a.nodes}x{a.functions}_step1_MDU_bnb_children_stream_B{a.batch}_fix{a.fix}_"
             f"{'cold' if a.cold else 'warm'}")
+
+
+def workload_name(a, kind):
+    if kind == "replay":
+        return f"synthetic_{a.nodes}x{a.functions}_step1_MDU_bnb_node_replay_s{a.seed}_B{a.batch}_reference_lp"
+    return children_workload_name(a)
 
 
 def log(msg):
@@ -284,6 +296,92 @@ def bnb_section(a, rank, world, dev, N, F):
             "ranks": world}
 
 
+class ReplayStream:
+    """The node LPs the product branch-and-bound submitted at this size (recorded by tools/record_bnb_trace.py
+    into tests/golden/bnb_trace_<N>x<F>_s<seed>.json), replayed in submission order as LP relaxations of the
+    REFERENCE model — the LP SCIP solves at those nodes (solver.py:35-40): a branching node's box is its
+    fixings, a leaf's fixes every c and n (open ones to 1).  `batch` in flight; a node starts from its
+    parent's final PDHG state when a slot still holds it (slots are refilled oldest-finished first, as the
+    B&B does), else from the root's.  With `world` ranks, rank r takes entries r, r + world, ... (the trace
+    repeated as often as the steps need)."""
+
+    def __init__(self, m, root, a, rank, world, trace):
+        self.m, self.root, self.a = m, root, a
+        self.lps = trace["lps"]
+        self.pos, self.stride = rank, world
+        self.counter = 0
+        self.done = []          # (status, obj, primal_obj, iters) per completed node
+        self.where = {}         # node key -> slot holding its final state
+        self.held = {}          # slot -> node key
+        self.running = {}       # slot -> node key
+        self.free = []
+        self.warm_parent = 0
+
+    def _box(self, e):
+        import numpy as np
+        F, N = self.a.functions, self.a.nodes
+        lb = np.full(self.m.n_int, -np.inf)
+        ub = np.full(self.m.n_int, np.inf)
+        if "open" in e:
+            lb[:F * N + N] = ub[:F * N + N] = 0.0
+            lb[e["open"]] = ub[e["open"]] = 1.0
+        else:
+            idx, val = e["fix"]
+            lb[idx] = ub[idx] = val
+        return lb, ub
+
+    def _refill(self):
+        import numpy as np
+        from core.engine.lp import LP_INFEASIBLE
+        a = self.a
+        while self.free and self.counter < self.limit:
+            slot = self.free.pop(0)
+            k = self.pos
+            self.pos += self.stride
+            rep, e = divmod(k, len(self.lps))
+            e = self.lps[e]
+            key = (rep, e["id"])
+            pkey = (rep, e["parent"])
+            old = self.held.pop(slot, None)       # this slot's finished state is overwritten now
+            if old is not None:
+                self.where.pop(old, None)
+            src = self.root
+            if e["warm_from_parent"] and pkey in self.where:
+                src = self.where[pkey]
+                self.warm_parent += 1
+            self.m.copy_state(src, slot)
+            lb, ub = self._box(e)
+            self.counter += 1
+            st = self.m.submit([slot], lb[None], ub[None], tol=a.tol, max_iters=a.max_iters,
+                               check_every=a.check_every, warm_start=True, warm_omega_floor=a.warm_omega_floor)
+            if int(st[0]) == LP_INFEASIBLE:
+                self.done.append((LP_INFEASIBLE, float("inf"), float("nan"), 0))
+                self.free.append(slot)
+            else:
+                self.running[slot] = key
+
+    def drain(self, n):
+        """Stream the next n recorded nodes through the `batch` slots until every one of them finished."""
+        self.limit = self.counter + n
+        if not self.free and not self.running:
+            self.free = list(range(self.a.batch))
+        self._refill()
+        while self.m.active() > 0:
+            r = self.m.advance(1)
+            for i, slot in enumerate(r["slots"].tolist()):
+                self.done.append((int(r["status"][i]), float(r["obj"][i]), float(r["primal_obj"][i]),
+                                  int(r["iters"][i])))
+                key = self.running.pop(slot)
+                self.where[key] = slot
+                self.held[slot] = key
+                self.free.append(slot)
+            self._refill()
+
+
+def trace_path(a):
+    return os.path.join(REPO, "tests", "golden", f"bnb_trace_{a.nodes}x{a.functions}_s{a.seed}.json")
+
+
 class NodeStream:
     """B&B child LPs of the root, `batch` of them in flight on the engine (nep_lp_submit/advance):
     a slot whose LP finishes takes the next node at once, as a B&B with an open-node queue does."""
@@ -348,7 +446,7 @@ def main():
         import torch.distributed as td
         td.init_process_group("nccl", device_id=dev)
 
-    from core.engine.lp import LPModel, LP_OPTIMAL
+    from core.engine.lp import LPModel, LP_BOUND, LP_CUTOFF, LP_INFEASIBLE, LP_OPTIMAL
     from core.utils import data_to_solver_input
     from core.utils.synthetic import synthetic_payload
 
@@ -365,6 +463,7 @@ def main():
     t_root = time.perf_counter()
     rr = m.solve([root], tol=a.tol, max_iters=a.root_max_iters, check_every=a.root_check_every)
     root_obj, root_status, root_iters = float(rr["obj"][0]), int(rr["status"][0]), int(rr["iters"][0])
+    root_seconds = time.perf_counter() - t_root
     log(f"rank {rank}: root LP status {root_status} obj {root_obj:.10g} after {root_iters} iterations "
         f"({time.perf_counter() - t_root:.2f}s)")
     if root_status != LP_OPTIMAL:
@@ -381,50 +480,72 @@ def main():
         log(f"rank {rank}: root polish to gap {a.root_gap_tol:g}: status {root_polish['status']} after "
             f"{root_polish['iters']} iterations ({root_polish['seconds']:.2f}s)")
 
-    stream = NodeStream(m, root, a, rank)
+    kind = a.stream
+    if kind == "auto":
+        kind = "replay" if os.path.exists(trace_path(a)) else "children"
+    if kind == "replay":
+        with open(trace_path(a)) as fh:
+            stream = ReplayStream(m, root, a, rank, world, json.load(fh))
+    else:
+        stream = NodeStream(m, root, a, rank)
 
-    def bound_exchange():
-        ok = [o for st, o, _, _ in stream.done if st == LP_OPTIMAL]
+    def timed(stream, steps, tag):
+        """steps * B nodes of `stream`, drained, timed between barriers (max over ranks)."""
+        m.reset_stats()
+        i0 = len(stream.done)
+        if dist:
+            td.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        # the timed K steps: K*B nodes streamed through the B slots and drained (every node finished,
+        # hard ones included — no node is left iterating outside the timed region)
+        stream.drain(steps * B)
+        ok = [o for st_, o, _, _ in stream.done[i0:] if st_ == LP_OPTIMAL]
         best = torch.tensor([min(ok) if ok else float("inf")], dtype=torch.float64, device=dev)
         if dist:
             td.all_reduce(best, op=td.ReduceOp.MIN)     # B&B bound exchange (8 B)
+        torch.cuda.synchronize()
+        if dist:
+            td.barrier()
+        wall = time.perf_counter() - t0
+        log(f"rank {rank}: {tag}: {len(stream.done) - i0} node LPs completed in {wall:.2f}s")
+        res = stream.done[i0:]
+        n_ok = sum(1 for r in res if r[0] == LP_OPTIMAL)
+        n_first = sum(1 for r in res if r[0] == LP_OPTIMAL and r[3] <= 1)
+        n_res = sum(1 for r in res if r[0] in (LP_OPTIMAL, LP_INFEASIBLE, LP_BOUND, LP_CUTOFF))
+        n_it = sum(r[3] for r in res)
+        gmax = max([abs(p_ - o) / max(1.0, abs(o)) for s_, o, p_, _ in res if s_ == LP_OPTIMAL] or [0.0])
+        st = m.stats()
+        util = n_it / max(1, st["lp_iterations"])       # this rank's LP iterations / slot-iterations run
+        iq = [int(v) for v in np.percentile([r[3] for r in res], [50, 90, 100])] if res else [0, 0, 0]
+        tot = torch.tensor([wall, n_ok, n_it, gmax, len(res), n_first, n_res], dtype=torch.float64, device=dev)
+        if dist:
+            mx = tot.clone()
+            td.all_reduce(mx, op=td.ReduceOp.MAX)
+            sm = tot.clone()
+            td.all_reduce(sm, op=td.ReduceOp.SUM)
+            tot = torch.cat([mx[:1], sm[1:3], mx[3:4], sm[4:]])
+        wall, n_ok, n_it, gmax, n_done, n_first, n_res = (float(t) for t in tot.tolist())
+        return {"wall": wall, "certified": int(n_ok), "completed": int(n_done), "iterations": int(n_it),
+                "gmax": gmax, "first_check_certified": int(n_first), "resolved": int(n_res), "iters_p50_p90_max": iq,
+                "util": util, "stats": st}
 
     if a.warmup > 0:
         stream.drain(a.warmup * B)
-        bound_exchange()
         log(f"rank {rank}: warmup: {len(stream.done)} node LPs completed")
-    m.reset_stats()
-    i0 = len(stream.done)
-    if dist:
-        td.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    # the timed K steps: K*B nodes streamed through the B slots and drained (every node finished,
-    # hard ones included — no node is left iterating outside the timed region)
-    stream.drain(a.steps * B)
-    bound_exchange()
-    log(f"rank {rank}: {len(stream.done) - i0} node LPs completed in {time.perf_counter() - t0:.2f}s")
-    torch.cuda.synchronize()
-    if dist:
-        td.barrier()
-    wall = time.perf_counter() - t0
-    st = m.stats()
-    res = stream.done[i0:]
-    n_ok = sum(1 for r in res if r[0] == LP_OPTIMAL)
-    n_it = sum(r[3] for r in res)
-    gmax = max([abs(p - o) / max(1.0, abs(o)) for s_, o, p, _ in res if s_ == LP_OPTIMAL] or [0.0])
-    n_done = len(res)
-    util = n_it / max(1, st["lp_iterations"])           # this rank's LP iterations / slot-iterations run
-    iq = [int(v) for v in np.percentile([r[3] for r in res], [50, 90, 100])] if res else [0, 0, 0]
-
-    tot = torch.tensor([wall, n_ok, n_it, gmax, n_done], dtype=torch.float64, device=dev)
-    if dist:
-        mx = tot.clone()
-        td.all_reduce(mx, op=td.ReduceOp.MAX)
-        sm = tot.clone()
-        td.all_reduce(sm, op=td.ReduceOp.SUM)
-        wall, gmax = float(mx[0]), float(mx[3])
-        n_ok, n_it, n_done = int(sm[1]), int(sm[2]), int(sm[4])
+    prim = timed(stream, a.steps, kind)
+    st = prim["stats"]
+    wall, n_ok, n_it, gmax, n_done = prim["wall"], prim["certified"], prim["iterations"], prim["gmax"], prim["completed"]
+    iq, util = prim["iters_p50_p90_max"], prim["util"]
+    second = None
+    if kind == "replay" and a.children_steps > 0:
+        # the secondary figure: the round-1..3 stream of root children with 2 random c-fixings each
+        cs = NodeStream(m, root, a, rank)
+        sec = timed(cs, a.children_steps, "children")
+        second = {"workload": children_workload_name(a), "value": sec["certified"] / sec["wall"],
+                  "certified": sec["certified"], "completed": sec["completed"], "steps": a.children_steps,
+                  "wall_s": sec["wall"], "iters_p50_p90_max": sec["iters_p50_p90_max"],
+                  "first_check_certified_share": sec["first_check_certified"] / max(1, sec["completed"])}
     m.close()
     # the product's own B&B (every rank takes part: the sharded search when world > 1)
     bnb = None
@@ -447,7 +568,7 @@ def main():
     launch_ms = st["x_pass_ms"] / max(1, st["x_pass_sampled"])
     lps_per_launch = st["x_pass_lp_iters"] / max(1, st["x_pass_sampled"])
     achieved = per_lp * lps_per_launch / (launch_ms * 1e-3) / 1e9 if launch_ms > 0 else 0.0
-    workload = workload_name(a)
+    workload = workload_name(a, kind)
     traffic = traffic_ratio = None
     if os.path.exists(a.traffic):
         with open(a.traffic) as fh:
@@ -475,15 +596,20 @@ def main():
         "dtype": "f32 x-state, f64 duals/reductions/certificate",
         "data": "synthetic (SURVEY.md §8(d) generator, seed %d)" % a.seed,
         "config": {"workload": workload, "nodes": N, "functions": F, "lp_in_flight_per_gpu": B,
-                   "fixings_per_lp": a.fix, "tol": a.tol, "max_iters_per_lp": a.max_iters,
+                   "fixings_per_lp": a.fix if kind == "children" else "recorded B&B boxes", "tol": a.tol, "max_iters_per_lp": a.max_iters,
                    "routing_entries_P": P, "parallelism": f"bnb-subtrees x{world}"},
         "objective_gap": {"certified_max": gmax, "tol": a.tol,
                           "note": "(primal obj - Lagrangian bound)/max(1,|bound|) per certified LP; "
                                   "HiGHS parity on the reference's own models: tests/test_gpu_lp.py"},
-        "lp": {"certified": n_ok, "completed": n_done, "iterations": n_it,
+        "lp": {"stream": kind, "certified": n_ok, "completed": n_done, "iterations": n_it,
+               "resolved": prim["resolved"], "resolved_lp_per_s": prim["resolved"] / wall,
+               "first_check_certified_share": prim["first_check_certified"] / max(1, n_done),
+               "warm_from_parent_rank0": getattr(stream, "warm_parent", None),
                "mean_iters": n_it / max(1, n_done), "iters_p50_p90_max": iq,
                "slot_utilisation_rank0": util,
-               "root_obj": root_obj, "root_iters": root_iters, "root_polish": root_polish},
+               "root_obj": root_obj, "root_iters": root_iters, "root_seconds": root_seconds,
+               "root_polish": root_polish},
+        "children_stream": second,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_over_algorithmic": traffic_ratio,
                      "kernel": "x_pass", "algorithmic_bytes_per_launch": per_lp * lps_per_launch,

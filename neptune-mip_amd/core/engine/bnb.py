@@ -89,6 +89,8 @@ class BnBResult:
         # warm-start copies), the drain after a stop, the end (routing fetch, polish, repair)
         self.timing = dict.fromkeys(("advance", "finish", "submit", "drain", "end"), 0.0)
         self.timing["root"] = 0.0       # wall seconds until the root LP finished (it iterates alone)
+        self.split_hash = None          # sharded search: crc32 of the frontier every rank dealt (must agree)
+        self.rebalanced = 0             # open nodes this rank received from another rank
         self.advance_calls = 0
         self.inflight_sum = 0           # LPs in flight summed over the advance calls (mean: / advance_calls)
 
@@ -104,10 +106,12 @@ class BnBResult:
 
 
 class _Node:
-    __slots__ = ("bound", "idx", "val", "kind", "parent", "depth")
+    __slots__ = ("bound", "idx", "val", "kind", "parent", "depth", "nid")
 
     def __init__(self, bound, idx, val, kind, parent, depth):
+        # parent: (engine, slot, slot generation, parent's id) of the LP whose state may warm-start this one
         self.bound, self.idx, self.val, self.kind, self.parent, self.depth = bound, idx, val, kind, parent, depth
+        self.nid = -1            # submission order (the trace's id)
 
 
 class _Engine:
@@ -143,7 +147,8 @@ class BranchAndBound:
                  node_limit=20000, time_limit=None, upper_bound=math.inf, flow_tol=1e-4, log=None, comm=None,
                  warm=True, root_max_iters=200000, check_every=12, polish_tol=1e-8, polish_iters=20000,
                  seed_leaves=None, integer_bound=None, improve=None, repair=None, node_bound_res=1e-2,
-                 retry_res=math.inf, unit_flow_leaves=True, node_max_iters=None, bound_lp=None, bound_gap=1e-4):
+                 retry_res=math.inf, unit_flow_leaves=True, node_max_iters=None, bound_lp=None, bound_gap=1e-4,
+                 trace=None, rebalance_every=8):
         self.lp = lp
         self.two = bound_lp is not None
         self.N, self.F = lp.N, lp.F
@@ -159,6 +164,11 @@ class BranchAndBound:
         # the bound model's LPs stop once their own gap (repaired point vs best bound) is within bound_gap:
         # a node needs its bound, which is valid at any dual point; the leaves keep the certificate tolerance
         self.bound_gap = bound_gap
+        # trace: a list that receives one entry per submitted node LP (_trace_entry), or None
+        self.trace = trace
+        # sharded search: every rebalance_every loops, ranks with an empty frontier take open nodes from the
+        # fullest ones (_rebalance; 0: never)
+        self.rebalance_every = rebalance_every
         self.root_slot = lp.max_batch - 1
         self.inc_slot = lp.max_batch - 2
         self.tol, self.gap, self.max_iters = tol, gap, max_iters
@@ -347,11 +357,11 @@ class BranchAndBound:
         groups = {}
         copies = {}
         for eng, slot, node in items:
-            warm = False
+            warm, src = False, None
             if self.warm and eng.root_ready:
                 src = eng.root_slot
                 if node.parent is not None:
-                    pe, ps, pg = node.parent
+                    pe, ps, pg = node.parent[:3]
                     if pe is eng and eng.gen[ps] == pg:
                         src = ps
                 if src != slot:
@@ -362,6 +372,9 @@ class BranchAndBound:
             # (the bound model's root is a branching node like the others: it stops once its bound converged)
             bres = self.node_bound_res if (node.kind == NODE and (eng.root_ready or self.two)) else 0.0
             groups.setdefault((eng.name, warm, budget, bres), (eng, []))[1].append((slot, node))
+            node.nid = next(self.nid_seq)
+            if self.trace is not None:
+                self.trace.append(self._trace_entry(eng, node, src if warm else None, budget, bres))
         # warm-start copies: a slot that is both a parent state (source) and a new node's slot
         # (destination) is read before it is overwritten; a cycle falls back to the root's state
         for eng, cps in copies.values():
@@ -421,7 +434,7 @@ class BranchAndBound:
             if self.warm and st not in (LP_INFEASIBLE, LP_CUTOFF):
                 lp.copy_state(slot, eng.root_slot)   # every later node can start from the root
             eng.root_ready = True
-            me0 = (eng, slot, eng.gen[slot])
+            me0 = (eng, slot, eng.gen[slot], node.nid)
             for idx, val in self.seed_leaves:
                 idx, val = np.asarray(idx), np.asarray(val, np.float64)
                 lb = self._ibound(idx, val)
@@ -462,9 +475,10 @@ class BranchAndBound:
                                 # a neighbour is no descendant of this leaf: its bound is its own
                                 self.pending.appendleft(_Node(self._ibound(idx, val), idx,
                                                               np.asarray(val, np.float64), LEAF,
-                                                              (eng, slot, eng.gen[slot]), node.depth))
+                                                              (eng, slot, eng.gen[slot], node.nid), node.depth))
             elif node.kind == LEAF and lp.diag(slot)["pres"] <= self.retry_res:
-                self.retry.append(_Node(bound, node.idx, node.val, RETRY, (eng, slot, eng.gen[slot]), node.depth))
+                self.retry.append(_Node(bound, node.idx, node.val, RETRY, (eng, slot, eng.gen[slot], node.nid),
+                                        node.depth))
             else:
                 res.unresolved += 1
                 self.unresolved_bounds.append(bound)
@@ -476,7 +490,7 @@ class BranchAndBound:
             return inc
         res.nodes += 1
         flow = lp.flows([slot])[0]
-        me = (eng, slot, eng.gen[slot])
+        me = (eng, slot, eng.gen[slot], node.nid)
         z, _ = lp.solution(slot, dense_x=False)
         for by_flow, min_flow in self.round_modes:
             leaf = self._round(node, flow, z[self.c0:self.c1], by_flow, min_flow)
@@ -500,6 +514,73 @@ class BranchAndBound:
                                            _Node(cb, idx, val, kind, me, node.depth + 1)))
         eng.free.append(slot)        # most recently finished last: its state survives longest
         return inc
+
+    def _frontier_hash(self):
+        """crc32 of the (sorted) open frontier: bounds, depths, fixings — identical on every rank at the split."""
+        import zlib
+        h = 0
+        for b, d, _, node in self.heap:
+            h = zlib.crc32(np.asarray([b, d], np.float64).tobytes(), h)
+            h = zlib.crc32(np.asarray(node.idx, np.int64).tobytes(), h)
+            h = zlib.crc32(np.asarray(node.val, np.float64).tobytes(), h)
+        return int(h)
+
+    def _rebalance(self, inc):
+        """Open-node rebalance of the sharded search (one all-gather of the frontier sizes, then one broadcast
+        per transfer): every rank whose frontier is empty takes half of the fullest remaining donor's (its
+        best-bound nodes, at most `batch`), so a rank whose subtrees died early does not idle.  The pairing
+        is computed identically on every rank from the gathered sizes; a moved node starts from its new
+        rank's root state."""
+        comm = self.comm
+        cnt = comm.gather([float(len(self.heap))])[:, 0].astype(np.int64)
+        idle = [r for r in range(comm.world) if cnt[r] == 0]
+        for r in idle:
+            d = int(np.argmax(cnt))
+            k = int(min(cnt[d] // 2, self.batch))
+            if k <= 0:
+                break
+            cnt[d] -= k
+            cnt[r] += k
+            if comm.rank == d:
+                give = [heapq.heappop(self.heap)[3] for _ in range(k)]
+                head = np.array([k] + [len(n.idx) for n in give], np.float64)
+            else:
+                head = np.zeros(k + 1)
+            head = comm.bcast(head, d)
+            lens = head[1:].astype(np.int64)
+            tot = int(lens.sum())
+            if comm.rank == d:
+                meta = np.array([[n.bound, n.depth, n.kind] for n in give], np.float64).ravel()
+                body = np.concatenate([meta, np.concatenate([n.idx for n in give]).astype(np.float64) if tot else [],
+                                       np.concatenate([n.val for n in give]) if tot else []])
+            else:
+                body = np.zeros(3 * k + 2 * tot)
+            body = comm.bcast(body, d)
+            if comm.rank == r:
+                meta, idx, val = body[:3 * k].reshape(k, 3), body[3 * k:3 * k + tot], body[3 * k + tot:]
+                o = 0
+                for q in range(k):
+                    n = int(lens[q])
+                    node = _Node(float(meta[q, 0]), idx[o:o + n].astype(np.int64), val[o:o + n].copy(),
+                                 int(meta[q, 2]), None, int(meta[q, 1]))
+                    o += n
+                    if node.bound < inc - self._gap_abs(inc):
+                        heapq.heappush(self.heap, (node.bound, -node.depth, next(self.seq), node))
+                        self.res.rebalanced += 1
+
+    def _trace_entry(self, eng, node, src, budget, bres):
+        """One submitted node LP for the replay fixture (bench.py's B&B node stream): the node's box (branching
+        nodes: their fixings; leaves: the open c / n — every other c and n is fixed to 0), the parent whose
+        state warm-started it (None: the model's root state or cold), its model and iteration budget."""
+        e = {"id": node.nid, "kind": _KIND_NAME[node.kind], "model": eng.name, "depth": node.depth,
+             "parent": None if node.parent is None else int(node.parent[3]),
+             "warm_from_parent": bool(src is not None and node.parent is not None and src == node.parent[1]),
+             "budget": int(budget), "bound_res": float(bres)}
+        if node.kind in (LEAF, RETRY):
+            e["open"] = [int(i) for i, v in zip(node.idx, node.val) if v > 0.5]
+        else:
+            e["fix"] = [[int(i) for i in node.idx], [float(v) for v in node.val]]
+        return e
 
     def _polish(self, res):
         """Re-solve the incumbent leaf from its own final state at polish_tol; keep the result when
@@ -580,6 +661,7 @@ class BranchAndBound:
         self.inflight = {}           # (engine name, slot) -> node
         self.keep = set()
         self.inc_node = None
+        self.nid_seq = itertools.count()
         L = _Engine(lp, self.reserved, "leaf")
         B = L if not self.two else _Engine(self.bound_lp, 1 if self.warm else 0, "bound")
         self.L, self.B = L, B
@@ -598,6 +680,7 @@ class BranchAndBound:
             if not sharded and len(self.heap) >= comm.world * self.batch and not self.inflight:
                 # deal the (identical on every rank) frontier: canonical order, round robin
                 self.heap.sort(key=lambda h: h[:3])
+                res.split_hash = self._frontier_hash()
                 self.heap = [h for i, h in enumerate(self.heap) if i % comm.world == comm.rank]
                 heapq.heapify(self.heap)
                 self.pending = deque(lf for i, lf in enumerate(self.pending) if i % comm.world == comm.rank)
@@ -617,6 +700,10 @@ class BranchAndBound:
             if stop:
                 limit_hit = True
                 break
+            loops = getattr(self, "_loops", 0) + 1
+            self._loops = loops
+            if sharded and comm.world > 1 and self.rebalance_every and loops % self.rebalance_every == 0:
+                self._rebalance(inc)
             # fill the free slots: retries, rounding leaves, then best-first open nodes
             items = []
             if not self.two:
@@ -638,7 +725,9 @@ class BranchAndBound:
                 if self.refroot is not None and L.free:
                     items.append((L, L.free.popleft(), self.refroot))
                     self.refroot = None
-                while B.free and self.heap:
+                # (the branching nodes wait for both roots: 32 bound LPs beside the lone reference root would
+                # starve its one-slot blocks — 512x256: not done after 60 s, 1.8 s alone)
+                while B.free and self.heap and (not B.root_ready or L.root_ready):
                     _, _, _, node = heapq.heappop(self.heap)
                     if node.bound >= inc - self._gap_abs(inc):
                         continue

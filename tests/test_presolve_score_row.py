@@ -32,7 +32,7 @@ def test_score_row_presolve_matches_highs(name, variant):
 
     class Recording(B.BranchAndBound):
         def _submit(self, items, inc):
-            seen.extend((node.idx.copy(), node.val.copy()) for _, node in items)
+            seen.extend((node.idx.copy(), node.val.copy()) for _, _, node in items)
             return super()._submit(items, inc)
 
     Recording(lp, data.workload_matrix, data.function_memory_matrix, data.node_memory_matrix, batch=2,
