@@ -87,7 +87,7 @@ class BnBResult:
         self.drained = 0         # LPs still iterating at a stop decision (stopped at their next check)
         # wall seconds by phase: device waits in advance, host work per finished LP, submits (incl.
         # warm-start copies), the drain after a stop, the end (routing fetch, polish, repair)
-        self.timing = dict.fromkeys(("advance", "finish", "submit", "drain", "end"), 0.0)
+        self.timing = dict.fromkeys(("advance", "finish", "submit", "drain", "end", "primal"), 0.0)
         self.timing["root"] = 0.0       # wall seconds until the root LP finished (it iterates alone)
         self.split_hash = None          # sharded search: crc32 of the frontier every rank dealt (must agree)
         self.rebalanced = 0             # open nodes this rank received from another rank
@@ -148,7 +148,7 @@ class BranchAndBound:
                  warm=True, root_max_iters=200000, check_every=12, polish_tol=1e-8, polish_iters=20000,
                  seed_leaves=None, integer_bound=None, improve=None, repair=None, node_bound_res=1e-2,
                  retry_res=math.inf, unit_flow_leaves=True, node_max_iters=None, bound_lp=None, bound_gap=1e-4,
-                 trace=None, rebalance_every=8):
+                 trace=None, rebalance_every=8, primal=None, primal_every=64):
         self.lp = lp
         self.two = bound_lp is not None
         self.N, self.F = lp.N, lp.F
@@ -169,6 +169,11 @@ class BranchAndBound:
         # sharded search: every rebalance_every loops, ranks with an empty frontier take open nodes from the
         # fullest ones (_rebalance; 0: never)
         self.rebalance_every = rebalance_every
+        # primal(idx, val, z, flow) -> [(idx, val)]: leaves completing a branching node's fixings, built from its
+        # LP (z, flow) with the instance's data (core/engine/heuristics.py); run at the root and then on every
+        # primal_every-th branched node
+        self.primal = primal
+        self.primal_every = max(1, int(primal_every))
         self.root_slot = lp.max_batch - 1
         self.inc_slot = lp.max_batch - 2
         self.tol, self.gap, self.max_iters = tol, gap, max_iters
@@ -501,6 +506,17 @@ class BranchAndBound:
                     lb = max(bound, self._ibound(*leaf))
                     if lb < inc - self._gap_abs(inc):
                         self.pending.append(_Node(lb, leaf[0], leaf[1], LEAF, me, node.depth + 1))
+        if self.primal is not None and (node.depth == 0 or res.nodes % self.primal_every == 0):
+            t = time.time()
+            for idx, val in self.primal(node.idx, node.val, z, flow):
+                key = np.packbits(np.asarray(val) > 0.5).tobytes()
+                if key not in self.seen_leaves:
+                    self.seen_leaves.add(key)
+                    lb = max(bound, self._ibound(idx, val))
+                    if lb < inc - self._gap_abs(inc):
+                        self.pending.appendleft(_Node(lb, np.asarray(idx), np.asarray(val, np.float64), LEAF, me,
+                                                      node.depth + 1))
+            res.timing["primal"] += time.time() - t
         var = self._branch_var(node, flow, slot, lp)
         if var is not None:
             for v in (1.0, 0.0):

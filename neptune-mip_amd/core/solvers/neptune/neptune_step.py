@@ -20,6 +20,7 @@ import numpy as np
 
 from ...engine import lp as _lp
 from ...engine.bnb import OPTIMAL, BranchAndBound
+from ...engine.heuristics import capacity_greedy
 from ...engine.routing import SparseRouting, repair_cpu
 from ..solver import Solver
 
@@ -98,6 +99,43 @@ class NeptuneStepBase(Solver):
         fixings (+inf: none exists), or None."""
         return None
 
+    def objective_weights(self):
+        """(cost per open node, coefficient of sum W D of the routing) of the step-1 objective, or None."""
+        return None
+
+    def primal_heuristic(self, layout):
+        """primal(idx, val, z, flow) -> [(idx, val)]: capacity-greedy leaves of a branching node (core/engine/
+        heuristics.py), the LP's n ranking the nodes; None where the objective has no node count."""
+        wts = self.objective_weights()
+        if wts is None or layout.get("n") is None:
+            return None
+        d = self.data
+        F, N = len(d.functions), len(d.nodes)
+        c0, c1 = layout["c"]
+        n0, n1 = layout["n"]
+        W = np.asarray(d.workload_matrix, np.float64)
+        D = np.asarray(d.node_delay_matrix, np.float64)
+        cpr = np.asarray(d.core_per_req_matrix, np.float64)
+        cores = np.asarray(d.node_cores_matrix, np.float64).reshape(N)
+        fmem = np.asarray(d.function_memory_matrix, np.float64).reshape(F)
+        nmem = np.asarray(d.node_memory_matrix, np.float64).reshape(N)
+
+        def primal(idx, val, z, flow):
+            idx = np.asarray(idx)
+            cfix = np.full(F * N, -1.0)
+            sel = (idx >= c0) & (idx < c1)
+            cfix[idx[sel] - c0] = np.asarray(val)[sel]
+            nfix = np.full(N, -1.0)
+            sel = (idx >= n0) & (idx < n1)
+            nfix[idx[sel] - n0] = np.asarray(val)[sel]
+            out = []
+            for C, n, _ in capacity_greedy(W, D, cpr, cores, fmem, nmem, np.asarray(z[n0:n1], np.float64),
+                                           flow=flow, tries=2, node_cost=wts[0], delay_coef=wts[1],
+                                           c_fix=cfix.reshape(F, N), n_fix=nfix):
+                out.append((np.concatenate([np.arange(c0, c1), np.arange(n0, n1)]), np.concatenate([C.ravel(), n])))
+            return out
+        return primal
+
     def improve(self, layout):
         """improve(idx, val, value) -> [(idx, val)]: neighbour placements of a new incumbent leaf
         worth solving (a local-search heuristic), or None."""
@@ -153,7 +191,7 @@ class NeptuneStepBase(Solver):
                                  improve=self.improve(model.layout()), repair=self.routing_repair(model.layout()),
                                  node_bound_res=self.node_bound_res, unit_flow_leaves=self.unit_flow_leaves,
                                  node_max_iters=max(1, int(self.lp_max_iters * self.node_iters_fraction)),
-                                 bound_lp=bmodel)
+                                 bound_lp=bmodel, primal=self.primal_heuristic(model.layout()))
             res = bnb.solve()
             layout = model.layout()
         finally:
@@ -228,6 +266,10 @@ class NeptuneStep1CPUMinUtilization(NeptuneStep1CPUBase):
     def upper_bound(self):
         return float(len(self.data.nodes))
 
+    def objective_weights(self):
+        # minimize_utilization (objectives.py:13-28): sum n
+        return 1.0, 0.0
+
     def results(self):
         x, c = super().results()
         self.data.prev_n = self.n_vector
@@ -270,6 +312,12 @@ class NeptuneStep1CPUMinDelayAndUtilization(NeptuneStep1CPUMinUtilization):
             if mwd > 0:
                 ub += (1 - self.alpha) * float((W * D.max(axis=1)[None, :]).sum()) / mwd
         return ub
+
+    def objective_weights(self):
+        # minimize_node_delay_and_utilization (objectives.py:30-53): alpha / N per open node, (1 - alpha) / MWD
+        W = np.asarray(self.data.workload_matrix, np.float64)
+        mwd = _mwd(self.data) if W.sum() else 0.0
+        return self.alpha / len(self.data.nodes), ((1 - self.alpha) / mwd if mwd > 0 else 0.0)
 
     def routing_coef(self):
         # minimize_node_delay_and_utilization (objectives.py:30-53): (1 - alpha) W[f, i] D[i, j] / MWD, no x

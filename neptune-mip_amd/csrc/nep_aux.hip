@@ -192,7 +192,7 @@ __global__ __launch_bounds__(256) void score_pass_j(DeviceView v, const double *
     const bool c = zi[v.il.oc + f * v.N + j] != 0.0;
     if (c) { mem += v.mem_f[f]; sumc += 1.0; }
   }
-  const double cores = v.hi[v.dl.o5 + j], nmem = v.hi[v.dl.o3 + j];
+  const double cores = v.capn[v.N + j], nmem = v.capn[j];
   double nval = 0.0, nused = 0.0;
   if (v.has_n) {
     nval = zi[v.il.on + j] != 0.0 ? 1.0 : 0.0;

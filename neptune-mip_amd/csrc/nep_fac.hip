@@ -10,7 +10,8 @@
 //                  f of the x <= c duals lambda, kept from the previous pass) — then every routing row of f:
 //                  the gradient with lambda[r, :], the simplex projection, lambda's dual step with the
 //                  reflected x and c, the Halpern combination of both, the CPU shares;
-//   fac_node_pass  per node: the memory (C3) and CPU (C5) rows, n, then the c <= n duals of every f.
+//   fac_node_pass  per node: n, the memory (C3) and CPU (C5) rows (capacities Mem_j n, cores_j n), then the
+//                  c <= n duals of every f.
 // Certificate point: x̂ with the least c every row allows (c = max_r x̂[r, j]) and the least n (max_f c).
 // Reference rows: constraints_step1.py:18-23 (C3), :27-34 (C4), :57-65 (C5), :101-103 (C8); the cuts hold for
 // the binaries of :5-15 and :69-78.  Objective objectives.py:24-53.
@@ -439,7 +440,7 @@ void fac_x_pass(DeviceView v, const int32_t *__restrict__ slots, int plain, int 
 }
 
 // One workgroup per (slot, block of kNodeJ nodes): the function shares of the node rows (fixed order), then
-// wave 0 updates C3, C5 and n, then every thread the c <= n duals of its functions at its node.
+// wave 0 updates n, C3 and C5, then every thread the c <= n duals of its functions at its node.
 template <bool CHECK, bool INIT>
 __global__ __launch_bounds__(kNodeThreads) void fac_node_pass(DeviceView v, const int32_t *__restrict__ slots, int first,
                                                               int plain, int it) {
@@ -518,23 +519,30 @@ __global__ __launch_bounds__(kNodeThreads) void fac_node_pass(DeviceView v, cons
         cmax = fmax(cmax, red[4][q][lane]);
       }
     }
-    if (CHECK) {   // certificate point: C3 at the repaired c, C5 at x̂
-      a.res = fmax(a.res, row_viol(memr, p3.lo, p3.hi) / nrm3);
-      a.res = fmax(a.res, row_viol(U, p5.lo, p5.hi) / nrm5);
-    }
-    dual_step_p<CHECK, INIT>(y, ya, kz, kza, dl.o3 + j, memc, p3, sigma, copy_anchor, halp, lam, a);
-    const double y5n = dual_step_p<CHECK, INIT>(y, ya, kz, kza, dl.o5 + j, U, p5, sigma, copy_anchor, halp, lam, a);
-    v.kty[slot * v.skty + (int64_t)F * NP + j] = (float)y5n;
-    // n[j]: the c <= n rows give it the coefficient -1 each, so its reduced cost is cost_n + sum_f mu[f, j]
+    // n[j] first (its T step prices the rows at the old duals): the c <= n rows give it the coefficient -1
+    // each, C3 -Mem_j and C5 -cores_j, so its reduced cost is cost_n + sum_f mu[f, j] + Mem_j y3 + cores_j y5
+    const double capM = v.capn[j], capC = v.capn[N + j];
     const double n_old = pn.z;
-    const double nn = primal_step_p<CHECK>(zi, zia, il.on + j, pn.cost + musum, pn, tau, copy_anchor, halp, lam, a);
+    const double nn = primal_step_p<CHECK>(zi, zia, il.on + j, pn.cost + musum + capM * p3.y + capC * p5.y, pn, tau,
+                                           copy_anchor, halp, lam, a);
     nref[lane] = 2.0 * nn - n_old;
-    if (CHECK) {   // repaired n: the least value every c[:, j] allows (n >= c), within the node box
-      const double nr = fmax(pn.lb, cmax);
+    if (CHECK) {   // repaired n: the least value the repaired c (n >= c, Mem_j n >= its memory) and x̂ (cores_j
+                   // n >= its CPU) allow, within the node box; C3 / C5 at that point
+      double nr = fmax(pn.lb, cmax);
+      if (capM > 0.0) nr = fmax(nr, memr / capM);
+      if (capC > 0.0) nr = fmax(nr, U / capC);
       a.res = fmax(a.res, nr - pn.ub);
+      nr = fmin(nr, pn.ub);
+      a.res = fmax(a.res, row_viol(memr - capM * nr, p3.lo, p3.hi) / nrm3);
+      a.res = fmax(a.res, row_viol(U - capC * nr, p5.lo, p5.hi) / nrm5);
       a.pobj += pn.cost * nr;
       v.zr[slot * v.sint + il.on + j] = nr;
     }
+    // C3 / C5 at (ĉ, x̂, n̂)
+    dual_step_p<CHECK, INIT>(y, ya, kz, kza, dl.o3 + j, memc - capM * nn, p3, sigma, copy_anchor, halp, lam, a);
+    const double y5n =
+        dual_step_p<CHECK, INIT>(y, ya, kz, kza, dl.o5 + j, U - capC * nn, p5, sigma, copy_anchor, halp, lam, a);
+    v.kty[slot * v.skty + (int64_t)F * NP + j] = (float)y5n;
   }
   __syncthreads();
   // the c <= n duals mu[f, j] of this node block: reflected activity (2ĉ - c) - (2n̂ - n); their Lagrangian

@@ -82,6 +82,7 @@ struct Model {
   int N = 0, F = 0, NP = 0, variant = 0, step = 1, has_n = 0, step2 = 0;
   int fac = 0;                      // NEP_RELAX_FACILITY (include/neptune_lp.h)
   std::vector<double> rhoL;         // fac: row scale of the x[r, j] <= c[f, j] rows, per (f, j)
+  std::vector<double> capn;         // [2][N] node memory, node cores
   double alpha = 0.5, M = 1e6, eps = 1e-6, sigma4 = -1, cost_n = 0, score_n_coef = 0, w_dis = 0;
   int R = 0, JB = 0, CPL = 1, max_batch = 1;
   DualLayout dl{};
@@ -388,9 +389,13 @@ int build(Model &m, const nep_model_desc &d) {
     m.lo[dl.o2 + k] = -m.eps;
   }
   for (int k = 0; k < FN && m.fac; ++k) m.hi[dl.oQ + k] = 0.0;
+  m.capn.resize(2 * (size_t)N);
   for (int j = 0; j < N; ++j) {
-    m.hi[dl.o3 + j] = d.node_memory[j];
-    m.hi[dl.o5 + j] = d.node_cores[j];
+    m.capn[j] = d.node_memory[j];
+    m.capn[N + j] = d.node_cores[j];
+    // (fac: C3 / C5 carry n[j] on the right, mem c - Mem_j n <= 0 and CPU - cores_j n <= 0)
+    m.hi[dl.o3 + j] = m.fac ? 0.0 : d.node_memory[j];
+    m.hi[dl.o5 + j] = m.fac ? 0.0 : d.node_cores[j];
     if (m.has_n && !m.fac) { m.hi[dl.o6 + j] = 0.0; m.lo[dl.o7 + j] = -m.eps; }
   }
   if (m.step2) {
@@ -443,6 +448,11 @@ int build(Model &m, const nep_model_desc &d) {
         K.add(dl.oD3b, il.oc + k, 1.0);
         K.add(dl.oD4, il.oc + k, m.sigma4);
       }
+    }
+  if (m.fac)
+    for (int j = 0; j < N; ++j) {
+      K.add(dl.o3 + j, il.on + j, -m.capn[j]);
+      K.add(dl.o5 + j, il.on + j, -m.capn[N + j]);
     }
   if (m.has_n && !m.fac)
     for (int j = 0; j < N; ++j) {
@@ -615,6 +625,7 @@ int build(Model &m, const nep_model_desc &d) {
       double b = 0.0;
       if (std::isfinite(m.lo[k])) b = std::max(b, std::fabs(m.lo[k]));
       if (std::isfinite(m.hi[k])) b = std::max(b, std::fabs(m.hi[k]));
+      if (m.fac && k >= dl.o3 && k < dl.o5 + N) b = m.capn[k < dl.o5 ? k - dl.o3 : N + k - dl.o5];   // (hi = 0)
       bn2 += std::pow(m.rho[k] * b, 2);
     }
     m.omega0 = (cn2 > 0.0 && bn2 > 0.0) ? std::sqrt(cn2) / std::sqrt(bn2) : 1.0;
@@ -662,6 +673,7 @@ int setup_device(Model &m, int max_batch, void *stream) {
   if ((rc = upload(m, &v.rownorm, m.rownorm))) return rc;
   if ((rc = upload(m, &v.cost_int, m.cost_int))) return rc;
   if ((rc = upload(m, &v.mem_f, m.mem_f))) return rc;
+  if ((rc = upload(m, &v.capn, m.capn))) return rc;
   return NEP_OK;
 }
 

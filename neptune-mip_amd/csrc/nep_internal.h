@@ -137,6 +137,7 @@ struct DeviceView {
   const int32_t *frow;
   const float *D, *cpr;
   const double *gam, *rho, *lo, *hi, *rownorm, *cost_int, *mem_f;
+  const double *capn;                    // [2][N] node memory, node cores (C3 / C5 capacities)
   // per slot (base pointers; slot stride below)
   float *x;
   float *xa;

@@ -221,7 +221,9 @@ def facility_relaxation(m, data):
     step-1 MinUtilization / MinDelayAndUtilization model `m` (build_model's dict): the big-M pairs C1/C2
     (constraints_step1.py:5-15) and C6/C7 (:69-78) are replaced by x[i,f,j] <= c[f,j] for every (i, f, j) and
     c[f,j] <= n[j] — valid for every integral placement (c = 0 forces the column's flow to 0 through C1; n = 0
-    forces c = 0 through C6), and implying C1 and C6 for integral c, n; C2 / C7 (the eps floors) are relaxed.
+    forces c = 0 through C6), and implying C1 and C6 for integral c, n; C2 / C7 (the eps floors) are relaxed;
+    the capacity rows C3 / C5 take n[j] on their right-hand side (Mem_j n[j], cores_j n[j]: a closed node has
+    neither memory nor CPU for anything).
     Test infrastructure: its HiGHS value is what the engine's facility LPs are checked against."""
     L = m["layout"]
     assert L.step == 1 and L.has_n, "step-1 MinUtilization / MinDelayAndUtilization only"
@@ -233,7 +235,18 @@ def facility_relaxation(m, data):
     coo = A.tocoo()
     big = (coo.col >= L.n0) & (coo.col < L.n0 + N) & ((coo.data == -float(BIG_M)) | (coo.data == -1.0))
     keep[np.unique(coo.row[big])] = False                       # C6/C7 (the rows with -M n / -n)
-    A, lo, hi = A[keep], m["lo"][keep], m["hi"][keep]
+    # capacity rows scaled by n: C3 sum_f mem_f c[f,j] <= Mem_j n[j], C5 CPU_j <= cores_j n[j] (valid: an
+    # integral n[j] = 0 closes every c[:, j] and x[:, :, j]); rows C3 / C5 are the first N rows after C1/C2 and
+    # the N rows after C4 (build_model's order)
+    r3 = 2 * F * N + np.arange(N)
+    r5 = 2 * F * N + N + F * N + np.arange(N)
+    cap = sp.csr_matrix((np.concatenate([-m["hi"][r3], -m["hi"][r5]]),
+                         (np.concatenate([r3, r5]), np.concatenate([L.n0 + np.arange(N)] * 2))), shape=A.shape)
+    A = (A + cap).tocsr()
+    hi = m["hi"].copy()
+    hi[r3] = 0.0
+    hi[r5] = 0.0
+    A, lo, hi = A[keep], m["lo"][keep], hi[keep]
     nv = A.shape[1]
     k = F * N * N
     r = np.arange(k)

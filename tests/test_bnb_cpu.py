@@ -127,3 +127,34 @@ def test_bnb_two_models_matches_recorded_mip(name, k):
     else:
         assert res.status == INFEASIBLE, res.as_dict()
     assert res.lp_status_kind["refroot"]["certified"] + res.lp_status_kind["refroot"]["cutoff"] <= 1
+
+
+@pytest.mark.parametrize("name,k", STEP1_N[:8])
+def test_bnb_primal_heuristic_keeps_optimum(name, k):
+    """The capacity-greedy primal heuristic (core/engine/heuristics.py, NeptuneStepBase.primal_heuristic) hooked
+    into the two-model search: its leaves are feasible for the reference rows (every one the leaf LP solves
+    is an integral placement of the reference model), so the search still ends at the recorded MIP optimum."""
+    from core.engine.bnb import INFEASIBLE, OPTIMAL, BranchAndBound
+    from core.solvers import SOLVERS
+    from oracle_lp import StreamingOracleLP
+    p, data = _data(name)
+    rec = G[name]["models"][k]
+    variant = VARIANT[p["solver"]["type"]]
+    alpha = p["solver"].get("args", {}).get("alpha", 0.5)
+    solver = SOLVERS[p["solver"]["type"]](**p["solver"].get("args", {}))
+    step1 = solver.step1 if hasattr(solver, "step1") else solver
+    step1.load_data(data)
+    lp = StreamingOracleLP(data, variant, step=1, max_batch=10, alpha=alpha)
+    blp = StreamingOracleLP(data, variant, step=1, max_batch=9, alpha=alpha, relaxation=1)
+    primal = step1.primal_heuristic(lp.layout())
+    assert primal is not None
+    calls = []
+    res = BranchAndBound(lp, data.workload_matrix, data.function_memory_matrix, data.node_memory_matrix,
+                         batch=8, node_limit=20000, bound_lp=blp, primal_every=4,
+                         primal=lambda *a: calls.append(1) or primal(*a)).solve()
+    assert calls
+    if rec["status"] == 0:
+        assert res.status == OPTIMAL, res.as_dict()
+        assert _close(res.objective, rec["mip_objective"]), (res.objective, rec["mip_objective"])
+    else:
+        assert res.status == INFEASIBLE, res.as_dict()
