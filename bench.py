@@ -75,8 +75,11 @@ def parse(argv=None):
     ap.add_argument("--cold", action="store_true", help="cold-start every node LP")
     ap.add_argument("--stream", default="auto", choices=("auto", "replay", "children"),
                     help="the timed node-LP stream: the product B&B's recorded nodes (replay, tests/golden/"
-                         "bnb_trace_<N>x<F>_s<seed>.json) or root children with --fix random fixings; auto: "
+                         "bnb_trace_<N>x<F>_s<seed>.json.gz) or root children with --fix random fixings; auto: "
                          "replay when the trace exists")
+    ap.add_argument("--native-steps", type=int, default=8,
+                    help="with the replay stream: steps of the native-model replay timed after it (each recorded "
+                         "box on the model the product ran it on; 0 = skip)")
     ap.add_argument("--children-steps", type=int, default=24,
                     help="with the replay stream: steps of the children stream timed after it (secondary figure)")
     ap.add_argument("--cpu-budget", type=float, default=150.0,
@@ -250,11 +253,12 @@ def cpu_baseline(N, F, seed, fix, budget, workers):
 def bnb_section(a, rank, world, dev, N, F):
     """The product's own branch-and-bound (core/engine/bnb.py, the search SCIP runs inside
     pywraplp Solve(), solver.py:35-40) on BASELINE config 3's / 4's instance (256x128, 512x256, step-1
-    NeptuneMinDelayAndUtilization), time-limited: certified node LPs per second INSIDE the B&B, the
-    node-LP mix (finished LPs per status, iteration percentiles), nodes, incumbent, bound and gap.
-    With N ranks the search is the sharded one (subtrees per rank, one packed all-gather per loop over
+    NeptuneMinDelayAndUtilization), time-limited, configured as the product's step 1 runs it
+    (NeptuneStepBase.branch_and_bound: facility-relaxation bounds on the branching nodes, reference-model
+    leaves, the capacity-greedy root heuristic): node LPs per second INSIDE the B&B, the
+    node-LP mix (finished LPs per model/kind and status, iteration percentiles), nodes, incumbent, bound and
+    gap.  With N ranks the search is the sharded one (subtrees per rank, one packed all-gather per loop over
     RCCL: core/engine/comm.TorchComm)."""
-    from core.engine.bnb import BranchAndBound
     from core.engine.comm import LocalComm, TorchComm
     from core.engine.lp import LPModel
     from core.solvers.neptune.neptune_step import NeptuneStep1CPUMinDelayAndUtilization
@@ -263,15 +267,14 @@ def bnb_section(a, rank, world, dev, N, F):
     p = synthetic_payload(N, F, seed=a.seed)
     data = data_to_solver_input(p, with_db=False)
     alpha = p["solver"]["args"]["alpha"]
-    st1 = NeptuneStep1CPUMinDelayAndUtilization(alpha=alpha, verbose=False)
+    st1 = NeptuneStep1CPUMinDelayAndUtilization(alpha=alpha, verbose=False, batch=a.batch, lp_tol=a.tol,
+                                                lp_max_iters=a.max_iters)
     st1.load_data(data)
-    ub = st1.upper_bound()
     m = LPModel(data, "MinDelayAndUtilization", step=1, alpha=alpha, max_batch=a.batch + 2)
+    bm = st1.bound_model(data, a.batch + 1)
     comm = TorchComm(device=dev) if world > 1 else LocalComm()
-    bnb = BranchAndBound(m, data.workload_matrix, data.function_memory_matrix, data.node_memory_matrix,
-                         batch=a.batch, tol=a.tol, max_iters=a.max_iters, time_limit=a.bnb_seconds,
-                         upper_bound=ub * (1 + 1e-6) + 1e-6, comm=comm, check_every=a.check_every,
-                         root_max_iters=a.root_max_iters, node_max_iters=a.max_iters // 4)
+    bnb = st1.branch_and_bound(m, bm, time_limit=a.bnb_seconds, comm=comm, check_every=a.check_every,
+                               root_max_iters=a.root_max_iters)
     m.reset_stats()
     t0 = time.perf_counter()
     res = bnb.solve()
@@ -279,6 +282,8 @@ def bnb_section(a, rank, world, dev, N, F):
     if world > 1:
         wall = comm.max(wall)
     m.close()
+    if bm is not None:
+        bm.close()
     inc = res.objective
     gap = None if inc is None else (inc - res.bound) / max(1.0, abs(inc))
     d = res.as_dict()
@@ -293,35 +298,48 @@ def bnb_section(a, rank, world, dev, N, F):
             "drained_at_stop": res.drained,
             "lp_iters_p50_p90_p99_max_rank0": d["lp_iters_p50_p90_p99_max"],
             "lp_iterations": res.lp_iterations, "incumbent": inc, "bound": res.bound, "rel_gap": gap,
-            "ranks": world}
+            "root_seconds": res.timing.get("root"), "host_seconds": {k: res.timing.get(k) for k in
+                                                                  ("finish", "submit", "primal", "end")},
+            "advance_seconds": res.timing.get("advance"), "ranks": world}
 
 
 class ReplayStream:
     """The node LPs the product branch-and-bound submitted at this size (recorded by tools/record_bnb_trace.py
-    into tests/golden/bnb_trace_<N>x<F>_s<seed>.json), replayed in submission order as LP relaxations of the
-    REFERENCE model — the LP SCIP solves at those nodes (solver.py:35-40): a branching node's box is its
-    fixings, a leaf's fixes every c and n (open ones to 1).  `batch` in flight; a node starts from its
-    parent's final PDHG state when a slot still holds it (slots are refilled oldest-finished first, as the
-    B&B does), else from the root's.  With `world` ranks, rank r takes entries r, r + world, ... (the trace
-    repeated as often as the steps need)."""
+    into tests/golden/bnb_trace_<N>x<F>_s<seed>.json.gz), replayed in submission order.  A branching node's box
+    is its fixings, a leaf's fixes every c and n (open ones to 1).
 
-    def __init__(self, m, root, a, rank, world, trace):
-        self.m, self.root, self.a = m, root, a
-        self.lps = trace["lps"]
+    models: {"leaf": (reference LPModel, root slot), "bound": (facility LPModel, root slot) or absent}.
+    native=False: every box is an LP relaxation of the REFERENCE model (the LP SCIP solves at that node,
+    solver.py:35-40) at the bench's tol / --max-iters, to its certificate.  native=True: every box on the
+    model the product ran it on (branching nodes: the facility relaxation) with the product's
+    iteration budget, stops (bound_res, gap_tol) and incumbent cutoff — the product's own node-LP mix.
+    `batch` slots per model; a node starts from its parent's final PDHG state when a slot of its model still
+    holds it (slots are refilled oldest-finished first, as the B&B does; the recorded run's own slot reuse
+    is not replayed), else from that model's root.  The
+    two roots (depth-0 entries) were solved before the timed region and are skipped.  With `world` ranks,
+    rank r takes entries r, r + world, ... (the trace repeated as often as the steps need)."""
+
+    def __init__(self, models, a, rank, world, trace, native=False):
+        self.models, self.a, self.native = models, a, native
+        self.lps = [e for e in trace["lps"] if e["parent"] is not None]
         self.pos, self.stride = rank, world
         self.counter = 0
         self.done = []          # (status, obj, primal_obj, iters) per completed node
-        self.where = {}         # node key -> slot holding its final state
-        self.held = {}          # slot -> node key
-        self.running = {}       # slot -> node key
-        self.free = []
+        self.kinds = []         # (model, kind) per completed node
+        self.where = {}         # (model, node key) -> slot holding its final state
+        self.held = {}          # (model, slot) -> node key
+        self.running = {}       # (model, slot) -> (node key, kind)
+        self.free = {name: list(range(a.batch)) for name in models}
         self.warm_parent = 0
 
-    def _box(self, e):
+    def _model(self, e):
+        return e["model"] if (self.native and e["model"] in self.models) else "leaf"
+
+    def _box(self, m, e):
         import numpy as np
         F, N = self.a.functions, self.a.nodes
-        lb = np.full(self.m.n_int, -np.inf)
-        ub = np.full(self.m.n_int, np.inf)
+        lb = np.full(m.n_int, -np.inf)
+        ub = np.full(m.n_int, np.inf)
         if "open" in e:
             lb[:F * N + N] = ub[:F * N + N] = 0.0
             lb[e["open"]] = ub[e["open"]] = 1.0
@@ -331,55 +349,66 @@ class ReplayStream:
         return lb, ub
 
     def _refill(self):
-        import numpy as np
+        import math
         from core.engine.lp import LP_INFEASIBLE
         a = self.a
-        while self.free and self.counter < self.limit:
-            slot = self.free.pop(0)
-            k = self.pos
+        while self.counter < self.limit:
+            rep, i = divmod(self.pos, len(self.lps))
+            e = self.lps[i]
+            name = self._model(e)
+            if not self.free[name]:
+                break                            # in order: the next node waits for a slot of its model
+            m, root = self.models[name]
+            slot = self.free[name].pop(0)
             self.pos += self.stride
-            rep, e = divmod(k, len(self.lps))
-            e = self.lps[e]
             key = (rep, e["id"])
-            pkey = (rep, e["parent"])
-            old = self.held.pop(slot, None)       # this slot's finished state is overwritten now
+            pkey = (name, (rep, e["parent"]))
+            old = self.held.pop((name, slot), None)       # this slot's finished state is overwritten now
             if old is not None:
-                self.where.pop(old, None)
-            src = self.root
-            if e["warm_from_parent"] and pkey in self.where:
+                self.where.pop((name, old), None)
+            src = root
+            if pkey in self.where:
                 src = self.where[pkey]
                 self.warm_parent += 1
-            self.m.copy_state(src, slot)
-            lb, ub = self._box(e)
+            m.copy_state(src, slot)
+            lb, ub = self._box(m, e)
             self.counter += 1
-            st = self.m.submit([slot], lb[None], ub[None], tol=a.tol, max_iters=a.max_iters,
-                               check_every=a.check_every, warm_start=True, warm_omega_floor=a.warm_omega_floor)
+            if self.native:
+                kw = dict(max_iters=e["budget"], bound_res=e["bound_res"], gap_tol=e.get("gap_tol", 0.0),
+                          cutoff=math.inf if e.get("cutoff") is None else e["cutoff"])
+            else:
+                kw = dict(max_iters=a.max_iters)
+            st = m.submit([slot], lb[None], ub[None], tol=a.tol, check_every=a.check_every, warm_start=True,
+                          warm_omega_floor=a.warm_omega_floor, **kw)
             if int(st[0]) == LP_INFEASIBLE:
                 self.done.append((LP_INFEASIBLE, float("inf"), float("nan"), 0))
-                self.free.append(slot)
+                self.kinds.append((name, e["kind"]))
+                self.free[name].append(slot)
             else:
-                self.running[slot] = key
+                self.running[(name, slot)] = (key, e["kind"])
 
     def drain(self, n):
-        """Stream the next n recorded nodes through the `batch` slots until every one of them finished."""
+        """Stream the next n recorded nodes through the slots until every one of them finished."""
         self.limit = self.counter + n
-        if not self.free and not self.running:
-            self.free = list(range(self.a.batch))
         self._refill()
-        while self.m.active() > 0:
-            r = self.m.advance(1)
-            for i, slot in enumerate(r["slots"].tolist()):
-                self.done.append((int(r["status"][i]), float(r["obj"][i]), float(r["primal_obj"][i]),
-                                  int(r["iters"][i])))
-                key = self.running.pop(slot)
-                self.where[key] = slot
-                self.held[slot] = key
-                self.free.append(slot)
+        while any(m.active() > 0 for m, _ in self.models.values()):
+            for name, (m, _) in self.models.items():
+                if m.active() <= 0:
+                    continue
+                r = m.advance(0 if len(self.models) > 1 else 1)
+                for i, slot in enumerate(r["slots"].tolist()):
+                    self.done.append((int(r["status"][i]), float(r["obj"][i]), float(r["primal_obj"][i]),
+                                      int(r["iters"][i])))
+                    key, kind = self.running.pop((name, slot))
+                    self.kinds.append((name, kind))
+                    self.where[(name, key)] = slot
+                    self.held[(name, slot)] = key
+                    self.free[name].append(slot)
             self._refill()
 
 
 def trace_path(a):
-    return os.path.join(REPO, "tests", "golden", f"bnb_trace_{a.nodes}x{a.functions}_s{a.seed}.json")
+    return os.path.join(REPO, "tests", "golden", f"bnb_trace_{a.nodes}x{a.functions}_s{a.seed}.json.gz")
 
 
 class NodeStream:
@@ -446,7 +475,9 @@ def main():
         import torch.distributed as td
         td.init_process_group("nccl", device_id=dev)
 
-    from core.engine.lp import LPModel, LP_BOUND, LP_CUTOFF, LP_INFEASIBLE, LP_OPTIMAL
+    from core.engine.lp import LPModel, LP_BOUND, LP_CUTOFF, LP_INFEASIBLE, LP_ITERATION_LIMIT, LP_OPTIMAL
+    STATUS_NAME = {LP_OPTIMAL: "certified", LP_ITERATION_LIMIT: "limit", LP_INFEASIBLE: "infeasible",
+                   LP_CUTOFF: "cutoff", LP_BOUND: "bound"}
     from core.utils import data_to_solver_input
     from core.utils.synthetic import synthetic_payload
 
@@ -483,15 +514,32 @@ def main():
     kind = a.stream
     if kind == "auto":
         kind = "replay" if os.path.exists(trace_path(a)) else "children"
+    bm = fac_root = None
     if kind == "replay":
-        with open(trace_path(a)) as fh:
-            stream = ReplayStream(m, root, a, rank, world, json.load(fh))
+        import gzip
+        with gzip.open(trace_path(a), "rt") as fh:
+            trace = json.load(fh)
+        stream = ReplayStream({"leaf": (m, root)}, a, rank, world, trace)
+        if a.native_steps > 0:
+            # the facility relaxation (the product's bound model) and its root, stopped as the product's is:
+            # bound converged (bound_res 1e-2, gap_tol 1e-4) or the root budget (core/engine/bnb.py _submit)
+            from core.engine.lp import RELAX_FACILITY
+            bm = LPModel(data, "MinDelayAndUtilization", step=1, alpha=alpha, max_batch=B + 1,
+                         relaxation=RELAX_FACILITY)
+            t_fr = time.perf_counter()
+            fr = bm.solve([root], tol=a.tol, max_iters=a.root_max_iters, check_every=a.check_every,
+                        bound_res=1e-2, gap_tol=1e-4)
+            fac_root = {"status": int(fr["status"][0]), "obj": float(fr["obj"][0]), "iters": int(fr["iters"][0]),
+                        "seconds": time.perf_counter() - t_fr}
+            log(f"rank {rank}: facility-relaxation root: {fac_root}")
     else:
         stream = NodeStream(m, root, a, rank)
 
     def timed(stream, steps, tag):
         """steps * B nodes of `stream`, drained, timed between barriers (max over ranks)."""
         m.reset_stats()
+        if bm is not None:
+            bm.reset_stats()
         i0 = len(stream.done)
         if dist:
             td.barrier()
@@ -537,7 +585,25 @@ def main():
     st = prim["stats"]
     wall, n_ok, n_it, gmax, n_done = prim["wall"], prim["certified"], prim["iterations"], prim["gmax"], prim["completed"]
     iq, util = prim["iters_p50_p90_max"], prim["util"]
-    second = None
+    second = native = None
+    if kind == "replay" and bm is not None:
+        # the product's own node-LP mix: every recorded box on the model the B&B ran it on, with its budget,
+        # stops and cutoff (branching nodes: the facility relaxation; leaves: the reference model)
+        ns = ReplayStream({"leaf": (m, root), "bound": (bm, root)}, a, rank, world, trace, native=True)
+        nat = timed(ns, a.native_steps, "replay (native models)")
+        mix = {}
+        for (name, k), r in zip(ns.kinds, ns.done):
+            d = mix.setdefault(f"{name}/{k}", {})
+            s_ = STATUS_NAME.get(r[0], str(r[0]))
+            d[s_] = d.get(s_, 0) + 1
+        native = {"workload": workload_name(a, "replay") + "_native_models", "resolved_lp_per_s":
+                  nat["resolved"] / nat["wall"], "certified_lp_per_s": nat["certified"] / nat["wall"],
+                  "resolved": nat["resolved"], "certified": nat["certified"], "completed": nat["completed"],
+                  "steps": a.native_steps, "wall_s": nat["wall"], "iters_p50_p90_max": nat["iters_p50_p90_max"],
+                  "status_by_model_kind_rank0": mix, "facility_root": fac_root,
+                  "note": "resolved = certified + infeasible + cutoff + bound-converged (LP_BOUND); branching "
+                          "nodes that end at their 1024-iteration budget keep a valid bound but are not counted"}
+        bm.close()
     if kind == "replay" and a.children_steps > 0:
         # the secondary figure: the round-1..3 stream of root children with 2 random c-fixings each
         cs = NodeStream(m, root, a, rank)
@@ -609,6 +675,7 @@ def main():
                "slot_utilisation_rank0": util,
                "root_obj": root_obj, "root_iters": root_iters, "root_seconds": root_seconds,
                "root_polish": root_polish},
+        "native_replay": native,
         "children_stream": second,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_over_algorithmic": traffic_ratio,

@@ -148,7 +148,7 @@ class BranchAndBound:
                  warm=True, root_max_iters=200000, check_every=12, polish_tol=1e-8, polish_iters=20000,
                  seed_leaves=None, integer_bound=None, improve=None, repair=None, node_bound_res=1e-2,
                  retry_res=math.inf, unit_flow_leaves=True, node_max_iters=None, bound_lp=None, bound_gap=1e-4,
-                 trace=None, rebalance_every=8, primal=None, primal_every=64):
+                 trace=None, rebalance_every=8, primal=None, primal_every=0):
         self.lp = lp
         self.two = bound_lp is not None
         self.N, self.F = lp.N, lp.F
@@ -170,10 +170,12 @@ class BranchAndBound:
         # fullest ones (_rebalance; 0: never)
         self.rebalance_every = rebalance_every
         # primal(idx, val, z, flow) -> [(idx, val)]: leaves completing a branching node's fixings, built from its
-        # LP (z, flow) with the instance's data (core/engine/heuristics.py); run at the root and then on every
-        # primal_every-th branched node
+        # LP (z, flow) with the instance's data (core/engine/heuristics.py); run at the root and, with
+        # primal_every > 0, on every primal_every-th branched node (0: the root only — with the facility
+        # relaxation's bounds the nodes' own rounding leaves find the same incumbents at 256x128 / 512x256, and
+        # the greedy costs ~2 s per call at 512x256)
         self.primal = primal
-        self.primal_every = max(1, int(primal_every))
+        self.primal_every = max(0, int(primal_every))
         self.root_slot = lp.max_batch - 1
         self.inc_slot = lp.max_batch - 2
         self.tol, self.gap, self.max_iters = tol, gap, max_iters
@@ -361,6 +363,7 @@ class BranchAndBound:
         """items: [(engine, slot, node)].  One nep_lp_submit per (engine, warm, iteration budget) group."""
         groups = {}
         copies = {}
+        cutoff = min(inc, self.ub0)
         for eng, slot, node in items:
             warm, src = False, None
             if self.warm and eng.root_ready:
@@ -379,7 +382,7 @@ class BranchAndBound:
             groups.setdefault((eng.name, warm, budget, bres), (eng, []))[1].append((slot, node))
             node.nid = next(self.nid_seq)
             if self.trace is not None:
-                self.trace.append(self._trace_entry(eng, node, src if warm else None, budget, bres))
+                self.trace.append(self._trace_entry(eng, node, src if warm else None, budget, bres, cutoff))
         # warm-start copies: a slot that is both a parent state (source) and a new node's slot
         # (destination) is read before it is overwritten; a cycle falls back to the root's state
         for eng, cps in copies.values():
@@ -392,7 +395,6 @@ class BranchAndBound:
                     continue
                 src, dst = cps.pop(k)
                 eng.lp.copy_state(src, dst)
-        cutoff = min(inc, self.ub0)
         for (_, warm, budget, bres), (eng, its) in groups.items():
             n_int = eng.lp.n_int
             slots = np.array([s for s, _ in its], np.int32)
@@ -506,7 +508,7 @@ class BranchAndBound:
                     lb = max(bound, self._ibound(*leaf))
                     if lb < inc - self._gap_abs(inc):
                         self.pending.append(_Node(lb, leaf[0], leaf[1], LEAF, me, node.depth + 1))
-        if self.primal is not None and (node.depth == 0 or res.nodes % self.primal_every == 0):
+        if self.primal is not None and (node.depth == 0 or (self.primal_every and res.nodes % self.primal_every == 0)):
             t = time.time()
             for idx, val in self.primal(node.idx, node.val, z, flow):
                 key = np.packbits(np.asarray(val) > 0.5).tobytes()
@@ -584,14 +586,17 @@ class BranchAndBound:
                         heapq.heappush(self.heap, (node.bound, -node.depth, next(self.seq), node))
                         self.res.rebalanced += 1
 
-    def _trace_entry(self, eng, node, src, budget, bres):
+    def _trace_entry(self, eng, node, src, budget, bres, cutoff):
         """One submitted node LP for the replay fixture (bench.py's B&B node stream): the node's box (branching
         nodes: their fixings; leaves: the open c / n — every other c and n is fixed to 0), the parent whose
-        state warm-started it (None: the model's root state or cold), its model and iteration budget."""
+        state warm-started it (None: the model's root state or cold), its model, iteration budget, stops
+        (bound_res, gap_tol) and the incumbent cutoff it ran under (None: none yet)."""
         e = {"id": node.nid, "kind": _KIND_NAME[node.kind], "model": eng.name, "depth": node.depth,
              "parent": None if node.parent is None else int(node.parent[3]),
              "warm_from_parent": bool(src is not None and node.parent is not None and src == node.parent[1]),
-             "budget": int(budget), "bound_res": float(bres)}
+             "budget": int(budget), "bound_res": float(bres),
+             "gap_tol": float(self.bound_gap if (self.two and eng is self.B) else 0.0),
+             "cutoff": float(cutoff) if math.isfinite(cutoff) else None}
         if node.kind in (LEAF, RETRY):
             e["open"] = [int(i) for i, v in zip(node.idx, node.val) if v > 0.5]
         else:

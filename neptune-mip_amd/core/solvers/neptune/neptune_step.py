@@ -171,6 +171,24 @@ class NeptuneStepBase(Solver):
         moves may use (None: no such row over x)"""
         return None
 
+    def branch_and_bound(self, model, bmodel=None, **overrides):
+        """The step's search (core/engine/bnb.py) over `model` (leaves; max_batch >= batch + 2) and `bmodel`
+        (the bound model of bound_model(), or None), configured as solve() runs it; `overrides` replace
+        BranchAndBound arguments (the bench's comm / time limit / iteration budgets)."""
+        data = self.data
+        ub = self.upper_bound()
+        layout = model.layout()
+        kw = dict(batch=self.batch, tol=self.lp_tol, max_iters=self.lp_max_iters, node_limit=self.node_limit,
+                  time_limit=self.time_limit,
+                  upper_bound=ub * (1 + 1e-6) + 1e-6 if math.isfinite(ub) else ub, log=self.log,
+                  seed_leaves=self.seed_leaves(layout), integer_bound=self.integer_bound(layout),
+                  improve=self.improve(layout), repair=self.routing_repair(layout),
+                  node_bound_res=self.node_bound_res, unit_flow_leaves=self.unit_flow_leaves,
+                  node_max_iters=max(1, int(self.lp_max_iters * self.node_iters_fraction)),
+                  bound_lp=bmodel, primal=self.primal_heuristic(layout))
+        kw.update(overrides)
+        return BranchAndBound(model, data.workload_matrix, data.function_memory_matrix, data.node_memory_matrix, **kw)
+
     def solve(self):
         self.init_objective()
         data = self.data
@@ -181,18 +199,7 @@ class NeptuneStepBase(Solver):
         bmodel = None
         try:
             bmodel = self.bound_model(data, self.batch + 1)
-            ub = self.upper_bound()
-            bnb = BranchAndBound(model, data.workload_matrix, data.function_memory_matrix, data.node_memory_matrix,
-                                 batch=self.batch, tol=self.lp_tol, max_iters=self.lp_max_iters,
-                                 node_limit=self.node_limit,
-                                 time_limit=self.time_limit,
-                                 upper_bound=ub * (1 + 1e-6) + 1e-6 if math.isfinite(ub) else ub, log=self.log,
-                                 seed_leaves=self.seed_leaves(model.layout()), integer_bound=self.integer_bound(model.layout()),
-                                 improve=self.improve(model.layout()), repair=self.routing_repair(model.layout()),
-                                 node_bound_res=self.node_bound_res, unit_flow_leaves=self.unit_flow_leaves,
-                                 node_max_iters=max(1, int(self.lp_max_iters * self.node_iters_fraction)),
-                                 bound_lp=bmodel, primal=self.primal_heuristic(model.layout()))
-            res = bnb.solve()
+            res = self.branch_and_bound(model, bmodel).solve()
             layout = model.layout()
         finally:
             model.close()

@@ -50,3 +50,24 @@ def test_solver_flow_on_gpu(name):
                 assert set(x[src][fn]) == set(dsts), (src, fn, x[src][fn], dsts)
                 for dst, val in dsts.items():
                     assert abs(x[src][fn][dst] - val) <= 1e-3, (src, fn, dst, x[src][fn][dst], val)
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_solver_step1_search_is_optimal(name):
+    """The step-1 search itself ends OPTIMAL (not LIMIT with a matching score) wherever the reference's
+    recorded step-1 MIP has an optimum — SCIP proves these small instances at once (round-3 VERDICT: testpy's
+    3x2 step 1 ended LIMIT)."""
+    import core.solvers as S
+    from core.utils import data_to_solver_input
+    p = payload(name)
+    data = data_to_solver_input(p, workload_coeff=p.get("workload_coeff", 1), with_db=False)
+    solver = S.SOLVERS[p["solver"]["type"]](**p["solver"].get("args", {}))
+    step1 = getattr(solver, "step1", None)
+    if step1 is None or not hasattr(step1, "branch_and_bound") or G[name]["models"][0]["status"] != 0:
+        pytest.skip("no NEPTUNE step 1 / no recorded step-1 optimum")
+    step1.load_data(data)
+    step1.solve()
+    r = step1.result
+    print(name, r.status, r.objective, r.bound, r.nodes, r.lps, r.as_dict()["lp_status_kind"])
+    assert r.status == "OPTIMAL", (r.status, r.objective, r.bound)
+    assert _close(r.objective, G[name]["models"][0]["mip_objective"])

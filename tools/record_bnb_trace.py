@@ -1,10 +1,11 @@
 #!/usr/bin/env python3
 """Record the node LPs the product branch-and-bound submits (core/engine/bnb.py trace=) on a synthetic
-instance, for bench.py's replay stream (tests/golden/bnb_trace_<N>x<F>_s<seed>.json).  Runs on the GPU box;
+instance, for bench.py's replay stream (tests/golden/bnb_trace_<N>x<F>_s<seed>.json.gz).  Runs on the GPU box;
 the search is the product's (facility-relaxation bounds, reference-model leaves), time-limited.
 
   python3 tools/record_bnb_trace.py 512 256 60 gpurun_out/trace     [seed 0]
 """
+import gzip
 import json
 import os
 import sys
@@ -15,8 +16,7 @@ sys.path[:0] = [os.path.join(REPO, "neptune-mip_amd"), REPO]
 
 
 def main():
-    from core.engine.bnb import BranchAndBound
-    from core.engine.lp import LPModel, RELAX_FACILITY
+    from core.engine.lp import LPModel
     from core.solvers.neptune.neptune_step import NeptuneStep1CPUMinDelayAndUtilization
     from core.utils import data_to_solver_input
     from core.utils.synthetic import synthetic_payload
@@ -24,27 +24,25 @@ def main():
     seed = int(sys.argv[5]) if len(sys.argv) > 5 else 0
     p = synthetic_payload(N, F, seed=seed)
     data = data_to_solver_input(p, with_db=False)
-    st1 = NeptuneStep1CPUMinDelayAndUtilization(alpha=0.5, verbose=False)
+    # the product's step-1 search (NeptuneStepBase.branch_and_bound) at bench.py's defaults: 32 node LPs in
+    # flight per model, tol 1e-6, 4096-iteration leaves (branching nodes a quarter of that)
+    st1 = NeptuneStep1CPUMinDelayAndUtilization(alpha=0.5, verbose=False, batch=32, lp_tol=1e-6, lp_max_iters=4096)
     st1.load_data(data)
-    ub = st1.upper_bound()
     m = LPModel(data, "MinDelayAndUtilization", step=1, alpha=0.5, max_batch=34)
-    bm = LPModel(data, "MinDelayAndUtilization", step=1, alpha=0.5, max_batch=33, relaxation=RELAX_FACILITY)
+    bm = st1.bound_model(data, 33)
     trace = []
     t0 = time.time()
     try:
-        res = BranchAndBound(m, data.workload_matrix, data.function_memory_matrix, data.node_memory_matrix,
-                             batch=32, tol=1e-6, time_limit=secs, root_max_iters=400000,
-                             upper_bound=ub * (1 + 1e-6) + 1e-6, node_max_iters=1024, bound_lp=bm,
-                             trace=trace).solve()
+        res = st1.branch_and_bound(m, bm, time_limit=secs, root_max_iters=400000, trace=trace).solve()
     finally:
         m.close()
         bm.close()
     os.makedirs(out, exist_ok=True)
-    path = os.path.join(out, f"bnb_trace_{N}x{F}_s{seed}.json")
+    path = os.path.join(out, f"bnb_trace_{N}x{F}_s{seed}.json.gz")
     doc = {"nodes": N, "functions": F, "seed": seed, "seconds": time.time() - t0, "status": res.status,
            "incumbent": res.objective, "bound": res.bound, "generator": "tools/record_bnb_trace.py",
            "lps": trace}
-    with open(path, "w") as fh:
+    with gzip.open(path, "wt", compresslevel=9) as fh:
         json.dump(doc, fh, separators=(",", ":"))
     kinds = {}
     for e in trace:
