@@ -45,9 +45,11 @@ enum { NEP_STEP1 = 1, NEP_STEP2_DELETE = 2, NEP_STEP2_CREATE = 3 };
  *                        for branch-and-bound bounds: x[i,f,j] <= c[f,j] for every routing
  *                        row and c[f,j] <= n[j] (valid for every integral placement: constraints_step1.py:5-15,
  *                        :69-78 with c, n binary) replace the big-M pairs C1/C2 and C6/C7, which they imply
- *                        for integral c, n (C2 and C7, the eps floors, are relaxed).  Same variables, z_int and
- *                        objective; C3 memory, C4, C5 CPU and C8 kept.  Its bound is valid for the MIP, not
- *                        equal to the reference LP's */
+ *                        for integral c, n (C2 and C7, the eps floors, are relaxed); the capacity rows take n on
+ *                        their right-hand side, C3 sum_f mem_f c[f,j] <= Mem_j n[j] and C5 CPU_j <= cores_j n[j]
+ *                        (constraints_step1.py:18-23, :57-65: a closed node has neither).  Same variables, z_int
+ *                        and objective; C4 and C8 kept.  Its bound is valid for the MIP, not equal to the
+ *                        reference LP's */
 enum { NEP_RELAX_REFERENCE = 0, NEP_RELAX_FACILITY = 1 };
 
 enum { NEP_OK = 0, NEP_ERR_ARG = -1, NEP_ERR_HIP = -2, NEP_ERR_NOMEM = -3, NEP_ERR_STATE = -4 };

@@ -79,6 +79,7 @@ class BnBResult:
         self.incumbent_slot = None
         self.polished = False    # the incumbent's LP was re-solved at the polish tolerance
         self.repaired = None     # the CPU repair of the returned routing succeeded (None: not run)
+        self.heuristic_incumbents = 0   # incumbents taken from a checked heuristic point (no LP behind them)
         # node-LP mix: finished LPs per engine status (+ presolve-infeasible submits) and their iterations
         self.lp_status = {"certified": 0, "bound": 0, "limit": 0, "infeasible": 0, "cutoff": 0, "numerical": 0,
                           "presolve_infeasible": 0}
@@ -97,7 +98,8 @@ class BnBResult:
     def as_dict(self):
         d = {k: getattr(self, k) for k in ("status", "objective", "bound", "nodes", "leaves", "lps", "certified",
                                            "lp_iterations", "unresolved", "seconds", "polished", "repaired",
-                                           "lp_status", "lp_status_kind", "drained", "timing")}
+                                           "lp_status", "lp_status_kind", "drained", "timing",
+                                           "heuristic_incumbents")}
         d["inflight_mean"] = self.inflight_sum / max(1, self.advance_calls)
         d["resolved"] = sum(v for k, v in self.lp_status.items() if k not in ("limit", "numerical"))
         it = np.asarray(self.lp_iters, np.float64)
@@ -148,7 +150,7 @@ class BranchAndBound:
                  warm=True, root_max_iters=200000, check_every=12, polish_tol=1e-8, polish_iters=20000,
                  seed_leaves=None, integer_bound=None, improve=None, repair=None, node_bound_res=1e-2,
                  retry_res=math.inf, unit_flow_leaves=True, node_max_iters=None, bound_lp=None, bound_gap=1e-4,
-                 trace=None, rebalance_every=8, primal=None, primal_every=0):
+                 trace=None, rebalance_every=8, primal=None, primal_every=0, leaf_warm_incumbent=False):
         self.lp = lp
         self.two = bound_lp is not None
         self.N, self.F = lp.N, lp.F
@@ -169,13 +171,18 @@ class BranchAndBound:
         # sharded search: every rebalance_every loops, ranks with an empty frontier take open nodes from the
         # fullest ones (_rebalance; 0: never)
         self.rebalance_every = rebalance_every
-        # primal(idx, val, z, flow) -> [(idx, val)]: leaves completing a branching node's fixings, built from its
-        # LP (z, flow) with the instance's data (core/engine/heuristics.py); run at the root and, with
+        # primal(idx, val, z, flow) -> [(idx, val[, sol])]: leaves completing a branching node's fixings, built
+        # from its LP (z, flow) with the instance's data (core/engine/heuristics.py); sol, when given, is a
+        # feasible point of that leaf checked by the caller ({"objective", "z", "row", "dst", "val"}: a direct
+        # incumbent before any LP runs on the leaf, whose LP is queued too); run at the root and, with
         # primal_every > 0, on every primal_every-th branched node (0: the root only — with the facility
         # relaxation's bounds the nodes' own rounding leaves find the same incumbents at 256x128 / 512x256, and
         # the greedy costs ~2 s per call at 512x256)
         self.primal = primal
         self.primal_every = max(0, int(primal_every))
+        # leaves (and their retries) warm-start from the incumbent leaf's final state once there is one
+        # (its routing and CPU prices sit next to the new leaf's) instead of the reference root's
+        self.leaf_warm_incumbent = bool(leaf_warm_incumbent)
         self.root_slot = lp.max_batch - 1
         self.inc_slot = lp.max_batch - 2
         self.tol, self.gap, self.max_iters = tol, gap, max_iters
@@ -368,6 +375,9 @@ class BranchAndBound:
             warm, src = False, None
             if self.warm and eng.root_ready:
                 src = eng.root_slot
+                if (self.leaf_warm_incumbent and node.kind in (LEAF, RETRY) and eng is self.L
+                        and self.res.incumbent_slot == eng.inc_slot):
+                    src = eng.inc_slot
                 if node.parent is not None:
                     pe, ps, pg = node.parent[:3]
                     if pe is eng and eng.gen[ps] == pg:
@@ -418,8 +428,9 @@ class BranchAndBound:
                     self.inflight[(eng.name, slot)] = node
                     eng.inflight += 1
 
-    def _finish(self, eng, slot, node, st, obj, pobj, iters, inc):
-        """Process one finished node LP (of engine `eng`); returns the (possibly improved) incumbent value."""
+    def _finish(self, eng, slot, node, st, obj, pobj, iters, inc, flow=None):
+        """Process one finished node LP (of engine `eng`); returns the (possibly improved) incumbent value.
+        flow: its F x N flows when the caller already read them (one device read per block, _prefetch)."""
         res = self.res
         lp = eng.lp
         eng.inflight -= 1
@@ -496,7 +507,8 @@ class BranchAndBound:
             eng.free.append(slot)
             return inc
         res.nodes += 1
-        flow = lp.flows([slot])[0]
+        if flow is None:
+            flow = lp.flows([slot])[0]
         me = (eng, slot, eng.gen[slot], node.nid)
         z, _ = lp.solution(slot, dense_x=False)
         for by_flow, min_flow in self.round_modes:
@@ -510,7 +522,11 @@ class BranchAndBound:
                         self.pending.append(_Node(lb, leaf[0], leaf[1], LEAF, me, node.depth + 1))
         if self.primal is not None and (node.depth == 0 or (self.primal_every and res.nodes % self.primal_every == 0)):
             t = time.time()
-            for idx, val in self.primal(node.idx, node.val, z, flow):
+            for item in self.primal(node.idx, node.val, z, flow):
+                idx, val = item[0], item[1]
+                sol = item[2] if len(item) > 2 else None
+                if sol is not None and sol["objective"] < inc - self._gap_abs(inc):
+                    inc = self._heuristic_incumbent(sol)
                 key = np.packbits(np.asarray(val) > 0.5).tobytes()
                 if key not in self.seen_leaves:
                     self.seen_leaves.add(key)
@@ -532,6 +548,38 @@ class BranchAndBound:
                                            _Node(cb, idx, val, kind, me, node.depth + 1)))
         eng.free.append(slot)        # most recently finished last: its state survives longest
         return inc
+
+    def _heuristic_incumbent(self, sol):
+        """A checked heuristic point as the incumbent: objective, z and routing (engine rows) taken as given,
+        no LP slot behind it (an LP incumbent found later replaces it as usual)."""
+        res = self.res
+        res.objective = float(sol["objective"])
+        res.z = np.asarray(sol["z"], np.float64)
+        res.x = self.lp.routing_from_entries(sol["row"], sol["dst"], sol["val"])
+        res.incumbent_slot = None
+        res.heuristic_incumbents += 1
+        self.inc_node = None
+        for e in self.engines:
+            e.lp.set_params(self.tol, min(res.objective, self.ub0))
+        self.log(f"incumbent {res.objective:.10g} (capacity greedy; lps {res.lps}, nodes {res.nodes})")
+        return res.objective
+
+    def _prefetch(self, eng, r, inc):
+        """The flows of every branching node in an advance result that will branch (not pruned, not
+        infeasible / cut off), read in ONE device call: {slot: flow [F, N]}."""
+        want = []
+        for i, slot in enumerate(r["slots"].tolist()):
+            node = self.inflight.get((eng.name, slot))
+            st = int(r["status"][i])
+            if node is None or node.kind != NODE or st in (LP_INFEASIBLE, LP_CUTOFF):
+                continue
+            if max(node.bound, float(r["obj"][i])) >= inc - self._gap_abs(inc):
+                continue
+            want.append(slot)
+        if not want:
+            return {}
+        fl = eng.lp.flows(want)
+        return {s: fl[k] for k, s in enumerate(want)}
 
     def _frontier_hash(self):
         """crc32 of the (sorted) open frontier: bounds, depths, fixings — identical on every rank at the split."""
@@ -630,7 +678,7 @@ class BranchAndBound:
         certified incumbent (lowest rank on ties, chosen on the certified objectives BEFORE any polish)
         polishes it and broadcasts objective, integer vector and compacted routing entries."""
         comm, lp = self.comm, self.lp
-        mine = res.objective is not None and res.incumbent_slot is not None and res.objective <= inc
+        mine = res.objective is not None and res.objective <= inc
         g = comm.gather([res.bound, 1.0 if limit_hit else 0.0, 1.0 if unresolved_below else 0.0, 1.0 if mine else 0.0,
                          res.nodes - self.presplit[0], res.lps - self.presplit[1], res.certified - self.presplit[2],
                          1.0 if self.unresolved_bounds else 0.0])
@@ -649,9 +697,10 @@ class BranchAndBound:
         owner = int(owners[0])
         own = comm.rank == owner
         if own:
-            res.x = lp.routing(res.incumbent_slot)
-            if self.polish_tol:
-                self._polish(res)
+            if res.incumbent_slot is not None:      # (a heuristic incumbent carries its routing already)
+                res.x = lp.routing(res.incumbent_slot)
+                if self.polish_tol:
+                    self._polish(res)
             head = np.array([res.objective, 1.0 if res.polished else 0.0, float(len(res.x.row))])
         else:
             head = np.zeros(3)
@@ -786,10 +835,11 @@ class BranchAndBound:
                     r = eng.lp.advance((0 if self.time_limit else 1) if sharded else eng.inflight)
                 t3 = time.perf_counter()
                 tm["advance"] += t3 - t2
+                fl = self._prefetch(eng, r, inc)
                 for i, slot in enumerate(r["slots"].tolist()):
                     node = self.inflight.pop((eng.name, slot))
                     inc = self._finish(eng, slot, node, int(r["status"][i]), float(r["obj"][i]),
-                                       float(r["primal_obj"][i]), int(r["iters"][i]), inc)
+                                       float(r["primal_obj"][i]), int(r["iters"][i]), inc, fl.get(slot))
                 t2 = time.perf_counter()
                 tm["finish"] += t2 - t3
         # drain what still iterates (a stop decision): a cutoff of -inf stops every LP in flight at its next

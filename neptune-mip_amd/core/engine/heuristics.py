@@ -14,7 +14,8 @@ import numpy as np
 
 def capacity_greedy(W, D, cpr, cores, fmem, nmem, n_rank, flow=None, start=None, step=None, tries=4,
                     node_cost=0.0, delay_coef=0.0, c_fix=None, n_fix=None, new_pen=0.5):
-    """Leaves [(c [F, N] 0/1, n [N] 0/1, estimate)], best estimate first (at most `tries`, one per node count).
+    """Leaves [(c [F, N] 0/1, n [N] 0/1, estimate, route)], best estimate first (at most `tries`, one per node
+    count); route = (f, i, j) arrays: the loaded source i of f sends all of its workload to j.
 
     W [F, N] workload, D [N, N] delay, cpr [F, N], cores [N], fmem [F], nmem [N]; n_rank [N]: the order in
     which nodes are opened (descending); flow [F, N] (optional): the LP's flows, tie-break among equal delays.
@@ -64,6 +65,7 @@ def capacity_greedy(W, D, cpr, cores, fmem, nmem, n_rank, flow=None, start=None,
             C[f, j] = 1.0
             mem[j] -= fmem[f]
         delay = 0.0
+        rf, ri, rj = [], [], []
         pen = new_pen * float(np.median(D[np.ix_(openj, openj)])) if k > 1 else 0.0
         for r in rows if ok else ():
             f, i = int(fs[r]), int(src[r])
@@ -79,6 +81,9 @@ def capacity_greedy(W, D, cpr, cores, fmem, nmem, n_rank, flow=None, start=None,
             j = int(best[np.argmax(fl[f, best])] if fl is not None and len(best) > 1 else best[0])
             cap[j] -= need[j]
             delay += load[r] * D[i, j]
+            rf.append(f)
+            ri.append(i)
+            rj.append(j)
             if C[f, j] == 0:
                 C[f, j] = 1.0
                 mem[j] -= fmem[f]
@@ -94,7 +99,8 @@ def capacity_greedy(W, D, cpr, cores, fmem, nmem, n_rank, flow=None, start=None,
         if ok:
             n = (C.sum(axis=0) > 0).astype(np.float64)
             n[nfx == 1.0] = 1.0
-            out.append((C, n, node_cost * float(n.sum()) + delay_coef * delay))
+            out.append((C, n, node_cost * float(n.sum()) + delay_coef * delay,
+                        (np.asarray(rf, np.int64), np.asarray(ri, np.int64), np.asarray(rj, np.int64))))
         k += step
     out.sort(key=lambda t: t[2])
     return out

@@ -103,9 +103,11 @@ class NeptuneStepBase(Solver):
         """(cost per open node, coefficient of sum W D of the routing) of the step-1 objective, or None."""
         return None
 
-    def primal_heuristic(self, layout):
-        """primal(idx, val, z, flow) -> [(idx, val)]: capacity-greedy leaves of a branching node (core/engine/
-        heuristics.py), the LP's n ranking the nodes; None where the objective has no node count."""
+    def primal_heuristic(self, layout, row_map=None):
+        """primal(idx, val, z, flow) -> [(idx, val, sol)]: capacity-greedy leaves of a branching node (core/engine/
+        heuristics.py), the LP's n ranking the nodes; None where the objective has no node count.
+        sol (with row_map = the model's (row_f, row_src)): the greedy point itself as an incumbent —
+        {"objective", "z", "row", "dst", "val"} — when it passes check_placement in fp64, else None."""
         wts = self.objective_weights()
         if wts is None or layout.get("n") is None:
             return None
@@ -129,12 +131,82 @@ class NeptuneStepBase(Solver):
             sel = (idx >= n0) & (idx < n1)
             nfix[idx[sel] - n0] = np.asarray(val)[sel]
             out = []
-            for C, n, _ in capacity_greedy(W, D, cpr, cores, fmem, nmem, np.asarray(z[n0:n1], np.float64),
-                                           flow=flow, tries=2, node_cost=wts[0], delay_coef=wts[1],
-                                           c_fix=cfix.reshape(F, N), n_fix=nfix):
-                out.append((np.concatenate([np.arange(c0, c1), np.arange(n0, n1)]), np.concatenate([C.ravel(), n])))
+            for C, n, _, route in capacity_greedy(W, D, cpr, cores, fmem, nmem, np.asarray(z[n0:n1], np.float64),
+                                                  flow=flow, tries=2, node_cost=wts[0], delay_coef=wts[1],
+                                                  c_fix=cfix.reshape(F, N), n_fix=nfix):
+                sol = None if row_map is None else self._greedy_incumbent(C, n, route, row_map, wts, layout)
+                out.append((np.concatenate([np.arange(c0, c1), np.arange(n0, n1)]), np.concatenate([C.ravel(), n]),
+                            sol))
             return out
         return primal
+
+    def _greedy_incumbent(self, C, n, route, row_map, wts, layout):
+        """The greedy's placement and routing as a feasible point of the reference model, in the engine's
+        aggregated rows (every loaded source's row to its node, each pooled zero-workload row to one open
+        placement of its function), with its objective computed from the reference's objective
+        (objectives.py:13-53) — or None when check_placement rejects it."""
+        d = self.data
+        F, N = len(d.functions), len(d.nodes)
+        W = np.asarray(d.workload_matrix, np.float64)
+        D = np.asarray(d.node_delay_matrix, np.float64)
+        rf, rs = (np.asarray(a) for a in row_map)
+        rowid = {(int(f), int(i)): r for r, (f, i) in enumerate(zip(rf.tolist(), rs.tolist()))}
+        f_, i_, j_ = route
+        dst = np.full(len(rf), -1, np.int64)
+        for f, i, j in zip(f_.tolist(), i_.tolist(), j_.tolist()):
+            r = rowid.get((f, i))
+            if r is None:
+                return None
+            dst[r] = j
+        for r in np.flatnonzero(dst < 0):
+            f = int(rf[r])
+            opened = np.flatnonzero(C[f] > 0.5)
+            if opened.size == 0:
+                return None
+            if rs[r] >= 0 and W[f, rs[r]] > 0:
+                return None                      # a loaded source the greedy left unrouted
+            dst[r] = int(opened[0])
+        x_fij = np.zeros((F, N, N))              # x[f, i, j] (the pooled rows expanded over their sources)
+        for r in range(len(rf)):
+            f, i = int(rf[r]), int(rs[r])
+            if i >= 0:
+                x_fij[f, i, dst[r]] = 1.0
+            else:
+                for i0 in np.flatnonzero(W[f] == 0):
+                    x_fij[f, i0, dst[r]] = 1.0
+        if not self.check_placement(C, n, x_fij):
+            return None
+        obj = wts[0] * float(n.sum()) + wts[1] * float(np.einsum("fi,ij,fij->", W, D, x_fij))
+        c0, c1 = layout["c"]
+        n0, n1 = layout["n"]
+        z = np.zeros(max(c1, n1))
+        z[c0:c1] = C.ravel()
+        z[n0:n1] = n
+        return {"objective": obj, "z": z, "row": np.arange(len(rf)), "dst": dst, "val": np.ones(len(rf))}
+
+    def check_placement(self, C, n, x):
+        """Every step-1 row of the reference (constraints_step1.py) at an integral point, in fp64: C1/C2 (flow
+        only into open placements, >= 1 - eps into each), C3 memory, C4 each source routed once, C5 CPU
+        (<= cores + 1e-6, the checker's tolerance), C6/C7 (n = any placement), C8 budget."""
+        d = self.data
+        W = np.asarray(d.workload_matrix, np.float64)
+        cpr = np.asarray(d.core_per_req_matrix, np.float64)
+        col = x.sum(axis=1)                                                       # [f, j]
+        if (col > 1e6 * C + 1e-9).any() or (col < C - 1e-6 - 1e-12).any():
+            return False
+        if ((np.asarray(d.function_memory_matrix, np.float64) @ C) > np.asarray(d.node_memory_matrix, np.float64) + 1e-9).any():
+            return False
+        if np.abs(x.sum(axis=2) - 1.0).max() > 1e-12:
+            return False
+        cpu = np.einsum("fi,fj,fij->j", W, cpr, x)
+        if (cpu > np.asarray(d.node_cores_matrix, np.float64) + 1e-6).any():
+            return False
+        used = C.sum(axis=0)
+        if (used > 1e6 * n + 1e-9).any() or (used < n - 1e-6).any():
+            return False
+        cost = np.asarray(getattr(d, "node_costs", np.zeros(len(n))), np.float64)
+        budget = float(getattr(d, "node_budget", np.inf))
+        return float(cost @ n) <= budget + 1e-9
 
     def improve(self, layout):
         """improve(idx, val, value) -> [(idx, val)]: neighbour placements of a new incumbent leaf
@@ -185,7 +257,7 @@ class NeptuneStepBase(Solver):
                   improve=self.improve(layout), repair=self.routing_repair(layout),
                   node_bound_res=self.node_bound_res, unit_flow_leaves=self.unit_flow_leaves,
                   node_max_iters=max(1, int(self.lp_max_iters * self.node_iters_fraction)),
-                  bound_lp=bmodel, primal=self.primal_heuristic(layout))
+                  bound_lp=bmodel, primal=self.primal_heuristic(layout, _row_map(model)))
         kw.update(overrides)
         return BranchAndBound(model, data.workload_matrix, data.function_memory_matrix, data.node_memory_matrix, **kw)
 
@@ -227,6 +299,12 @@ class NeptuneStepBase(Solver):
         self.data.prev_x = self.x_matrix
         self.data.prev_c = self.c_matrix
         return self.x_matrix, self.c_matrix
+
+
+def _row_map(model):
+    """(row_f, row_src) of a model's routing rows (the engine's aggregated rows), or None."""
+    rm = getattr(model, "row_map", None)
+    return rm() if rm is not None else None
 
 
 def _max_delay_per_source(data):

@@ -92,6 +92,8 @@ struct Model {
   std::vector<double> row_wsc_d;    // the score-row weights in fp64 (presolve's proofs; row_wsc is the kernels' fp32)
   std::vector<RowInfo> rows;
   std::vector<double> W;            // [F*N]
+  std::vector<double> cprh;         // [F*N] core_per_req (the presolve's CPU cover test)
+  std::vector<double> wsum;         // [F] sum_i W[f, i]
   std::vector<double> nat_lb, nat_ub, cost_int;
   std::vector<double> lo, hi, rownorm, rho, gam;
   std::vector<double> mem_f;
@@ -105,6 +107,7 @@ struct Model {
   bool score_x = false;
   std::vector<double> Dh;            // [N*N] delay matrix (step 2 with score_x only)
   std::vector<uint8_t> allow;        // scratch [F*N]
+  std::vector<uint8_t> allow2;       // scratch [F*N] (CPU cover test)
   bool x_cost_free = true;     // no routing entry carries objective cost (step 2; W == 0)
   int32_t *d_exact = nullptr;  // per submitted node: the box fixes the objective (Ctrl::exact)
   // node presolve as a sparse change of the base box (presolve_setup / presolve_node)
@@ -164,11 +167,23 @@ struct Model {
   int pipe_max_done = INT_MAX;
   std::vector<int32_t> launched;
   Ctrl *h_ctrl = nullptr;
+  float *h_flows = nullptr;     // pinned staging of nep_lp_get_flows(_split): [2][max_batch][F*N] + slots
+  // pinned staging of nep_lp_submit's uploads (slots, change offsets / indices / bounds, exact flags): the
+  // call returns without waiting for them; the next submit waits on ev_sub before rewriting the staging
+  int32_t *h_sub_i = nullptr;
+  double *h_sub_d = nullptr;
+  size_t cap_sub_i = 0, cap_sub_d = 0;
+  hipEvent_t ev_sub = nullptr;
+  bool sub_pending = false;
   ~Model() {
     if (stream) (void)hipStreamSynchronize(stream);
     if (aux) (void)hipStreamSynchronize(aux);
     if (h_ctrl) (void)hipHostFree(h_ctrl);
     if (h_act) (void)hipHostFree(h_act);
+    if (h_flows) (void)hipHostFree(h_flows);
+    if (h_sub_i) (void)hipHostFree(h_sub_i);
+    if (h_sub_d) (void)hipHostFree(h_sub_d);
+    if (ev_sub) (void)hipEventDestroy(ev_sub);
     for (void *p : allocs) (void)hipFree(p);
     for (hipGraphExec_t g : block_graph)
       if (g) (void)hipGraphExecDestroy(g);
@@ -234,6 +249,10 @@ int build(Model &m, const nep_model_desc &d) {
   const int chunks = m.NP / 4;
   m.CPL = chunks <= 64 ? 1 : chunks <= 128 ? 2 : chunks <= 256 ? 4 : 8;
   m.W.assign(d.workload, d.workload + (size_t)F * N);
+  m.cprh.assign(d.core_per_req, d.core_per_req + (size_t)F * N);
+  m.wsum.assign(F, 0.0);
+  for (int f = 0; f < F; ++f)
+    for (int i = 0; i < N; ++i) m.wsum[f] += m.W[(size_t)f * N + i];
   const double *D = d.delay;
 
   // exact aggregation of zero-workload sources: they enter only the column sums (C1/C2) and their
@@ -644,7 +663,14 @@ int setup_device(Model &m, int max_batch, void *stream) {
   }
   HIPCHK(hipEventCreate(&m.ev0));
   HIPCHK(hipEventCreate(&m.ev1));
-  HIPCHK(hipStreamCreateWithFlags(&m.aux, hipStreamNonBlocking));
+  // the auxiliary stream (host reads of finished slots, warm-start copies, submits) at the highest priority:
+  // its small kernels and copies are dispatched between the workgroups of the block in flight instead of
+  // queueing behind it (round-4 B&B profile: a flows read waited ~0.5 ms for a 64x32 block)
+  {
+    int least = 0, greatest = 0;
+    if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) greatest = 0;
+    HIPCHK(hipStreamCreateWithPriority(&m.aux, hipStreamNonBlocking, greatest));
+  }
   HIPCHK(hipEventCreateWithFlags(&m.ev_aux, hipEventDisableTiming));
   DeviceView &v = m.v;
   v.N = m.N; v.NP = m.NP; v.F = m.F; v.R = m.R; v.JB = m.JB; v.CPL = m.CPL;
@@ -838,6 +864,44 @@ static double score_row_xmin(const Model &m, const uint8_t *allow, int ld) {
   return xmin;
 }
 
+// CPU cover test over a box's allowed placements allow[f * ld + j] (c[f, j] not fixed to 0): every routing
+// row of f sends its whole workload W[f, i] to allowed destinations (C4, constraints_step1.py:27-34), each
+// unit costing cpr[f, j] cores at j (C5, :57-65), so (a) sum_f wsum_f min_{j allowed} cpr[f, j] cannot exceed
+// the cores of the nodes any loaded function may use, and (b) a function with ONE allowed destination puts
+// all of wsum_f cpr[f, j] on that node.  Either failing proves the box infeasible — e.g. a rounding leaf
+// that opens too few nodes, whose LP PDHG can only stall on (a residual stuck at the overload).  Only for
+// non-negative CPU coefficients (the generator's and the reference's inputs).
+static bool cpu_cover_ok(const Model &m, const uint8_t *allow, int ld) {
+  if (!m.x_coef_nonneg) return true;
+  const int N = m.N, F = m.F;
+  std::vector<uint8_t> usable(N, 0);
+  std::vector<double> forced(N, 0.0);
+  double demand = 0.0;
+  for (int f = 0; f < F; ++f) {
+    if (m.wsum[f] <= 0.0) continue;
+    const uint8_t *al = allow + (size_t)f * ld;
+    double mc = INF;
+    int cnt = 0, only = -1;
+    for (int j = 0; j < N; ++j)
+      if (al[j]) {
+        mc = std::min(mc, m.cprh[(size_t)f * N + j]);
+        usable[j] = 1;
+        ++cnt;
+        only = j;
+      }
+    if (cnt == 0) return false;
+    demand += m.wsum[f] * mc;
+    if (cnt == 1) forced[only] += m.wsum[f] * m.cprh[(size_t)f * N + only];
+  }
+  double cap = 0.0;
+  for (int j = 0; j < N; ++j) {
+    const double cores = m.capn[N + j];
+    if (forced[j] > cores + 1e-6 * std::max(1.0, cores)) return false;
+    if (usable[j]) cap += cores;
+  }
+  return demand <= cap + 1e-6 * std::max(1.0, cap);
+}
+
 bool presolve_full(const Model &m, const double *lbi, const double *ubi, std::vector<double> &lb,
                    std::vector<double> &ub, std::vector<uint8_t> &mask) {
   const int n = m.il.n_int, N = m.N, F = m.F, NP = m.NP;
@@ -870,7 +934,7 @@ bool presolve_full(const Model &m, const double *lbi, const double *ubi, std::ve
   if (m.score_x) amin[m.dl.oS] += score_row_xmin(m, mask.data(), NP);   // (see presolve_node)
   for (int k = 0; k < m.dl.n_dual; ++k)
     if (!row_range_ok(m, k, amin[k], amax[k])) return false;
-  return true;
+  return cpu_cover_ok(m, mask.data(), NP);
 }
 
 // once per model: the base box (natural bounds) and what presolve_node() needs
@@ -968,6 +1032,18 @@ bool presolve_node(Model &m, const double *lbi, const double *ubi, std::vector<i
       m.dmin[r] += std::min(a * l, a * u) - std::min(a * bl, a * bu);
       m.dmax[r] += std::max(a * l, a * u) - std::max(a * bl, a * bu);
     }
+  }
+  if (ok && !ftouched.empty()) {
+    // the CPU cover test (cpu_cover_ok) over the node's allowed placements; a box that closes no placement
+    // has the base box's (tested in presolve_full)
+    m.allow2.assign((size_t)F * N, 0);
+    for (int f = 0; f < F; ++f)
+      for (int j = 0; j < N; ++j) m.allow2[(size_t)f * N + j] = m.base_mask[(size_t)f * NP + j];
+    for (size_t t = c0; t < ci.size(); ++t) {
+      const int k = ci[t];
+      if (k >= oc && k < oc + F * N) m.allow2[k - oc] = cu[t] > 0.0;
+    }
+    ok = cpu_cover_ok(m, m.allow2.data(), N);
   }
   if (ok && m.score_x) {
     // The score / delay row (constraints_step2.py:57-88) over x: every routing row carries mass 1 on its
@@ -1088,17 +1164,46 @@ int submit(Model &m, int n, const int32_t *slots, const double *lbi, const doubl
   }
   const int nf = (int)fresh.size();
   // the node boxes on the device: base box copy + the packed changes scattered over it (a few
-  // KB per node instead of the 2 x 8 x n_int bytes of bounds and the F x NP mask)
-  HIPCHK(hipMemcpyAsync(m.d_new, fresh.data(), nf * sizeof(int32_t), hipMemcpyHostToDevice, m.aux));
-  HIPCHK(hipMemcpyAsync(m.d_chg_off, off.data(), off.size() * sizeof(int32_t), hipMemcpyHostToDevice, m.aux));
+  // KB per node instead of the 2 x 8 x n_int bytes of bounds and the F x NP mask), staged through pinned
+  // host memory so the call need not wait for the copies (nor for the initialisation kernels behind them)
+  const size_t need_i = 2 * (size_t)nf + off.size() + ci.size(), need_d = cl.size() + cu.size();
+  if (m.sub_pending) HIPCHK(hipEventSynchronize(m.ev_sub));   // the previous submit's copies have read the staging
+  m.sub_pending = false;
+  if (need_i > m.cap_sub_i) {
+    if (m.h_sub_i) HIPCHK(hipHostFree(m.h_sub_i));
+    m.h_sub_i = nullptr;
+    m.cap_sub_i = std::max(need_i, 2 * m.cap_sub_i);
+    void *h = nullptr;
+    if (hipHostMalloc(&h, m.cap_sub_i * sizeof(int32_t)) != hipSuccess) return fail(NEP_ERR_NOMEM, "hipHostMalloc (submit)");
+    m.h_sub_i = static_cast<int32_t *>(h);
+  }
+  if (need_d > m.cap_sub_d) {
+    if (m.h_sub_d) HIPCHK(hipHostFree(m.h_sub_d));
+    m.h_sub_d = nullptr;
+    m.cap_sub_d = std::max(need_d, 2 * m.cap_sub_d);
+    void *h = nullptr;
+    if (hipHostMalloc(&h, m.cap_sub_d * sizeof(double)) != hipSuccess) return fail(NEP_ERR_NOMEM, "hipHostMalloc (submit)");
+    m.h_sub_d = static_cast<double *>(h);
+  }
+  if (!m.ev_sub) HIPCHK(hipEventCreateWithFlags(&m.ev_sub, hipEventDisableTiming));
+  int32_t *hf = m.h_sub_i, *ho = hf + nf, *hc = ho + off.size(), *he = hc + ci.size();
+  double *hl = m.h_sub_d, *hu = hl + cl.size();
+  std::copy(fresh.begin(), fresh.end(), hf);
+  std::copy(off.begin(), off.end(), ho);
+  std::copy(ci.begin(), ci.end(), hc);
+  std::copy(exact.begin(), exact.end(), he);
+  std::copy(cl.begin(), cl.end(), hl);
+  std::copy(cu.begin(), cu.end(), hu);
+  HIPCHK(hipMemcpyAsync(m.d_new, hf, nf * sizeof(int32_t), hipMemcpyHostToDevice, m.aux));
+  HIPCHK(hipMemcpyAsync(m.d_chg_off, ho, off.size() * sizeof(int32_t), hipMemcpyHostToDevice, m.aux));
   if (!ci.empty()) {
-    HIPCHK(hipMemcpyAsync(m.d_chg_idx, ci.data(), ci.size() * sizeof(int32_t), hipMemcpyHostToDevice, m.aux));
-    HIPCHK(hipMemcpyAsync(m.d_chg_lb, cl.data(), cl.size() * sizeof(double), hipMemcpyHostToDevice, m.aux));
-    HIPCHK(hipMemcpyAsync(m.d_chg_ub, cu.data(), cu.size() * sizeof(double), hipMemcpyHostToDevice, m.aux));
+    HIPCHK(hipMemcpyAsync(m.d_chg_idx, hc, ci.size() * sizeof(int32_t), hipMemcpyHostToDevice, m.aux));
+    HIPCHK(hipMemcpyAsync(m.d_chg_lb, hl, cl.size() * sizeof(double), hipMemcpyHostToDevice, m.aux));
+    HIPCHK(hipMemcpyAsync(m.d_chg_ub, hu, cu.size() * sizeof(double), hipMemcpyHostToDevice, m.aux));
   }
   HIPCHK(launch_node_bounds(v, m.d_new, nf, m.d_base_lb, m.d_base_ub, m.d_base_mask, m.d_chg_off, m.d_chg_idx,
                             m.d_chg_lb, m.d_chg_ub, max_chg, m.aux));
-  HIPCHK(hipMemcpyAsync(m.d_exact, exact.data(), nf * sizeof(int32_t), hipMemcpyHostToDevice, m.aux));
+  HIPCHK(hipMemcpyAsync(m.d_exact, he, nf * sizeof(int32_t), hipMemcpyHostToDevice, m.aux));
   HIPCHK(launch_init_slot(v, m.d_new, m.d_exact, nf, o.warm_start != 0, m.eta, m.omega0, m.aux));
   HIPCHK(launch_x_pass(v, m.d_new, nf, false, true, true, true, 0, m.aux));
   HIPCHK(launch_node_pass(v, m.d_new, nf, false, true, true, true, 0, m.aux));
@@ -1107,7 +1212,8 @@ int submit(Model &m, int n, const int32_t *slots, const double *lbi, const doubl
   HIPCHK(hipEventRecord(m.ev_aux, m.aux));
   HIPCHK(hipStreamWaitEvent(m.stream, m.ev_aux, 0));
   m.act.insert(m.act.end(), fresh.begin(), fresh.end());   // (d_slots follows at the next launch_block)
-  HIPCHK(hipStreamSynchronize(m.aux));   // (the uploads above read host vectors that end with this call)
+  HIPCHK(hipEventRecord(m.ev_sub, m.aux));
+  m.sub_pending = true;
   return NEP_OK;
 }
 
@@ -1364,13 +1470,24 @@ int flows(Model &m, int n, const int32_t *slots, float *out, float *wout = nullp
   int rc;
   const size_t plane = (size_t)m.max_batch * m.F * m.N;
   if (!m.d_flows && (rc = dalloc(m, &m.d_flows, 2 * plane))) return rc;
-  HIPCHK(hipMemcpyAsync(m.d_new, slots, n * sizeof(int32_t), hipMemcpyHostToDevice, m.aux));
+  // pinned staging both ways: pageable copies cost ~0.3 ms per call while a block iterates (round-4 B&B
+  // profile, tools/bnb_profile.py: 2.5 of 10 s at 64x32)
+  if (!m.h_flows) {
+    void *h = nullptr;
+    if (hipHostMalloc(&h, sizeof(float) * 2 * plane + sizeof(int32_t) * m.max_batch) != hipSuccess)
+      return fail(NEP_ERR_NOMEM, "hipHostMalloc (flows)");
+    m.h_flows = static_cast<float *>(h);
+  }
+  int32_t *hs = reinterpret_cast<int32_t *>(m.h_flows + 2 * plane);
+  std::memcpy(hs, slots, n * sizeof(int32_t));
+  const size_t cnt = (size_t)n * m.F * m.N;
+  HIPCHK(hipMemcpyAsync(m.d_new, hs, n * sizeof(int32_t), hipMemcpyHostToDevice, m.aux));
   HIPCHK(launch_node_flows(m.v, m.d_new, n, m.d_flows, wout ? m.d_flows + plane : nullptr, m.aux));
-  HIPCHK(hipMemcpyAsync(out, m.d_flows, (size_t)n * m.F * m.N * sizeof(float), hipMemcpyDeviceToHost, m.aux));
-  if (wout)
-    HIPCHK(hipMemcpyAsync(wout, m.d_flows + plane, (size_t)n * m.F * m.N * sizeof(float), hipMemcpyDeviceToHost,
-                          m.aux));
+  HIPCHK(hipMemcpyAsync(m.h_flows, m.d_flows, cnt * sizeof(float), hipMemcpyDeviceToHost, m.aux));
+  if (wout) HIPCHK(hipMemcpyAsync(m.h_flows + plane, m.d_flows + plane, cnt * sizeof(float), hipMemcpyDeviceToHost, m.aux));
   HIPCHK(hipStreamSynchronize(m.aux));
+  std::memcpy(out, m.h_flows, cnt * sizeof(float));
+  if (wout) std::memcpy(wout, m.h_flows + plane, cnt * sizeof(float));
   return NEP_OK;
 }
 
@@ -1553,7 +1670,8 @@ int nep_lp_copy_state(void *model, int32_t src, int32_t dst) {
     HIPCHK(hipMemcpyAsync(v.lsum + dst * v.slsum, v.lsum + src * v.slsum, v.slsum * sizeof(float),
                           hipMemcpyDeviceToDevice, m.aux));
   }
-  HIPCHK(hipStreamSynchronize(m.aux));
+  // no host wait: every later use of src / dst is ordered behind these copies — host reads and submits run
+  // on `aux`, and a slot iterates on `stream` only after its submit's initialisation (ev_aux)
   return NEP_OK;
 }
 

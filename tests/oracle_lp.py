@@ -143,6 +143,10 @@ class OracleLP:
         from core.engine.routing import SparseRouting
         return SparseRouting.from_dense(self.solution(slot, dense_x=True)[1])
 
+    def row_map(self):
+        """(row_f, row_src): one literal routing row per (f, i)"""
+        return np.repeat(np.arange(self.F), self.N).astype(np.int32), np.tile(np.arange(self.N), self.F).astype(np.int32)
+
     def routing_from_entries(self, row, dst, val):
         from core.engine.routing import SparseRouting
         N, F = self.N, self.F

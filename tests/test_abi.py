@@ -142,3 +142,39 @@ def test_facility_relaxation_build():
     for variant, step in (("MinDelay", 1), ("MinDelayAndUtilization", STEP2_CREATE)):
         with pytest.raises(EngineUnavailable):
             debug_build(data, variant, step=step, relaxation=RELAX_FACILITY, max_score=1.0)
+
+
+def test_presolve_cpu_cover_proves_overloaded_leaf_infeasible():
+    """The node presolve's CPU cover test (nep_host.cpp cpu_cover_ok): testpy's step-1 rounding leaf that opens
+    node 0 only (c[0,0] = c[1,0] = n[0] = 1, everything else 0) overloads node 0's CPU — HiGHS finds the box
+    infeasible (tools/leaf_limit_probe.py) and PDHG could only stall on it (round-4 GPU suite: testpy's step 1
+    ended LIMIT).  Both the from-scratch and the sparse-change presolve must reject it, and the leaf that
+    also opens node 1 must pass."""
+    import numpy as np
+    from golden_util import payload
+    from core.engine.lp import debug_presolve
+    from core.utils import data_to_solver_input
+    from oracle.formulation import build_model
+    from oracle.inputs import data_to_solver_input as oracle_input
+    from oracle.solve import solve
+    p = payload("testpy")
+    data = data_to_solver_input(p, workload_coeff=p.get("workload_coeff", 1), with_db=False)
+    N, F = len(data.nodes), len(data.functions)
+    variant = {"NeptuneMinDelayAndUtilization": "MinDelayAndUtilization", "NeptuneMinUtilization": "MinUtilization",
+               "NeptuneMinDelay": "MinDelay"}[p["solver"]["type"]]
+    alpha = p["solver"].get("args", {}).get("alpha", 0.5)
+    n_int = F * N + N
+    lb = np.zeros((2, n_int))
+    ub = np.zeros((2, n_int))
+    for b, opened in enumerate(([0, 3, 6], [0, 3, 4, 6, 7])):
+        lb[b, opened] = ub[b, opened] = 1.0
+    ok_full, ok_node, _, _ = debug_presolve(data, variant, lb, ub, step=1, alpha=alpha)
+    ref = build_model(oracle_input(p, workload_coeff=p.get("workload_coeff", 1), with_db=False), variant, step=1,
+                      alpha=alpha)
+    nx = N * N * F
+    for b in range(2):
+        rl, ru = ref["lb"].copy(), ref["ub"].copy()
+        rl[nx:], ru[nx:] = lb[b], ub[b]
+        st, _, _ = solve(ref, relax=True, lb=rl, ub=ru)
+        assert bool(ok_full[b]) == bool(ok_node[b]) == (st == 0), (b, ok_full[b], ok_node[b], st)
+    assert not ok_full[0]

@@ -146,15 +146,59 @@ def test_bnb_primal_heuristic_keeps_optimum(name, k):
     step1.load_data(data)
     lp = StreamingOracleLP(data, variant, step=1, max_batch=10, alpha=alpha)
     blp = StreamingOracleLP(data, variant, step=1, max_batch=9, alpha=alpha, relaxation=1)
-    primal = step1.primal_heuristic(lp.layout())
+    primal = step1.primal_heuristic(lp.layout(), lp.row_map())
     assert primal is not None
-    calls = []
+    calls, sols = [], []
+
+    def hook(*a):
+        out = primal(*a)
+        calls.append(1)
+        sols.extend(item[2] for item in out if item[2] is not None)
+        return out
     res = BranchAndBound(lp, data.workload_matrix, data.function_memory_matrix, data.node_memory_matrix,
-                         batch=8, node_limit=20000, bound_lp=blp, primal_every=4,
-                         primal=lambda *a: calls.append(1) or primal(*a)).solve()
+                         batch=8, node_limit=20000, bound_lp=blp, primal_every=4, primal=hook).solve()
     assert calls
+    for sol in sols:   # every checked greedy point is feasible: its objective is >= the MIP optimum
+        assert sol["objective"] >= rec["mip_objective"] - 1e-6 * max(1.0, abs(rec["mip_objective"]))
     if rec["status"] == 0:
         assert res.status == OPTIMAL, res.as_dict()
         assert _close(res.objective, rec["mip_objective"]), (res.objective, rec["mip_objective"])
     else:
         assert res.status == INFEASIBLE, res.as_dict()
+
+
+@pytest.mark.parametrize("name,k", STEP1_N[:8])
+def test_heuristic_incumbent_is_feasible_reference_point(name, k):
+    """A checked capacity-greedy point taken as the incumbent (BranchAndBound._heuristic_incumbent) before any
+    leaf LP: stopped right after the root (node_limit=1), the search returns it — and its (z, routing) is a
+    feasible point of the reference formulation (oracle/formulation.py rows, fp64) whose objective is the
+    returned one."""
+    from core.engine.bnb import BranchAndBound
+    from core.solvers import SOLVERS
+    from oracle.formulation import build_model
+    from oracle.inputs import data_to_solver_input as oracle_input
+    from oracle_lp import StreamingOracleLP
+    p, data = _data(name)
+    variant = VARIANT[p["solver"]["type"]]
+    alpha = p["solver"].get("args", {}).get("alpha", 0.5)
+    solver = SOLVERS[p["solver"]["type"]](**p["solver"].get("args", {}))
+    step1 = solver.step1 if hasattr(solver, "step1") else solver
+    step1.load_data(data)
+    lp = StreamingOracleLP(data, variant, step=1, max_batch=10, alpha=alpha)
+    blp = StreamingOracleLP(data, variant, step=1, max_batch=9, alpha=alpha, relaxation=1)
+    res = BranchAndBound(lp, data.workload_matrix, data.function_memory_matrix, data.node_memory_matrix,
+                         batch=8, node_limit=1, bound_lp=blp, polish_tol=0,
+                         primal=step1.primal_heuristic(lp.layout(), lp.row_map())).solve()
+    if not res.heuristic_incumbents:
+        pytest.skip("the greedy found no checked point at the root of this instance")
+    N, F = len(data.nodes), len(data.functions)
+    m = build_model(oracle_input(p, workload_coeff=p.get("workload_coeff", 1), with_db=False), variant, step=1,
+                    alpha=alpha)
+    x = np.zeros((F, N, N))
+    i, f, j, v = res.x.entries()
+    x[f, i, j] = v
+    full = np.concatenate([x.ravel(), np.asarray(res.z, np.float64)])
+    act = m["A"] @ full
+    assert (act <= m["hi"] + 1e-6).all() and (act >= m["lo"] - 1e-6).all()
+    assert (full >= m["lb"] - 1e-12).all() and (full <= m["ub"] + 1e-12).all()
+    assert abs(float(m["c"] @ full) - res.objective) <= 1e-9 * max(1.0, abs(res.objective))

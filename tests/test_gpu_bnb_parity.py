@@ -1,6 +1,7 @@
 """HiGHS parity on the node LPs an actual branch-and-bound visits (not random fixings): the product B&B
 (core/engine/bnb.py) runs on the 64x32 synthetic instance (BASELINE config 2, step-1
-MinDelayAndUtilization) for a few seconds; deep node boxes it finished are re-solved by HiGHS on the
+MinDelayAndUtilization) for a few seconds, every node on the reference model (no bound_lp: the reference LP
+at branching nodes too, the LP SCIP solves there); deep node boxes it finished are re-solved by HiGHS on the
 reference formulation (oracle/):
   * certified LPs (NEP_LP_OPTIMAL; mostly rounding leaves, every c and n fixed) equal HiGHS within 1e-6;
   * bound-converged branching nodes (NEP_LP_BOUND) hold a valid bound (<= HiGHS + 1e-6) — printed with
@@ -31,10 +32,10 @@ def test_bnb_node_lps_match_highs():
     rec = {LP_OPTIMAL: [], LP_BOUND: [], LP_INFEASIBLE: []}
 
     class Recording(B.BranchAndBound):
-        def _finish(self, slot, node, st, obj, pobj, iters, inc):
+        def _finish(self, eng, slot, node, st, obj, pobj, iters, inc, *rest):
             if st in rec:
                 rec[st].append((node.idx.copy(), node.val.copy(), obj))
-            return super()._finish(slot, node, st, obj, pobj, iters, inc)
+            return super()._finish(eng, slot, node, st, obj, pobj, iters, inc, *rest)
 
     try:
         Recording(m, data.workload_matrix, data.function_memory_matrix, data.node_memory_matrix, batch=32, tol=5e-7,
