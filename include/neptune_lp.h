@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define NEP_API_VERSION 7
+#define NEP_API_VERSION 8
 
 /* variants: neptune.py:41-66 (NeptuneMinDelay / MinUtilization / MinDelayAndUtilization) */
 enum { NEP_MIN_DELAY = 0, NEP_MIN_UTILIZATION = 1, NEP_MIN_DELAY_AND_UTILIZATION = 2 };
@@ -225,6 +225,19 @@ int nep_debug_build(const nep_model_desc *desc, double *eta, double *rho, double
 int nep_debug_presolve(const nep_model_desc *desc, int32_t n, const double *lb_int, const double *ub_int,
                        int32_t *ok_full, int32_t *ok_node, double *box_full, double *box_node);
 void nep_reset_stats(void *model);
+
+/* Branch-and-bound rounding heuristic (host only, no model; core/engine/bnb.py): one branching
+ * node's LP -> a leaf fixing every c (and n).  c_fix [F*N] / n_fix [N] (n_fix NULL: no n): -1 free, 0 / 1
+ * fixed by the node; flow [F*N] the node's flows, zc [F*N] its c (NULL: 0).  Fixed-open c first, then the free
+ * c with zc >= 1/2 (largest first), then (by_flow) the free (f, j) with flow > flow_threshold (largest
+ * first), each while node j's memory has room (constraints_step1.py:18-23); a function left without a
+ * destination gets the one with the largest c, then flow; n = any c; a node fixed open gets its smallest
+ * fitting function.  Returns 1 and fills c_out [F*N] (n_out [N]) with the leaf, 0 when the node has none,
+ * < 0 on a bad argument.  Replaces the reference's nothing: SCIP's own primal heuristics run inside
+ * Solve() (core/solvers/solver.py:37). */
+int nep_round_leaf(int32_t F, int32_t N, const double *c_fix, const double *n_fix, const float *flow, const double *zc,
+                   const double *fn_mem, const double *node_mem, int32_t by_flow, double flow_threshold, double *c_out,
+                   double *n_out);
 
 const char *nep_last_error(void);
 int nep_api_version(void);

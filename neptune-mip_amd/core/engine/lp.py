@@ -18,7 +18,7 @@ STEP1, STEP2_DELETE, STEP2_CREATE = 1, 2, 3
 LP_OPTIMAL, LP_ITERATION_LIMIT, LP_INFEASIBLE, LP_CUTOFF, LP_NUMERICAL, LP_BOUND = 0, 1, 2, 3, 4, 5
 VARIANTS = {"MinDelay": MIN_DELAY, "MinUtilization": MIN_UTILIZATION,
             "MinDelayAndUtilization": MIN_DELAY_AND_UTILIZATION}
-API_VERSION = 7
+API_VERSION = 8
 RELAX_REFERENCE, RELAX_FACILITY = 0, 1
 
 _dp = ctypes.POINTER(ctypes.c_double)
@@ -65,7 +65,7 @@ EXPORTS = ("nep_model_create", "nep_model_destroy", "nep_model_get_info", "nep_l
            "nep_lp_get_flows_split",
            "nep_last_error", "nep_api_version", "nep_lp_get_diag", "nep_debug_build", "nep_debug_state",
            "nep_debug_presolve", "nep_lp_set_params", "nep_lp_get_flows", "nep_lp_routing_entries",
-           "nep_lp_allocation_entries", "nep_lp_score_check")
+           "nep_lp_allocation_entries", "nep_lp_score_check", "nep_round_leaf")
 SCORE_FIELDS = ("network_delay", "nodes_used", "node_cost", "bad_c_x", "bad_memory", "bad_handle", "bad_cpu",
                 "bad_n_c", "bad_budget", "handle_maxdev", "cpu_maxexcess")
 
@@ -109,6 +109,8 @@ def load_library(path=None):
     lib.nep_lp_routing_entries.argtypes = [vp, i32, ctypes.c_double, i32, i64, pi64, pi32, pi32, _dp]
     lib.nep_lp_allocation_entries.argtypes = [vp, i32, ctypes.c_double, i64, pi64, pi32, pi32]
     lib.nep_lp_score_check.argtypes = [vp, i32, _dp]
+    lib.nep_round_leaf.argtypes = [i32, i32, _dp, _dp, ctypes.POINTER(ctypes.c_float), _dp, _dp, _dp, i32,
+                                   ctypes.c_double, _dp, _dp]
     lib.nep_last_error.restype = ctypes.c_char_p
     lib.nep_api_version.restype = ctypes.c_int
     if lib.nep_api_version() != API_VERSION:
@@ -116,6 +118,27 @@ def load_library(path=None):
     if path is None:
         _lib = lib
     return lib
+
+
+def round_leaf(c_fix, n_fix, flow, zc, fn_mem, node_mem, by_flow, flow_threshold):
+    """The B&B rounding heuristic (nep_round_leaf, host code of the engine library): c_fix [F, N] / n_fix [N]
+    (None: no n) with -1 free and 0 / 1 fixed, flow [F, N], zc [F, N] (None: 0).  Returns (c [F*N], n [N] or
+    None) or None when the node has no leaf."""
+    lib = load_library()
+    c_fix = np.ascontiguousarray(c_fix, np.float64)
+    F, N = c_fix.shape
+    nf = None if n_fix is None else np.ascontiguousarray(n_fix, np.float64)
+    fl = np.ascontiguousarray(flow, np.float32)
+    zcv = None if zc is None else np.ascontiguousarray(zc, np.float64)
+    fm = np.ascontiguousarray(fn_mem, np.float64)
+    nm = np.ascontiguousarray(node_mem, np.float64)
+    c_out = np.zeros(F * N)
+    n_out = None if nf is None else np.zeros(N)
+    rc = lib.nep_round_leaf(F, N, _ptr(c_fix), _ptr(nf), _ptr(fl, ctypes.c_float), _ptr(zcv), _ptr(fm), _ptr(nm),
+                            1 if by_flow else 0, float(flow_threshold), _ptr(c_out), _ptr(n_out))
+    if rc < 0:
+        raise EngineUnavailable(f"nep_round_leaf failed ({rc})")
+    return (c_out, n_out) if rc == 1 else None
 
 
 def _ptr(a, ctype=ctypes.c_double):

@@ -84,6 +84,66 @@ __device__ __forceinline__ void pooled_shift(const DeviceView &v, int slot, int 
   }
 }
 
+// The certificate's loaded-row shift (one wave, after pooled_shift; DESIGN.md §4 "Pooled shift"): a deficit
+// the pooled row could not serve — a function whose sources all carry workload, e.g. a placement forced
+// open by moved_to = 0 on an old placement (payload.json's step 2) — is taken from the function's loaded
+// rows at donor destinations with slack (S + eps above their own c), up to kShiftMax, written into the
+// stored iterate (so the routing read back is the point the certificate checks).  Unlike pooled flow this
+// moves CPU load (W[f, i] cpr per unit) and delay cost: the W-weighted column sums Wd and the objective /
+// score partials take the exact fp32 changes of the two entries.  Deterministic (rows, donors in order).
+__device__ __forceinline__ void loaded_shift(const DeviceView &v, int slot, int f, int r0, int nrows, float *x,
+                                             double *S, double *Wd, double &dpobj, double &dscore, int lane) {
+  const int N = v.N, NP = v.NP;
+  const double *zi = v.zi + slot * v.sint, *lb = v.lb + slot * v.sint, *ub = v.ub + slot * v.sint;
+  const int oc = v.il.oc + f * N;
+  auto target = [&](int j) { return fmin(fmax(zi[oc + j], lb[oc + j]), ub[oc + j]); };
+  for (int j0 = 0; j0 < N; j0 += kWave) {
+    const int j = j0 + lane;
+    const double need = j < N ? target(j) - v.eps - S[j] : 0.0;
+    uint64_t mask = __ballot(need > 0.0 && need <= kShiftMax);
+    while (mask) {
+      const int k = __builtin_ctzll(mask);
+      mask &= mask - 1;
+      const int jd = j0 + k;
+      double want = target(jd) - v.eps - S[jd];
+      for (int rr = 0; rr < nrows && want > 0.0; ++rr) {
+        const int r = r0 + rr;
+        const RowInfo ri = v.rows[r];
+        if (ri.src < 0) continue;
+        float *xr = x + (int64_t)r * NP;
+        const double m = ri.m;
+        for (int d0 = 0; d0 < N && want > 0.0; d0 += kWave) {
+          const int d = d0 + lane;
+          const double av = (d < N && d != jd) ? fmin(m * (double)xr[d], S[d] + v.eps - target(d)) : 0.0;
+          uint64_t dm = __ballot(av > 0.0);
+          while (dm && want > 0.0) {
+            const int kd = __builtin_ctzll(dm);
+            dm &= dm - 1;
+            const int dj = d0 + kd;
+            const double t = fmin(want, __shfl(av, kd, kWave));
+            if (lane == 0) {
+              const float oj = xr[jd], od = xr[dj];
+              const float nj = (float)((double)oj + t / m), nd = fmaxf((float)((double)od - t / m), 0.f);
+              const double tj = (double)nj - oj, td = (double)od - nd;   // the exact fp32 changes
+              xr[jd] = nj;
+              xr[dj] = nd;
+              S[jd] += m * tj;
+              S[dj] -= m * td;
+              Wd[jd] += (double)ri.w * tj;
+              Wd[dj] -= (double)ri.w * td;
+              const double dj_ = v.D[(int64_t)ri.src * NP + jd], dd_ = v.D[(int64_t)ri.src * NP + dj];
+              dpobj += (double)ri.wobj * (dj_ * tj - dd_ * td);
+              dscore += (double)ri.wsc * (dj_ * tj - dd_ * td);
+            }
+            want -= t;
+          }
+          __builtin_amdgcn_wave_barrier();
+        }
+      }
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------------------------
 // x_pass: one workgroup = all routing rows of ONE function f of one LP slot, then the
 // per-(f, j) small variables of that f.
@@ -500,6 +560,13 @@ void x_pass(DeviceView v, const int32_t *__restrict__ slots, int plain, int it, 
     __syncthreads();
     if (wave == 0) {
       pooled_shift(v, slot, f, lSd, lPm, lane);
+      // (the pooled row's own write-back below rewrites only its row; the loaded rows are written in place)
+      double dpo = 0.0, dsc = 0.0;
+      loaded_shift(v, slot, f, r0, nrows, x, lSd, lWd, dpo, dsc, lane);
+      if (lane == 0) {
+        s_pobj += dpo;
+        s_score += dsc;
+      }
       // the certificate's point is the STORED iterate (this plain iteration's x̂): the pooled row takes
       // the shifted flows, so the routing a caller reads back (nep_lp_get_rows / routing entries) is
       // the point the certificate checked, not one kShiftMax short of it on a column.  Unshifted

@@ -32,7 +32,7 @@ def run(N, F, secs, two, knobs):
                              batch=32, tol=1e-6, time_limit=secs, root_max_iters=400000,
                              upper_bound=ub * (1 + 1e-6) + 1e-6, repair=st1.routing_repair(m.layout()),
                              node_max_iters=1024, bound_lp=bm, log=lambda s: print("   ", s, flush=True),
-                             primal=st1.primal_heuristic(m.layout()) if os.environ.get("PRIMAL", "1") == "1" else None,
+                             primal=st1.primal_heuristic(m.layout(), m.row_map()) if os.environ.get("PRIMAL", "1") == "1" else None,
                              **knobs).solve()
     finally:
         m.close()
