@@ -911,6 +911,12 @@ bool presolve_full(const Model &m, const double *lbi, const double *ubi, std::ve
     for (int k = 0; k < n; ++k) lb[k] = std::max(lb[k], lbi[k]);
   if (ubi)
     for (int k = 0; k < n; ++k) ub[k] = std::min(ub[k], ubi[k]);
+  if (m.step2)   // (see presolve_node: c within the box its moved_from / moved_to bounds imply)
+    for (int k = 0; k < F * N; ++k) {
+      const double old = -m.lo[m.dl.oD1 + k];
+      ub[m.il.oc + k] = std::min(ub[m.il.oc + k], old + ub[m.il.omf + k]);
+      lb[m.il.oc + k] = std::max(lb[m.il.oc + k], old - ub[m.il.omt + k]);
+    }
   bool ok = true;
   if (m.has_n)
     for (int j = 0; j < N; ++j)
@@ -978,6 +984,35 @@ bool presolve_node(Model &m, const double *lbi, const double *ubi, std::vector<i
       ci.push_back(k);
       cl.push_back(l);
       cu.push_back(u);
+    }
+  }
+  if (m.step2) {
+    // bound propagation through the disruption rows D1 / D2 (constraints_step2.py:5-16): mf - c >= -old and
+    // mt + c >= old give c <= old + ub(mf) and c >= old - ub(mt).  A node that fixes moved_from = 0 where
+    // old = 0 closes the placement — so its routing column is masked, instead of PDHG having to find that its
+    // flow must be 0 through the 1/M-priced big-M row (payload.json step 2: 1.4 units of flow left on such a
+    // column after 200k iterations)
+    const size_t nc = ci.size();
+    for (size_t t = c0; t < nc; ++t) {
+      const int k = ci[t];
+      const bool isf = k >= m.il.omf && k < m.il.omf + F * N, ist = k >= m.il.omt && k < m.il.omt + F * N;
+      if (!isf && !ist) continue;
+      const int q = k - (isf ? m.il.omf : m.il.omt);
+      const double old = -m.lo[m.dl.oD1 + q];
+      const int kc = oc + q;
+      double nl = -INF, nu = INF;
+      if (isf) nu = old + cu[t];
+      else nl = old - cu[t];
+      if (m.pos[kc] >= 0) {
+        const size_t pc = c0 + m.pos[kc];
+        cu[pc] = std::min(cu[pc], nu);
+        cl[pc] = std::max(cl[pc], nl);
+      } else if (nu < m.base_ub[kc] || nl > m.base_lb[kc]) {
+        m.pos[kc] = (int)(ci.size() - c0);
+        ci.push_back(kc);
+        cl.push_back(std::max(m.base_lb[kc], nl));
+        cu.push_back(std::min(m.base_ub[kc], nu));
+      }
     }
   }
   if (m.has_n) {

@@ -46,11 +46,25 @@ namespace nep {
 // (x_pass, after the shift), so the shift may exceed fp32 rounding: pooled flow carries no cost, CPU load or
 // score coefficient, and a donor keeps S >= c - eps, so every row the certificate checks holds as before.
 constexpr double kShiftMax = 1e-3;
+// the c a shift aims the column at: the iterate's c clamped into its node box and, on step 2, into the box
+// the disruption rows imply with moved_from / moved_to fixed (constraints_step2.py:5-16: c <= old + ub_mf,
+// c >= old - ub_mt — e.g. moved_to = 0 on an old placement forces c = 1)
+__device__ __forceinline__ double c_target(const DeviceView &v, const double *zi, const double *lb, const double *ub,
+                                           int f, int j) {
+  const int k = v.il.oc + f * v.N + j;
+  double lo = lb[k], hi = ub[k];
+  if (v.step2) {
+    const int idx = f * v.N + j;
+    const double old = -v.lo[v.dl.oD1 + idx];
+    lo = fmax(lo, old - ub[v.il.omt + idx]);
+    hi = fmin(hi, old + ub[v.il.omf + idx]);
+  }
+  return fmin(fmax(zi[k], lo), hi);
+}
 __device__ __forceinline__ void pooled_shift(const DeviceView &v, int slot, int f, double *S, double *pm, int lane) {
   const int N = v.N;
   const double *zi = v.zi + slot * v.sint, *lb = v.lb + slot * v.sint, *ub = v.ub + slot * v.sint;
-  const int oc = v.il.oc + f * N;
-  auto target = [&](int j) { return fmin(fmax(zi[oc + j], lb[oc + j]), ub[oc + j]); };
+  auto target = [&](int j) { return c_target(v, zi, lb, ub, f, j); };
   for (int j0 = 0; j0 < N; j0 += kWave) {
     const int j = j0 + lane;
     // deficits up to kShiftMax (the stored row takes the shift: see x_pass)
@@ -95,8 +109,7 @@ __device__ __forceinline__ void loaded_shift(const DeviceView &v, int slot, int 
                                              double *S, double *Wd, double &dpobj, double &dscore, int lane) {
   const int N = v.N, NP = v.NP;
   const double *zi = v.zi + slot * v.sint, *lb = v.lb + slot * v.sint, *ub = v.ub + slot * v.sint;
-  const int oc = v.il.oc + f * N;
-  auto target = [&](int j) { return fmin(fmax(zi[oc + j], lb[oc + j]), ub[oc + j]); };
+  auto target = [&](int j) { return c_target(v, zi, lb, ub, f, j); };
   for (int j0 = 0; j0 < N; j0 += kWave) {
     const int j = j0 + lane;
     const double need = j < N ? target(j) - v.eps - S[j] : 0.0;
@@ -712,7 +725,15 @@ void x_pass(DeviceView v, const int32_t *__restrict__ slots, int plain, int it, 
       // mt = max(lb, old - c) (D1/D2; both cost F*N).  At convergence the clamp moves c by the PDHG
       // residual only, so the repaired point keeps the iterate's (near-optimal) choices; an empty
       // interval is a violation of the x-driven row.
-      const double loc = fmax(lb[il.oc + idx], S / v.M), hic = fmin(ub[il.oc + idx], S + v.eps);
+      double loc = fmax(lb[il.oc + idx], S / v.M), hic = fmin(ub[il.oc + idx], S + v.eps);
+      if (v.step2) {   // within the box the D rows imply at the node's moved_from / moved_to bounds, if any
+        const double old = -v.lo[dl.oD1 + idx];
+        const double dlo = old - ub[il.omt + idx], dhi = old + ub[il.omf + idx];
+        if (fmax(loc, dlo) <= fmin(hic, dhi)) {
+          loc = fmax(loc, dlo);
+          hic = fmin(hic, dhi);
+        }
+      }
       const double cr = loc > hic ? loc : fmin(fmax(cn, loc), hic);
       if (v.step2) {
         const double old = -v.lo[dl.oD1 + idx];

@@ -3,10 +3,10 @@ recorded models (root LPs of every step model, and seeded B&B-node fixings), wit
 
 A certified LP (NEP_LP_OPTIMAL) must be within 1e-6 max(1, |HiGHS|): the certificate evaluates the
 primal at a repaired, feasible point, so a certified value is an LP value, not only a
-bound.  Every LP must certify, except the step-2 node LPs listed in KNOWN_UNCERTIFIED (DESIGN.md §4
-'Known limit': their fixings force a routing column to carry >= 1 - eps and the PDHG routing stays
-~1e-6 short of it after 200k iterations); those must still return a bound within 1e-6 of HiGHS, and the
-test is reported XFAIL (not passed) while they stay uncertified."""
+bound.  Every LP must certify.  (Until round 4 two step-2 node LPs — payload model 1 LP 1, syn_4x3
+MinUtilization model 1 LP 3 — were listed uncertified: their boxes fix moved_from = 0 where old = 0, which
+closes the placement through D1, and PDHG left ~1 unit of flow on it; the presolve now propagates D1/D2 onto
+c's bounds and masks such columns)"""
 import numpy as np
 import pytest
 
@@ -17,13 +17,6 @@ TOL = 1e-6
 SOLVE_TOL = 5e-7      # certificate tolerance of the solves: below the 1e-6 parity bar
 
 
-# (golden case, model, LP index: 0 = root) -> why it does not certify (tools/step2_split_probe.py,
-# profiles/r03/step2_split_probe.log)
-KNOWN_UNCERTIFIED = {
-    ("payload", 1, 1): "moved_to fixed 0 on an old placement: the routing column stays 1.4e-6 short of 1 - eps",
-    ("syn_4x3_s0_r0.5_NeptuneMinUtilization", 1, 3): "forced placement: routing column 9e-7 short of 1 - eps",
-}
-
 
 def _gap(a, b):
     return abs(a - b) / max(1.0, abs(b))
@@ -31,7 +24,7 @@ def _gap(a, b):
 
 @pytest.mark.parametrize("name,k", lp_cases())
 def test_root_and_node_lps(name, k):
-    from core.engine.lp import LPModel, LP_ITERATION_LIMIT, LP_OPTIMAL
+    from core.engine.lp import LPModel, LP_OPTIMAL
     data, variant, step, kw = build_args(name, k)
     rec = G[name]["models"][k]
     nodes = G[name]['models'][k].get('node_lps', [])
@@ -44,28 +37,18 @@ def test_root_and_node_lps(name, k):
     ub = np.full((B, m.n_int), np.inf)
     for b, (l, u, _) in enumerate(nodes):
         lb[b + 1], ub[b + 1] = l, u
-    res = m.solve(np.arange(B), lb, ub, tol=SOLVE_TOL, max_iters=200000 if step >= 2 else 100000)
+    # (step 2: syn_6x4 MDU model 1 LP 3 certifies at 360k iterations, tools/step2_cert_probe.py)
+    res = m.solve(np.arange(B), lb, ub, tol=SOLVE_TOL, max_iters=400000 if step >= 2 else 100000)
     refs = [rec["lp_objective"]] + [r for _, _, r in nodes]
-    known = []
     for b, ref in enumerate(refs):
         st, obj = int(res["status"][b]), float(res["obj"][b])
         if ref is None:
             assert st != LP_OPTIMAL, f"node {b}: HiGHS infeasible but engine says optimal obj={obj}"
             continue
         assert obj <= ref + TOL * max(1.0, abs(ref)), f"node {b}: bound {obj} above the LP optimum {ref}"
-        why = KNOWN_UNCERTIFIED.get((name, k, b))
-        if st != LP_OPTIMAL and why is not None:
-            # a known uncertified step-2 LP: its bound must still equal HiGHS within 1e-6 (it is never a
-            # B&B incumbent); reported as XFAIL below
-            assert st == LP_ITERATION_LIMIT and _gap(obj, ref) <= TOL, f"node {b}: status {st} bound {obj} vs {ref}"
-            print(f"UNCERTIFIED step-2 LP {name} model {k} node {b}: bound {obj} (HiGHS {ref}): {why}")
-            known.append(f"LP {b}: {why}")
-            continue
         assert st == LP_OPTIMAL, f"node {b}: status {st} iters {res['iters'][b]} obj {obj} (HiGHS {ref})"
         assert _gap(obj, ref) <= TOL, f"node {b}: obj {obj} ref {ref} primal {res['primal_obj'][b]}"
     m.close()
-    if known:
-        pytest.xfail("uncertified (bound within 1e-6 of HiGHS): " + "; ".join(known))
 
 
 @pytest.mark.parametrize("continuous", [False, True])
