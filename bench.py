@@ -52,7 +52,7 @@ HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md "HBM")
 def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=24)
+    ap.add_argument("--steps", type=int, default=12)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--nodes", type=int, default=512)
     ap.add_argument("--functions", type=int, default=256)
@@ -77,7 +77,7 @@ def parse(argv=None):
                     help="the timed node-LP stream: the product B&B's recorded nodes (replay, tests/golden/"
                          "bnb_trace_<N>x<F>_s<seed>.json.gz) or root children with --fix random fixings; auto: "
                          "replay when the trace exists")
-    ap.add_argument("--native-steps", type=int, default=8,
+    ap.add_argument("--native-steps", type=int, default=6,
                     help="with the replay stream: steps of the native-model replay timed after it (each recorded "
                          "box on the model the product ran it on; 0 = skip)")
     ap.add_argument("--children-steps", type=int, default=24,

@@ -7,9 +7,10 @@ On the GPU box, one counter per pass (FETCH_SIZE and WRITE_SIZE do not fit one T
 Then (anywhere):
   python3 tools/traffic.py summarize gpurun_out/pmc_fetch gpurun_out/pmc_write > profiles/traffic.json
 
-`run` builds bench.py's default model (same generator, seed, batch), starts the batch's node LPs
-cold and runs 4 blocks of PDHG iterations: a few hundred dispatches, x_pass steady-state launches
-with all `batch` LPs active, as in the bench's timed region.  `summarize` averages the counters
+`run` builds bench.py's default model (same generator, seed, batch), starts `batch` node LPs on the
+first boxes of the bench's replay stream (tests/golden/bnb_trace_*.json.gz), warm from the root state as
+the replay does, and runs 4 blocks of PDHG iterations: a few hundred dispatches, x_pass steady-state
+launches with all `batch` LPs active, as in the bench's timed region.  `summarize` averages the counters
 over the steady-state x_pass launches (x_pass<CPL, false, false>, full grid) and converts them:
 FETCH_SIZE and WRITE_SIZE are KiB (rocprofiler-sdk derived_counters.xml); FETCH_SIZE is doubled for
 wide streaming reads on gfx950 (MI355X_MICROARCH.md, HBM).
@@ -29,15 +30,25 @@ def run():
     from core.engine.lp import LPModel
     from core.utils import data_to_solver_input
     from core.utils.synthetic import synthetic_payload
+    import gzip
     a = bench.parse([])
     p = synthetic_payload(a.nodes, a.functions, seed=a.seed)
     d = data_to_solver_input(p, with_db=False)
-    m = LPModel(d, "MinDelayAndUtilization", step=1, alpha=p["solver"]["args"]["alpha"], max_batch=a.batch)
-    lb, ub = bench.node_bounds(m.n_int, a.functions, a.nodes, a.batch, a.fix, seed=a.seed)
-    m.submit(np.arange(a.batch), lb, ub, tol=a.tol, max_iters=a.max_iters, check_every=a.check_every)
+    m = LPModel(d, "MinDelayAndUtilization", step=1, alpha=p["solver"]["args"]["alpha"], max_batch=a.batch + 1)
+    root = a.batch
+    m.solve([root], tol=a.tol, max_iters=a.root_max_iters, check_every=a.root_check_every)
+    with gzip.open(bench.trace_path(a), "rt") as fh:
+        trace = json.load(fh)
+    rs = bench.ReplayStream({"leaf": (m, root)}, a, 0, 1, trace)
+    boxes = [rs._box(m, e) for e in rs.lps[:a.batch]]
+    lb = np.array([b[0] for b in boxes])
+    ub = np.array([b[1] for b in boxes])
+    for s in range(a.batch):
+        m.copy_state(root, s)
+    m.submit(np.arange(a.batch), lb, ub, tol=a.tol, max_iters=a.max_iters, check_every=a.check_every, warm_start=True)
     for _ in range(4):
         m.advance(0)
-    print(json.dumps({"workload": bench.workload_name(a), "active": m.active(), "P": m.info.x_entries}))
+    print(json.dumps({"workload": bench.workload_name(a, "replay"), "active": m.active(), "P": m.info.x_entries}))
     m.close()
 
 
@@ -68,10 +79,10 @@ def summarize(fetch_dir, write_dir):
     write_kib = sum(w[wk]) / len(w[wk])
     fetch_b = 2.0 * fetch_kib * 1024.0
     write_b = write_kib * 1024.0
-    out = {"workload": bench.workload_name(a), "kernel": "x_pass<CPL,false,false>", "lps_per_launch": fk[1],
+    out = {"workload": bench.workload_name(a, "replay"), "kernel": "x_pass<CPL,false,false>", "lps_per_launch": fk[1],
            "fetch_kib_raw": fetch_kib, "write_kib_raw": write_kib, "fetch_bytes": fetch_b, "write_bytes": write_b,
            "bytes_per_launch": fetch_b + write_b, "launches": [len(f[fk]), len(w[wk])],
-           "note": "FETCH_SIZE x2 (gfx950 wide-read tally), KiB -> bytes; per steady-state x_pass launch"}
+           "note": "FETCH_SIZE x2 (gfx950 wide-read tally), KiB -> bytes; per steady-state x_pass launch; the bench model with the replay stream's first `batch` boxes iterating"}
     print(json.dumps(out, indent=1))
 
 
@@ -82,7 +93,7 @@ def summarize_sq(d):
     a = bench.parse([])
     c = _counters(d, a.functions)
     top = max(k[1] for k in c)
-    out = {"workload": bench.workload_name(a), "kernel": "x_pass<CPL,false,false,false>", "lps_per_launch": top,
+    out = {"workload": bench.workload_name(a, "replay"), "kernel": "x_pass<CPL,false,false,false>", "lps_per_launch": top,
            "counters": {k[0]: sum(v) / len(v) for k, v in c.items() if k[1] == top},
            "launches": max(len(v) for k, v in c.items() if k[1] == top)}
     print(json.dumps(out, indent=1))
