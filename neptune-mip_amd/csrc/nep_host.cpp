@@ -666,9 +666,12 @@ int setup_device(Model &m, int max_batch, void *stream) {
   // the auxiliary stream (host reads of finished slots, warm-start copies, submits) at the highest priority:
   // its small kernels and copies are dispatched between the workgroups of the block in flight instead of
   // queueing behind it (round-4 B&B profile: a flows read waited ~0.5 ms for a 64x32 block)
+  // (NEP_AUX_PRIORITY=0: default priority — the rocprofv3 PMC passes of tools/traffic.py run that way)
   {
     int least = 0, greatest = 0;
     if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) greatest = 0;
+    const char *e = std::getenv("NEP_AUX_PRIORITY");
+    if (e && std::atoi(e) == 0) greatest = least;
     HIPCHK(hipStreamCreateWithPriority(&m.aux, hipStreamNonBlocking, greatest));
   }
   HIPCHK(hipEventCreateWithFlags(&m.ev_aux, hipEventDisableTiming));

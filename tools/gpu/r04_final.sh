@@ -5,11 +5,9 @@ set -u
 cd "$GRAFT_REPO_ROOT"
 O=gpurun_out/${1:-r04_final}; mkdir -p "$O"
 export TMPDIR=/tmp
-timeout -k 10 180 rocprofv3 --kernel-trace --stats -d "$O/prof" -o run -- python3 bench.py --steps 4 --native-steps 0 --children-steps 4 --bnb-seconds 0 --cpu-budget 0 > "$O/prof_bench.json" 2> "$O/prof_bench.err"
-rc=$?; echo "rocprof rc=$rc"; [ $rc -eq 0 ] || exit $rc
-timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d "$O/pmc_fetch" -o run -- python3 tools/traffic.py run > "$O/pmc_fetch.log" 2>&1
+NEP_AUX_PRIORITY=0 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d "$O/pmc_fetch" -o run -- python3 tools/traffic.py run > "$O/pmc_fetch.log" 2>&1
 rc=$?; echo "pmc fetch rc=$rc"; [ $rc -eq 0 ] || exit $rc
-timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d "$O/pmc_write" -o run -- python3 tools/traffic.py run > "$O/pmc_write.log" 2>&1
+NEP_AUX_PRIORITY=0 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d "$O/pmc_write" -o run -- python3 tools/traffic.py run > "$O/pmc_write.log" 2>&1
 rc=$?; echo "pmc write rc=$rc"; [ $rc -eq 0 ] || exit $rc
 python3 tools/traffic.py summarize "$O/pmc_fetch" "$O/pmc_write" > "$O/traffic.json" && cp "$O/traffic.json" profiles/traffic.json
 rc=$?; echo "summarize rc=$rc"; cat "$O/traffic.json"; [ $rc -eq 0 ] || exit $rc

@@ -8,9 +8,10 @@ Then (anywhere):
   python3 tools/traffic.py summarize gpurun_out/pmc_fetch gpurun_out/pmc_write > profiles/traffic.json
 
 `run` builds bench.py's default model (same generator, seed, batch), starts `batch` node LPs on the
-first boxes of the bench's replay stream (tests/golden/bnb_trace_*.json.gz), warm from the root state as
-the replay does, and runs 4 blocks of PDHG iterations: a few hundred dispatches, x_pass steady-state
-launches with all `batch` LPs active, as in the bench's timed region.  `summarize` averages the counters
+first boxes of the bench's replay stream (tests/golden/bnb_trace_*.json.gz), cold (no root solve: a
+solve_batch of the lone root crashed rocprofv3's --pmc pass in round 4), and runs 4 blocks of PDHG
+iterations: a few hundred dispatches, x_pass steady-state launches with all `batch` LPs active, as in the
+bench's timed region.  Run it with NEP_AUX_PRIORITY=0.  `summarize` averages the counters
 over the steady-state x_pass launches (x_pass<CPL, false, false>, full grid) and converts them:
 FETCH_SIZE and WRITE_SIZE are KiB (rocprofiler-sdk derived_counters.xml); FETCH_SIZE is doubled for
 wide streaming reads on gfx950 (MI355X_MICROARCH.md, HBM).
@@ -34,18 +35,14 @@ def run():
     a = bench.parse([])
     p = synthetic_payload(a.nodes, a.functions, seed=a.seed)
     d = data_to_solver_input(p, with_db=False)
-    m = LPModel(d, "MinDelayAndUtilization", step=1, alpha=p["solver"]["args"]["alpha"], max_batch=a.batch + 1)
-    root = a.batch
-    m.solve([root], tol=a.tol, max_iters=a.root_max_iters, check_every=a.root_check_every)
+    m = LPModel(d, "MinDelayAndUtilization", step=1, alpha=p["solver"]["args"]["alpha"], max_batch=a.batch)
     with gzip.open(bench.trace_path(a), "rt") as fh:
         trace = json.load(fh)
-    rs = bench.ReplayStream({"leaf": (m, root)}, a, 0, 1, trace)
+    rs = bench.ReplayStream({"leaf": (m, 0)}, a, 0, 1, trace)
     boxes = [rs._box(m, e) for e in rs.lps[:a.batch]]
     lb = np.array([b[0] for b in boxes])
     ub = np.array([b[1] for b in boxes])
-    for s in range(a.batch):
-        m.copy_state(root, s)
-    m.submit(np.arange(a.batch), lb, ub, tol=a.tol, max_iters=a.max_iters, check_every=a.check_every, warm_start=True)
+    m.submit(np.arange(a.batch), lb, ub, tol=a.tol, max_iters=a.max_iters, check_every=a.check_every)
     for _ in range(4):
         m.advance(0)
     print(json.dumps({"workload": bench.workload_name(a, "replay"), "active": m.active(), "P": m.info.x_entries}))
