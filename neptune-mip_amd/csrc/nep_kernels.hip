@@ -36,6 +36,11 @@
 #ifndef NEP_INLINE_REFLECT
 #define NEP_INLINE_REFLECT 0
 #endif
+// waves per SIMD the certificate x_pass is compiled for (build flag; 2: 210 VGPRs, no spills; 3: 168 VGPRs
+// with 160 B/lane of spills, matching the 3 workgroups per CU its LDS allows)
+#ifndef NEP_CHECK_WAVES
+#define NEP_CHECK_WAVES 2
+#endif
 
 namespace nep {
 
@@ -180,7 +185,7 @@ __device__ __forceinline__ void loaded_shift(const DeviceView &v, int slot, int 
 // certificate iteration takes effect and the anchor is rewritten; the steady-state variant carries
 // no restart code (fewer registers live).
 template <int CPL, bool CHECK, bool INIT, bool FIRST, int TW>
-__global__ __launch_bounds__(kWave * TW) __attribute__((amdgpu_waves_per_eu(CHECK ? 2 : (TW == 16 ? 4 : 6), 8)))
+__global__ __launch_bounds__(kWave * TW) __attribute__((amdgpu_waves_per_eu(CHECK ? NEP_CHECK_WAVES : (TW == 16 ? 4 : 6), 8)))
 void x_pass(DeviceView v, const int32_t *__restrict__ slots, int plain, int it, int nslots, int nt_i) {
   const bool nt = nt_i != 0;
   constexpr int E = 4 * CPL;
