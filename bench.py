@@ -90,7 +90,8 @@ def parse(argv=None):
     ap.add_argument("--bnb-seconds", type=float, default=20.0,
                     help="time limit of the product branch-and-bound section (0 = skip)")
     ap.add_argument("--bnb-sizes", default="256x128,512x256",
-                    help="instances of the product B&B section (BASELINE configs 3 and 4), NxF comma-separated")
+                    help="instances of the product B&B section (BASELINE configs 3 and 4), NxF[:seconds] "
+                         "comma-separated (seconds: that instance's time limit, default --bnb-seconds)")
     ap.add_argument("--traffic", default=os.path.join(REPO, "profiles", "traffic.json"))
     return ap.parse_args(argv)
 
@@ -250,7 +251,7 @@ def cpu_baseline(N, F, seed, fix, budget, workers):
             "measured": [{"nodes": a, "functions": b, "seconds": t, "status": s} for a, b, t, s in pts]}
 
 
-def bnb_section(a, rank, world, dev, N, F):
+def bnb_section(a, rank, world, dev, N, F, seconds):
     """The product's own branch-and-bound (core/engine/bnb.py, the search SCIP runs inside
     pywraplp Solve(), solver.py:35-40) on BASELINE config 3's / 4's instance (256x128, 512x256, step-1
     NeptuneMinDelayAndUtilization), time-limited, configured as the product's step 1 runs it
@@ -273,7 +274,7 @@ def bnb_section(a, rank, world, dev, N, F):
     m = LPModel(data, "MinDelayAndUtilization", step=1, alpha=alpha, max_batch=a.batch + 2)
     bm = st1.bound_model(data, a.batch + 1)
     comm = TorchComm(device=dev) if world > 1 else LocalComm()
-    bnb = st1.branch_and_bound(m, bm, time_limit=a.bnb_seconds, comm=comm, check_every=a.check_every,
+    bnb = st1.branch_and_bound(m, bm, time_limit=seconds, comm=comm, check_every=a.check_every,
                                root_max_iters=a.root_max_iters)
     m.reset_stats()
     t0 = time.perf_counter()
@@ -288,7 +289,7 @@ def bnb_section(a, rank, world, dev, N, F):
     gap = None if inc is None else (inc - res.bound) / max(1.0, abs(inc))
     d = res.as_dict()
     finished = sum(v for k, v in res.lp_status.items() if k != "presolve_infeasible")
-    return {"workload": f"synthetic_{N}x{F}_step1_MDU_product_bnb", "time_limit_s": a.bnb_seconds,
+    return {"workload": f"synthetic_{N}x{F}_step1_MDU_product_bnb", "time_limit_s": seconds,
             "status": res.status, "wall_s": wall, "nodes": res.nodes, "leaves": res.leaves, "lps": res.lps,
             "certified_lps": res.certified, "certified_lp_per_s": res.certified / wall, "nodes_per_s": res.nodes / wall,
             "certified_share": res.certified / max(1, finished),
@@ -618,8 +619,9 @@ def main():
     if a.bnb_seconds > 0:
         bnb = []
         for size in a.bnb_sizes.split(","):
+            size, _, secs = size.partition(":")
             bn, bf = (int(t) for t in size.lower().split("x"))
-            bnb.append(bnb_section(a, rank, world, dev, bn, bf))
+            bnb.append(bnb_section(a, rank, world, dev, bn, bf, float(secs) if secs else a.bnb_seconds))
             log(f"rank {rank}: bnb {size}: {bnb[-1]['certified_lps']} certified node LPs, status {bnb[-1]['status']}, "
                 f"gap {bnb[-1]['rel_gap']}")
     if rank != 0:

@@ -80,6 +80,7 @@ class BnBResult:
         self.polished = False    # the incumbent's LP was re-solved at the polish tolerance
         self.repaired = None     # the CPU repair of the returned routing succeeded (None: not run)
         self.heuristic_incumbents = 0   # incumbents taken from a checked heuristic point (no LP behind them)
+        self.routing_warm = 0           # leaves warm-started with their branching node's routing (two models)
         # node-LP mix: finished LPs per engine status (+ presolve-infeasible submits) and their iterations
         self.lp_status = {"certified": 0, "bound": 0, "limit": 0, "infeasible": 0, "cutoff": 0, "numerical": 0,
                           "presolve_infeasible": 0}
@@ -99,7 +100,7 @@ class BnBResult:
         d = {k: getattr(self, k) for k in ("status", "objective", "bound", "nodes", "leaves", "lps", "certified",
                                            "lp_iterations", "unresolved", "seconds", "polished", "repaired",
                                            "lp_status", "lp_status_kind", "drained", "timing",
-                                           "heuristic_incumbents")}
+                                           "heuristic_incumbents", "routing_warm")}
         d["inflight_mean"] = self.inflight_sum / max(1, self.advance_calls)
         d["resolved"] = sum(v for k, v in self.lp_status.items() if k not in ("limit", "numerical"))
         it = np.asarray(self.lp_iters, np.float64)
@@ -150,7 +151,8 @@ class BranchAndBound:
                  warm=True, root_max_iters=200000, check_every=12, polish_tol=1e-8, polish_iters=20000,
                  seed_leaves=None, integer_bound=None, improve=None, repair=None, node_bound_res=1e-2,
                  retry_res=math.inf, unit_flow_leaves=True, node_max_iters=None, bound_lp=None, bound_gap=1e-4,
-                 trace=None, rebalance_every=8, primal=None, primal_every=0, leaf_warm_incumbent=False):
+                 trace=None, rebalance_every=8, primal=None, primal_every=0, leaf_warm_incumbent=False,
+                 leaf_routing_warm=True):
         self.lp = lp
         self.two = bound_lp is not None
         self.N, self.F = lp.N, lp.F
@@ -183,6 +185,9 @@ class BranchAndBound:
         # leaves (and their retries) warm-start from the incumbent leaf's final state once there is one
         # (its routing and CPU prices sit next to the new leaf's) instead of the reference root's
         self.leaf_warm_incumbent = bool(leaf_warm_incumbent)
+        # two models: a rounding leaf starts from the reference root's state with the routing x of the
+        # branching node it was rounded from (nep_lp_copy_routing) while that node's slot still holds it
+        self.leaf_routing_warm = bool(leaf_routing_warm)
         self.root_slot = lp.max_batch - 1
         self.inc_slot = lp.max_batch - 2
         self.tol, self.gap, self.max_iters = tol, gap, max_iters
@@ -299,6 +304,7 @@ class BranchAndBound:
         """items: [(engine, slot, node)].  One nep_lp_submit per (engine, warm, iteration budget) group."""
         groups = {}
         copies = {}
+        cross = []               # (leaf slot, branching-node slot of the bound model): routing warm starts
         cutoff = min(inc, self.ub0)
         for eng, slot, node in items:
             warm, src = False, None
@@ -314,6 +320,10 @@ class BranchAndBound:
                 if src != slot:
                     copies.setdefault(eng.name, (eng, []))[1].append((src, slot))
                 warm = True
+                if (self.two and self.leaf_routing_warm and node.kind == LEAF and eng is self.L
+                        and node.parent is not None and node.parent[0] is self.B
+                        and self.B.gen[node.parent[1]] == node.parent[2]):
+                    cross.append((slot, node.parent[1]))
             budget = (self.root_max_iters if (node.kind in (RETRY, REFROOT) or not eng.root_ready)
                       else (self.node_max_iters if node.kind == NODE else self.max_iters))
             # (the bound model's root is a branching node like the others: it stops once its bound converged)
@@ -323,8 +333,15 @@ class BranchAndBound:
             if self.trace is not None:
                 self.trace.append(self._trace_entry(eng, node, src if warm else None, budget, bres, cutoff))
         # warm-start copies: a slot that is both a parent state (source) and a new node's slot
-        # (destination) is read before it is overwritten; a cycle falls back to the root's state
-        for eng, cps in copies.values():
+        # (destination) is read before it is overwritten; a cycle falls back to the root's state.  The leaf
+        # model's copies run first, then the routing copies from the bound model's node slots (before that
+        # model's own copies may overwrite them)
+        order = sorted(copies.values(), key=lambda ec: 0 if ec[0] is self.L else 1)
+        done_cross = not cross
+        for eng, cps in order:
+            if not done_cross and eng is not self.L:
+                self._copy_cross(cross)
+                done_cross = True
             while cps:
                 srcs = {c[0] for c in cps}
                 k = next((i for i, (_, d) in enumerate(cps) if d not in srcs), None)
@@ -334,6 +351,8 @@ class BranchAndBound:
                     continue
                 src, dst = cps.pop(k)
                 eng.lp.copy_state(src, dst)
+        if not done_cross:
+            self._copy_cross(cross)
         for (_, warm, budget, bres), (eng, its) in groups.items():
             n_int = eng.lp.n_int
             slots = np.array([s for s, _ in its], np.int32)
@@ -477,6 +496,12 @@ class BranchAndBound:
                                            _Node(cb, idx, val, kind, me, node.depth + 1)))
         eng.free.append(slot)        # most recently finished last: its state survives longest
         return inc
+
+    def _copy_cross(self, cross):
+        """Routing warm starts of leaves from their branching nodes' slots of the bound model."""
+        for dst, src in cross:
+            self.L.lp.copy_routing_from(self.B.lp, src, dst)
+            self.res.routing_warm += 1
 
     def _heuristic_incumbent(self, sol):
         """A checked heuristic point as the incumbent: objective, z and routing (engine rows) taken as given,

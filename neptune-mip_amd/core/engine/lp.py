@@ -65,7 +65,7 @@ EXPORTS = ("nep_model_create", "nep_model_destroy", "nep_model_get_info", "nep_l
            "nep_lp_get_flows_split",
            "nep_last_error", "nep_api_version", "nep_lp_get_diag", "nep_debug_build", "nep_debug_state",
            "nep_debug_presolve", "nep_lp_set_params", "nep_lp_get_flows", "nep_lp_routing_entries",
-           "nep_lp_allocation_entries", "nep_lp_score_check", "nep_round_leaf")
+           "nep_lp_allocation_entries", "nep_lp_score_check", "nep_round_leaf", "nep_lp_copy_routing")
 SCORE_FIELDS = ("network_delay", "nodes_used", "node_cost", "bad_c_x", "bad_memory", "bad_handle", "bad_cpu",
                 "bad_n_c", "bad_budget", "handle_maxdev", "cpu_maxexcess")
 
@@ -96,6 +96,7 @@ def load_library(path=None):
     lib.nep_lp_get_rows.argtypes = [vp, i32, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(i32),
                                     ctypes.POINTER(i32)]
     lib.nep_lp_copy_state.argtypes = [vp, i32, i32]
+    lib.nep_lp_copy_routing.argtypes = [vp, i32, vp, i32]
     lib.nep_get_stats.argtypes = [vp, ctypes.POINTER(Stats)]
     lib.nep_reset_stats.argtypes = [vp]
     lib.nep_reset_stats.restype = None
@@ -431,6 +432,11 @@ class LPModel:
 
     def copy_state(self, src, dst):
         _check(self._lib, self._lib.nep_lp_copy_state(self._h, int(src), int(dst)), "nep_lp_copy_state")
+
+    def copy_routing_from(self, other, src, dst):
+        """x and thresholds of slot `src` of model `other` (same instance and rows, e.g. the facility
+        relaxation's) into this model's slot `dst` (nep_lp_copy_routing)."""
+        _check(self._lib, self._lib.nep_lp_copy_routing(self._h, int(dst), other._h, int(src)), "nep_lp_copy_routing")
 
     def stats(self):
         s = Stats()

@@ -1713,6 +1713,28 @@ int nep_lp_copy_state(void *model, int32_t src, int32_t dst) {
   return NEP_OK;
 }
 
+int nep_lp_copy_routing(void *dst_model, int32_t dst_slot, void *src_model, int32_t src_slot) {
+  if (!dst_model || !src_model) return fail(NEP_ERR_ARG, "null model");
+  Model &d = *static_cast<Model *>(dst_model);
+  Model &s = *static_cast<Model *>(src_model);
+  if (dst_slot < 0 || dst_slot >= d.max_batch || src_slot < 0 || src_slot >= s.max_batch)
+    return fail(NEP_ERR_ARG, "slot out of range");
+  if (d.busy[dst_slot]) return fail(NEP_ERR_STATE, "destination slot is still iterating");
+  if (s.busy[src_slot]) return fail(NEP_ERR_STATE, "source slot is still iterating");
+  if (d.R != s.R || d.N != s.N || d.NP != s.NP || d.F != s.F || d.row_f != s.row_f || d.row_src != s.row_src)
+    return fail(NEP_ERR_ARG, "the two models' routing rows differ");
+  if (&d == &s && dst_slot == src_slot) return NEP_OK;
+  // the source's own queued work on its slot first (its aux stream); then the copies on the destination's
+  // aux stream, waited for: the source model may rewrite its slot on its own streams right after this call
+  HIPCHK(hipStreamSynchronize(s.aux));
+  HIPCHK(hipMemcpyAsync(d.v.x + dst_slot * d.v.sx, s.v.x + src_slot * s.v.sx, d.v.sx * sizeof(float),
+                        hipMemcpyDeviceToDevice, d.aux));
+  HIPCHK(hipMemcpyAsync(d.v.theta + dst_slot * d.R, s.v.theta + src_slot * s.R, d.R * sizeof(float),
+                        hipMemcpyDeviceToDevice, d.aux));
+  HIPCHK(hipStreamSynchronize(d.aux));
+  return NEP_OK;
+}
+
 int nep_lp_set_params(void *model, double tol, double cutoff) {
   if (!model) return fail(NEP_ERR_ARG, "null model");
   Model &m = *static_cast<Model *>(model);

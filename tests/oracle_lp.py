@@ -126,6 +126,13 @@ class OracleLP:
         self.copies = getattr(self, "copies", 0) + 1
         self._sol[int(dst)] = self._sol.get(int(src))
 
+    def copy_routing_from(self, other, src, dst):
+        """nep_lp_copy_routing: HiGHS has no routing state to take, so this records the hand-off only (the B&B
+        tests check the two-model search issues it with a live bound-model slot)."""
+        assert other is not self and other.N == self.N and other.F == self.F
+        assert int(src) in other._sol, "routing warm start from a slot the bound model never solved"
+        self.routing_copies = getattr(self, "routing_copies", 0) + 1
+
     def rows(self, slot):
         x = self._sol[int(slot)]
         xb = x[:self.nx].reshape(self.F * self.N, self.N).astype(np.float32)

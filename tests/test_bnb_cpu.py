@@ -127,6 +127,7 @@ def test_bnb_two_models_matches_recorded_mip(name, k):
     else:
         assert res.status == INFEASIBLE, res.as_dict()
     assert res.lp_status_kind["refroot"]["certified"] + res.lp_status_kind["refroot"]["cutoff"] <= 1
+    assert res.routing_warm == getattr(lp, "routing_copies", 0)
 
 
 @pytest.mark.parametrize("name,k", STEP1_N[:8])
@@ -202,3 +203,24 @@ def test_heuristic_incumbent_is_feasible_reference_point(name, k):
     assert (act <= m["hi"] + 1e-6).all() and (act >= m["lo"] - 1e-6).all()
     assert (full >= m["lb"] - 1e-12).all() and (full <= m["ub"] + 1e-12).all()
     assert abs(float(m["c"] @ full) - res.objective) <= 1e-9 * max(1.0, abs(res.objective))
+
+
+
+def test_two_model_leaves_take_routing_warm_starts():
+    """Leaves of the two-model search start from their branching node's routing (nep_lp_copy_routing) when
+    that node's bound-model slot still holds it: across the step-1 goldens some do, and every hand-off reads a
+    slot the bound model solved (the oracle stub asserts it)."""
+    from core.engine.bnb import BranchAndBound
+    from oracle_lp import StreamingOracleLP
+    total = 0
+    for name, k in STEP1_N[:6]:
+        p, data = _data(name)
+        variant = VARIANT[p["solver"]["type"]]
+        alpha = p["solver"].get("args", {}).get("alpha", 0.5)
+        lp = StreamingOracleLP(data, variant, step=1, max_batch=10, alpha=alpha)
+        blp = StreamingOracleLP(data, variant, step=1, max_batch=9, alpha=alpha, relaxation=1)
+        res = BranchAndBound(lp, data.workload_matrix, data.function_memory_matrix, data.node_memory_matrix,
+                             batch=8, node_limit=20000, bound_lp=blp).solve()
+        assert res.routing_warm == getattr(lp, "routing_copies", 0)
+        total += res.routing_warm
+    assert total > 0
