@@ -89,7 +89,7 @@ def parse(argv=None):
                     help="CPU baseline worker processes (capped at the host's cores; 16 = the GPU box's share)")
     ap.add_argument("--bnb-seconds", type=float, default=20.0,
                     help="time limit of the product branch-and-bound section (0 = skip)")
-    ap.add_argument("--bnb-sizes", default="256x128,512x256",
+    ap.add_argument("--bnb-sizes", default="256x128:20,512x256:60",
                     help="instances of the product B&B section (BASELINE configs 3 and 4), NxF[:seconds] "
                          "comma-separated (seconds: that instance's time limit, default --bnb-seconds)")
     ap.add_argument("--traffic", default=os.path.join(REPO, "profiles", "traffic.json"))

@@ -132,7 +132,8 @@ class NeptuneStepBase(Solver):
             nfix[idx[sel] - n0] = np.asarray(val)[sel]
             out = []
             for C, n, _, route in capacity_greedy(W, D, cpr, cores, fmem, nmem, np.asarray(z[n0:n1], np.float64),
-                                                  flow=flow, tries=2, node_cost=wts[0], delay_coef=wts[1],
+                                                  flow=flow, tries=3, node_cost=wts[0], delay_coef=wts[1],
+                                                  new_pen=1.0,
                                                   c_fix=cfix.reshape(F, N), n_fix=nfix):
                 sol = None if row_map is None else self._greedy_incumbent(C, n, route, row_map, wts, layout)
                 out.append((np.concatenate([np.arange(c0, c1), np.arange(n0, n1)]), np.concatenate([C.ravel(), n]),

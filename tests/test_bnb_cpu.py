@@ -220,7 +220,7 @@ def test_two_model_leaves_take_routing_warm_starts():
         lp = StreamingOracleLP(data, variant, step=1, max_batch=10, alpha=alpha)
         blp = StreamingOracleLP(data, variant, step=1, max_batch=9, alpha=alpha, relaxation=1)
         res = BranchAndBound(lp, data.workload_matrix, data.function_memory_matrix, data.node_memory_matrix,
-                             batch=8, node_limit=20000, bound_lp=blp).solve()
+                             batch=8, node_limit=20000, bound_lp=blp, leaf_routing_warm=True).solve()
         assert res.routing_warm == getattr(lp, "routing_copies", 0)
         total += res.routing_warm
     assert total > 0

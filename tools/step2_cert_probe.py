@@ -5,6 +5,7 @@ then per (f, j): the column sum S (device flows), the repaired c / moved_from / 
 and the C1/C2 (S vs c) and D1/D2 (moves vs c, old) violations; beside them HiGHS's optimum of the same LP.
 
   python3 tools/step2_cert_probe.py payload 1 1
+  python3 tools/step2_cert_probe.py scale:syn64x32_MDU_s2delete 0 0     (tests/golden/scale.json cases)
 """
 import os
 import sys
@@ -20,17 +21,31 @@ def main():
     from gpu_cases import build_args, fixing_bounds
     name, k, b = sys.argv[1], int(sys.argv[2]), int(sys.argv[3])
     iters = int(os.environ.get("ITERS", "200000"))
-    data, variant, step, kw = build_args(name, k)
+    if name.startswith("scale:"):
+        from scale_util import case_model_args, node_bounds, scale_cases
+        c = scale_cases()[name[6:]]
+        data, variant, step, kw = case_model_args(c)
+        m = LPModel(data, variant, step=step, max_batch=2, **kw)
+        lb = np.full((1, m.n_int), -np.inf)
+        ub = np.full((1, m.n_int), np.inf)
+        ref = c["root"].get("lp_objective")
+        if b > 0:
+            l, u = node_bounds(c, m.n_int)
+            lb[0], ub[0] = l[b - 1], u[b - 1]
+            ref = c["nodes"][b - 1].get("lp_objective")
+    else:
+        data, variant, step, kw = build_args(name, k)
+        m = LPModel(data, variant, step=step, max_batch=2, **kw)
+        ref = None
+        lb = np.full((1, m.n_int), -np.inf)
+        ub = np.full((1, m.n_int), np.inf)
     N, F = len(data.nodes), len(data.functions)
     nx = N * N * F
-    m = LPModel(data, variant, step=step, max_batch=2, **kw)
-    nodes = fixing_bounds(name, k, m.n_int, nx)
-    lb = np.full((1, m.n_int), -np.inf)
-    ub = np.full((1, m.n_int), np.inf)
-    ref = None
-    if b > 0:
-        l, u, ref = nodes[b - 1]
-        lb[0], ub[0] = l, u
+    if not name.startswith("scale:"):
+        nodes = fixing_bounds(name, k, m.n_int, nx)
+        if b > 0:
+            l, u, ref = nodes[b - 1]
+            lb[0], ub[0] = l, u
     r = m.solve([0], lb, ub, tol=5e-7, max_iters=iters)
     d = m.diag(0)
     print(f"{name} model {k} LP {b}: status {r['status'][0]} obj {r['obj'][0]:.10g} pobj {r['primal_obj'][0]:.10g} "
@@ -60,6 +75,9 @@ def main():
                         None if mf is None else mf[f, j], None if mt is None else mt[f, j], blb[f, j], bub[f, j],
                         v1, v2, vd1, vd2))
     out.sort(key=lambda t: -t[0])
+    print(f"  flow on placements with old = 0: {float(S[old == 0].sum()):.6g}; sum c {float(c.sum()):.6g}; "
+          f"sum old {float(old.sum()):.6g}; sum mf {0 if mf is None else float(mf.sum()):.6g}; "
+          f"sum mt {0 if mt is None else float(mt.sum()):.6g}")
     print("  worst (f, j): viol S c old mf mt box_lb box_ub | C1 C2 D1 D2")
     for t in out[:8]:
         print("   ", t[1:3], " ".join(f"{v:.7g}" if v is not None else "-" for v in t[3:10]), "|",
