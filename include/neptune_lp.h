@@ -16,8 +16,10 @@
  * Conventions.  Plain pointers and sizes only.  Every call returns NEP_OK (0) on success or a
  * negative NEP_ERR_*; nep_last_error() gives a thread-local message.  Host arrays are read during
  * the call only.  The library owns all device workspaces; one model serves `max_batch` LP slots
- * (B&B nodes) that can be warm-started from each other.  All device work of a model is ordered on
- * one HIP stream; the HIP context is created on first use (safe after fork()).
+ * (B&B nodes) that can be warm-started from each other.  A model's device work runs on its iteration
+ * stream (the caller's or its own) and one auxiliary stream of the highest priority (slot reads, warm-start
+ * copies, submits), ordered by events: a slot iterates only after its submit's initialisation; the HIP
+ * context is created on first use (safe after fork()).
  *
  * Integer-variable vector ("z_int"), in the reference's variable-creation order minus x:
  *   step 1: c[F*N] (f-major), then n[N] (MinUtilization / MinDelayAndUtilization only)
@@ -226,7 +228,14 @@ int nep_debug_presolve(const nep_model_desc *desc, int32_t n, const double *lb_i
                        int32_t *ok_full, int32_t *ok_node, double *box_full, double *box_node);
 void nep_reset_stats(void *model);
 
-/* Branch-and-bound rounding heuristic (host only, no model; core/engine/bnb.py): one branching
+/* API 8: the routing state (x and its projection thresholds) of a finished slot of ANOTHER model of the same
+ * instance and row layout (e.g. a NEP_RELAX_FACILITY branching node) copied into a finished slot of this one —
+ * a leaf's warm start from its branching node's routing; the slot's other state (small variables, duals) is
+ * left as it is (typically the root's, nep_lp_copy_state); the next submit with warm_start iterates from it.
+ * NEP_ERR_ARG when the row layouts differ.  Replaces SCIP's LP warm start across its own node LPs. */
+int nep_lp_copy_routing(void *dst_model, int32_t dst_slot, void *src_model, int32_t src_slot);
+
+/* API 8: branch-and-bound rounding heuristic (host only, no model; core/engine/bnb.py): one branching
  * node's LP -> a leaf fixing every c (and n).  c_fix [F*N] / n_fix [N] (n_fix NULL: no n): -1 free, 0 / 1
  * fixed by the node; flow [F*N] the node's flows, zc [F*N] its c (NULL: 0).  Fixed-open c first, then the free
  * c with zc >= 1/2 (largest first), then (by_flow) the free (f, j) with flow > flow_threshold (largest
