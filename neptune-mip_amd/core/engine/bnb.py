@@ -152,7 +152,7 @@ class BranchAndBound:
                  seed_leaves=None, integer_bound=None, improve=None, repair=None, node_bound_res=1e-2,
                  retry_res=math.inf, unit_flow_leaves=True, node_max_iters=None, bound_lp=None, bound_gap=1e-4,
                  trace=None, rebalance_every=8, primal=None, primal_every=0, leaf_warm_incumbent=False,
-                 leaf_routing_warm=False):
+                 leaf_routing_warm=False, root_check_every=64):
         self.lp = lp
         self.two = bound_lp is not None
         self.N, self.F = lp.N, lp.F
@@ -189,6 +189,10 @@ class BranchAndBound:
         # branching node it was rounded from (nep_lp_copy_routing) while that node's slot still holds it.
         # Off by default: 256x128 / 512x256, 20 s, measured no better
         self.leaf_routing_warm = bool(leaf_routing_warm)
+        # the roots (which run alone on their model, tens of thousands of iterations) take a certificate
+        # check every root_check_every iterations instead of check_every: a 1-slot certificate launch costs
+        # ~3 plain ones (bench.py's root uses 64 as well)
+        self.root_check_every = int(root_check_every) if root_check_every else check_every
         self.root_slot = lp.max_batch - 1
         self.inc_slot = lp.max_batch - 2
         self.tol, self.gap, self.max_iters = tol, gap, max_iters
@@ -329,7 +333,8 @@ class BranchAndBound:
                       else (self.node_max_iters if node.kind == NODE else self.max_iters))
             # (the bound model's root is a branching node like the others: it stops once its bound converged)
             bres = self.node_bound_res if (node.kind == NODE and (eng.root_ready or self.two)) else 0.0
-            groups.setdefault((eng.name, warm, budget, bres), (eng, []))[1].append((slot, node))
+            ce = self.root_check_every if (node.kind == REFROOT or not eng.root_ready) else self.check_every
+            groups.setdefault((eng.name, warm, budget, bres, ce), (eng, []))[1].append((slot, node))
             node.nid = next(self.nid_seq)
             if self.trace is not None:
                 self.trace.append(self._trace_entry(eng, node, src if warm else None, budget, bres, cutoff))
@@ -354,7 +359,7 @@ class BranchAndBound:
                 eng.lp.copy_state(src, dst)
         if not done_cross:
             self._copy_cross(cross)
-        for (_, warm, budget, bres), (eng, its) in groups.items():
+        for (_, warm, budget, bres, ce), (eng, its) in groups.items():
             n_int = eng.lp.n_int
             slots = np.array([s for s, _ in its], np.int32)
             lb = np.full((len(its), n_int), -np.inf)
@@ -364,7 +369,7 @@ class BranchAndBound:
                 ub[b, node.idx] = node.val
             gap_tol = self.bound_gap if (self.two and eng is self.B) else 0.0
             st = eng.lp.submit(slots, lb, ub, tol=self.tol, cutoff=cutoff if math.isfinite(cutoff) else math.inf,
-                               max_iters=budget, check_every=self.check_every, warm_start=warm, bound_res=bres,
+                               max_iters=budget, check_every=ce, warm_start=warm, bound_res=bres,
                                gap_tol=gap_tol)
             for b, (slot, node) in enumerate(its):
                 eng.gen[slot] += 1
