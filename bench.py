@@ -80,6 +80,9 @@ def parse(argv=None):
     ap.add_argument("--native-steps", type=int, default=6,
                     help="with the replay stream: steps of the native-model replay timed after it (each recorded "
                          "box on the model the product ran it on; 0 = skip)")
+    ap.add_argument("--warm-ancestors", action="store_true",
+                    help="replay: a node whose parent's state is gone starts from its closest resident ancestor's "
+                         "(default: the root's, as the product B&B does)")
     ap.add_argument("--children-steps", type=int, default=24,
                     help="with the replay stream: steps of the children stream timed after it (secondary figure)")
     ap.add_argument("--cpu-budget", type=float, default=150.0,
@@ -323,6 +326,8 @@ class ReplayStream:
     def __init__(self, models, a, rank, world, trace, native=False):
         self.models, self.a, self.native = models, a, native
         self.lps = [e for e in trace["lps"] if e["parent"] is not None]
+        self.parent_of = {e["id"]: e["parent"] for e in trace["lps"]}
+        self.ancestors = getattr(a, "warm_ancestors", False)
         self.pos, self.stride = rank, world
         self.counter = 0
         self.done = []          # (status, obj, primal_obj, iters) per completed node
@@ -368,6 +373,13 @@ class ReplayStream:
             if old is not None:
                 self.where.pop((name, old), None)
             src = root
+            if pkey not in self.where and self.ancestors:
+                # (--warm-ancestors: the closest ancestor whose final state a slot still holds)
+                p = self.parent_of.get(e["parent"])
+                while p is not None and (name, (rep, p)) not in self.where:
+                    p = self.parent_of.get(p)
+                if p is not None:
+                    pkey = (name, (rep, p))
             if pkey in self.where:
                 src = self.where[pkey]
                 self.warm_parent += 1

@@ -14,3 +14,5 @@ for kn in '{"root_check_every": 64}' '{"root_check_every": 12}'; do
   rc=$?; echo "bnb [$kn] rc=$rc"; grep "two\|mix" "$O/bnb_rce$tag.log" | cut -c1-300
   [ $rc -eq 0 ] || exit $rc
 done
+timeout -k 10 300 python -u bench.py --steps 6 --warm-ancestors --native-steps 0 --children-steps 0 --bnb-seconds 0 --cpu-budget 0 > "$O/bench_anc.json" 2> "$O/bench_anc.err"
+rc=$?; echo "bench ancestors rc=$rc"; python3 -c "import json;d=json.load(open('$O/bench_anc.json'));print(d['value'], d['lp']['certified'], d['lp']['completed'], d['lp']['mean_iters'], d['lp']['warm_from_parent_rank0'])"
