@@ -131,16 +131,6 @@ def _full_size_check(payload, variant, fixings=0, seed=0):
         m.close()
 
 
-def test_full_size_1024x512_synthetic_root_and_children():
-    """BASELINE config 5's shape (1024x512) with a workload: the §8(d) generator (seed 0) instead of the Alibaba
-    trace (W == 0, whose step-1 roots certify at iteration 1 — round-3 VERDICT): root + 2 warm children,
-    certified and re-checked on the host in fp64 like the 512x256 case."""
-    from core.utils.synthetic import synthetic_payload
-    rr = _full_size_check(synthetic_payload(1024, 512, seed=0), "MinDelayAndUtilization", fixings=2)
-    print("1024x512 root iterations", rr["iters"][0], "obj", rr["obj"][0])
-    assert int(rr["iters"][0]) > 1
-
-
 def test_full_size_512x256_root_and_children():
     """BASELINE config 4's instance (512x256, §8(d) generator, seed 0): root + 4 warm children."""
     from core.utils.synthetic import synthetic_payload
