@@ -114,6 +114,13 @@ def load_library(path=None):
                                    ctypes.c_double, _dp, _dp]
     lib.nep_last_error.restype = ctypes.c_char_p
     lib.nep_api_version.restype = ctypes.c_int
+    # array arguments travel as plain addresses (_ptr: the array's data pointer as an int): ctypes' typed
+    # pointer casts cost ~2 us each, ~10 % of the B&B's host time at 64x32 (tools/bnb_profile.py)
+    scalar_ptrs = tuple(ctypes.POINTER(t) for t in (ctypes.c_double, ctypes.c_float, ctypes.c_int32, ctypes.c_int64))
+    for name in EXPORTS:
+        fn = getattr(lib, name)
+        if fn.argtypes:
+            fn.argtypes = [ctypes.c_void_p if t in scalar_ptrs else t for t in fn.argtypes]
     if lib.nep_api_version() != API_VERSION:
         raise EngineUnavailable(f"{p}: API version {lib.nep_api_version()} != {API_VERSION} (rebuild the engine)")
     if path is None:
@@ -143,7 +150,9 @@ def round_leaf(c_fix, n_fix, flow, zc, fn_mem, node_mem, by_flow, flow_threshold
 
 
 def _ptr(a, ctype=ctypes.c_double):
-    return None if a is None else a.ctypes.data_as(ctypes.POINTER(ctype))
+    """The data address of a C-contiguous numpy array (the library's array arguments are void*), or None.
+    (ctype documents the element type the C side reads.)"""
+    return None if a is None else a.ctypes.data
 
 
 def _check(lib, rc, what):
@@ -167,9 +176,11 @@ def _arrays(data, N, F):
 
 
 def _desc(k, N, F, variant, step, alpha, soften, max_score, prev_delay, budget, relaxation=RELAX_REFERENCE):
+    def dp(a):   # (structure fields keep their typed pointers)
+        return a.ctypes.data_as(_dp)
     return ModelDesc(N, F, variant, step, float(alpha), float(soften), float(max_score), float(prev_delay), 1e6,
-                     1e-6, _ptr(k["delay"]), _ptr(k["workload"]), _ptr(k["cpr"]), _ptr(k["fmem"]), _ptr(k["nmem"]),
-                     _ptr(k["ncores"]), _ptr(k["ncost"]), float(budget), _ptr(k["maxd"]), _ptr(k["old"]),
+                     1e-6, dp(k["delay"]), dp(k["workload"]), dp(k["cpr"]), dp(k["fmem"]), dp(k["nmem"]),
+                     dp(k["ncores"]), dp(k["ncost"]), float(budget), dp(k["maxd"]), dp(k["old"]),
                      int(relaxation))
 
 

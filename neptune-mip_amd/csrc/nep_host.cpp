@@ -1239,9 +1239,12 @@ int submit(Model &m, int n, const int32_t *slots, const double *lbi, const doubl
     HIPCHK(hipMemcpyAsync(m.d_chg_lb, hl, cl.size() * sizeof(double), hipMemcpyHostToDevice, m.aux));
     HIPCHK(hipMemcpyAsync(m.d_chg_ub, hu, cu.size() * sizeof(double), hipMemcpyHostToDevice, m.aux));
   }
+  HIPCHK(hipMemcpyAsync(m.d_exact, he, nf * sizeof(int32_t), hipMemcpyHostToDevice, m.aux));
+  // the staging is free again once these copies are done (the next submit waits for this event only, not
+  // for the initialisation kernels below)
+  HIPCHK(hipEventRecord(m.ev_sub, m.aux));
   HIPCHK(launch_node_bounds(v, m.d_new, nf, m.d_base_lb, m.d_base_ub, m.d_base_mask, m.d_chg_off, m.d_chg_idx,
                             m.d_chg_lb, m.d_chg_ub, max_chg, m.aux));
-  HIPCHK(hipMemcpyAsync(m.d_exact, he, nf * sizeof(int32_t), hipMemcpyHostToDevice, m.aux));
   HIPCHK(launch_init_slot(v, m.d_new, m.d_exact, nf, o.warm_start != 0, m.eta, m.omega0, m.aux));
   HIPCHK(launch_x_pass(v, m.d_new, nf, false, true, true, true, 0, m.aux));
   HIPCHK(launch_node_pass(v, m.d_new, nf, false, true, true, true, 0, m.aux));
@@ -1250,7 +1253,6 @@ int submit(Model &m, int n, const int32_t *slots, const double *lbi, const doubl
   HIPCHK(hipEventRecord(m.ev_aux, m.aux));
   HIPCHK(hipStreamWaitEvent(m.stream, m.ev_aux, 0));
   m.act.insert(m.act.end(), fresh.begin(), fresh.end());   // (d_slots follows at the next launch_block)
-  HIPCHK(hipEventRecord(m.ev_sub, m.aux));
   m.sub_pending = true;
   return NEP_OK;
 }
