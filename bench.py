@@ -66,8 +66,9 @@ def parse(argv=None):
     ap.add_argument("--warm-omega-floor", type=float, default=0.0,
                     help="warm-start primal-weight floor x the parent's (0: engine default)")
     ap.add_argument("--root-max-iters", type=int, default=400000)
-    ap.add_argument("--check-every", type=int, default=12,
-                    help="PDHG iterations per certificate check (node LPs; 8/12/16/24 measured, DESIGN.md §6)")
+    ap.add_argument("--check-every", type=int, default=48,
+                    help="PDHG iterations per certificate check of the timed streams (replay: 12 / 24 / 48 -> 5.70 / "
+                         "6.37 / 7.06 certified LP/s, DESIGN.md §6); the bnb section keeps the product's default")
     ap.add_argument("--root-check-every", type=int, default=64)
     ap.add_argument("--root-gap-tol", type=float, default=0.0,
                     help="after the root certifies at --tol, continue it (warm, same slot) until its objective gap "
@@ -277,8 +278,7 @@ def bnb_section(a, rank, world, dev, N, F, seconds):
     m = LPModel(data, "MinDelayAndUtilization", step=1, alpha=alpha, max_batch=a.batch + 2)
     bm = st1.bound_model(data, a.batch + 1)
     comm = TorchComm(device=dev) if world > 1 else LocalComm()
-    bnb = st1.branch_and_bound(m, bm, time_limit=seconds, comm=comm, check_every=a.check_every,
-                               root_max_iters=a.root_max_iters)
+    bnb = st1.branch_and_bound(m, bm, time_limit=seconds, comm=comm, root_max_iters=a.root_max_iters)
     m.reset_stats()
     t0 = time.perf_counter()
     res = bnb.solve()
@@ -540,7 +540,7 @@ def main():
             bm = LPModel(data, "MinDelayAndUtilization", step=1, alpha=alpha, max_batch=B + 1,
                          relaxation=RELAX_FACILITY)
             t_fr = time.perf_counter()
-            fr = bm.solve([root], tol=a.tol, max_iters=a.root_max_iters, check_every=a.check_every,
+            fr = bm.solve([root], tol=a.tol, max_iters=a.root_max_iters, check_every=a.root_check_every,
                         bound_res=1e-2, gap_tol=1e-4)
             fac_root = {"status": int(fr["status"][0]), "obj": float(fr["obj"][0]), "iters": int(fr["iters"][0]),
                         "seconds": time.perf_counter() - t_fr}
