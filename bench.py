@@ -60,9 +60,14 @@ def parse(argv=None):
     ap.add_argument("--fix", type=int, default=2, help="c[f,j] fixings per node LP")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--tol", type=float, default=1e-6)
-    ap.add_argument("--max-iters", type=int, default=4096,
-                    help="per node LP (a B&B node-LP iteration limit; nodes that reach it keep a valid "
-                         "Lagrangian bound but are not counted as LP relaxations)")
+    ap.add_argument("--max-iters", type=int, default=8192,
+                    help="per node LP of the timed streams (a B&B node-LP iteration limit; nodes that reach it keep "
+                         "a valid Lagrangian bound but are not counted as LP relaxations).  Replay, check every 48: "
+                         "2048 / 4096 / 8192 / 12288 / 16384 / 32768 -> 5.96 / 7.07 / 8.23 / 8.03 / 7.53 / 6.34 "
+                         "certified LP/s (DESIGN.md §6)")
+    ap.add_argument("--bnb-max-iters", type=int, default=4096,
+                    help="the bnb section's node-LP limit (leaves; branching nodes a quarter of it), as the replay "
+                         "trace was recorded")
     ap.add_argument("--warm-omega-floor", type=float, default=0.0,
                     help="warm-start primal-weight floor x the parent's (0: engine default)")
     ap.add_argument("--root-max-iters", type=int, default=400000)
@@ -273,7 +278,7 @@ def bnb_section(a, rank, world, dev, N, F, seconds):
     data = data_to_solver_input(p, with_db=False)
     alpha = p["solver"]["args"]["alpha"]
     st1 = NeptuneStep1CPUMinDelayAndUtilization(alpha=alpha, verbose=False, batch=a.batch, lp_tol=a.tol,
-                                                lp_max_iters=a.max_iters)
+                                                lp_max_iters=a.bnb_max_iters)
     st1.load_data(data)
     m = LPModel(data, "MinDelayAndUtilization", step=1, alpha=alpha, max_batch=a.batch + 2)
     bm = st1.bound_model(data, a.batch + 1)
