@@ -75,6 +75,9 @@ def parse(argv=None):
                     help="PDHG iterations per certificate check of the timed streams (replay: 12 / 24 / 48 -> 5.70 / "
                          "6.37 / 7.06 certified LP/s, DESIGN.md §6); the bnb section keeps the product's default")
     ap.add_argument("--root-check-every", type=int, default=64)
+    ap.add_argument("--root-polish-after", type=int, default=0,
+                    help="primal feasibility polishing of the (cold) root after this many iterations (0: the engine's "
+                         "default for cold LPs, none; DESIGN.md §4 'Polishing')")
     ap.add_argument("--root-gap-tol", type=float, default=0.0,
                     help="after the root certifies at --tol, continue it (warm, same slot) until its objective gap "
                          "is below this: the children warm-start from a well-converged root (0 = off)")
@@ -510,7 +513,8 @@ def main():
         f"built in {time.perf_counter() - t_build:.1f}s")
     P = m.info.x_entries
     t_root = time.perf_counter()
-    rr = m.solve([root], tol=a.tol, max_iters=a.root_max_iters, check_every=a.root_check_every)
+    rr = m.solve([root], tol=a.tol, max_iters=a.root_max_iters, check_every=a.root_check_every,
+                 polish_after=float(a.root_polish_after))
     root_obj, root_status, root_iters = float(rr["obj"][0]), int(rr["status"][0]), int(rr["iters"][0])
     root_seconds = time.perf_counter() - t_root
     log(f"rank {rank}: root LP status {root_status} obj {root_obj:.10g} after {root_iters} iterations "
