@@ -151,7 +151,7 @@ class BranchAndBound:
                  warm=True, root_max_iters=200000, check_every=12, polish_tol=1e-8, polish_iters=20000,
                  seed_leaves=None, integer_bound=None, improve=None, repair=None, node_bound_res=1e-2,
                  retry_res=math.inf, unit_flow_leaves=True, node_max_iters=None, bound_lp=None, bound_gap=1e-4,
-                 trace=None, rebalance_every=8, primal=None, primal_every=0, leaf_warm_incumbent=False,
+                 trace=None, rebalance_every=8, primal=None, primal_every=0,
                  leaf_routing_warm=False, root_check_every=64):
         self.lp = lp
         self.two = bound_lp is not None
@@ -182,9 +182,6 @@ class BranchAndBound:
         # the greedy costs ~2 s per call at 512x256)
         self.primal = primal
         self.primal_every = max(0, int(primal_every))
-        # leaves (and their retries) warm-start from the incumbent leaf's final state once there is one
-        # (its routing and CPU prices sit next to the new leaf's) instead of the reference root's
-        self.leaf_warm_incumbent = bool(leaf_warm_incumbent)
         # two models: a rounding leaf starts from the reference root's state with the routing x of the
         # branching node it was rounded from (nep_lp_copy_routing) while that node's slot still holds it.
         # Off by default: 256x128 / 512x256, 20 s, measured no better
@@ -315,9 +312,6 @@ class BranchAndBound:
             warm, src = False, None
             if self.warm and eng.root_ready:
                 src = eng.root_slot
-                if (self.leaf_warm_incumbent and node.kind in (LEAF, RETRY) and eng is self.L
-                        and self.res.incumbent_slot == eng.inc_slot):
-                    src = eng.inc_slot
                 if node.parent is not None:
                     pe, ps, pg = node.parent[:3]
                     if pe is eng and eng.gen[ps] == pg:
