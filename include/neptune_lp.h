@@ -163,6 +163,9 @@ int nep_lp_active(void *model);
  * certified slot (NEP_LP_OPTIMAL) z_int is the certificate's repaired point — the primal solution
  * whose objective primal_obj is and whose rows the certificate checked — else the PDHG iterate. */
 int nep_lp_get_solution(void *model, int32_t slot, double *z_int, float *x_dense);
+/* API 8: z_int of n finished slots at once (z_out [n][n_int], each as nep_lp_get_solution's): one device
+ * round trip for all the branching nodes an advance returned. */
+int nep_lp_get_solutions(void *model, int32_t n, const int32_t *slots, double *z_out);
 /* aggregated routing rows (host float, R*N) and the row map (row_f, row_src; src = -1: pooled
  * zero-workload sources of function f, each routed identically). */
 int nep_lp_get_rows(void *model, int32_t slot, float *xbar, int32_t *row_f, int32_t *row_src);

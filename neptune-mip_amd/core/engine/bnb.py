@@ -376,9 +376,9 @@ class BranchAndBound:
                     self.inflight[(eng.name, slot)] = node
                     eng.inflight += 1
 
-    def _finish(self, eng, slot, node, st, obj, pobj, iters, inc, flow=None):
+    def _finish(self, eng, slot, node, st, obj, pobj, iters, inc, pre=None):
         """Process one finished node LP (of engine `eng`); returns the (possibly improved) incumbent value.
-        flow: its F x N flows when the caller already read them (one device read per block, _prefetch)."""
+        pre: (flows F x N, z_int) when the caller already read them (one device read per block, _prefetch)."""
         res = self.res
         lp = eng.lp
         eng.inflight -= 1
@@ -455,10 +455,12 @@ class BranchAndBound:
             eng.free.append(slot)
             return inc
         res.nodes += 1
-        if flow is None:
+        if pre is not None:
+            flow, z = pre
+        else:
             flow = lp.flows([slot])[0]
+            z, _ = lp.solution(slot, dense_x=False)
         me = (eng, slot, eng.gen[slot], node.nid)
-        z, _ = lp.solution(slot, dense_x=False)
         for by_flow, min_flow in self.round_modes:
             leaf = self._round(node, flow, z[self.c0:self.c1], by_flow, min_flow)
             if leaf is not None:
@@ -519,8 +521,8 @@ class BranchAndBound:
         return res.objective
 
     def _prefetch(self, eng, r, inc):
-        """The flows of every branching node in an advance result that will branch (not pruned, not
-        infeasible / cut off), read in ONE device call: {slot: flow [F, N]}."""
+        """The flows and integer vectors of every branching node in an advance result that will branch (not
+        pruned, not infeasible / cut off), read in one device call each: {slot: (flow [F, N], z)}."""
         want = []
         for i, slot in enumerate(r["slots"].tolist()):
             node = self.inflight.get((eng.name, slot))
@@ -533,7 +535,8 @@ class BranchAndBound:
         if not want:
             return {}
         fl = eng.lp.flows(want)
-        return {s: fl[k] for k, s in enumerate(want)}
+        zs = eng.lp.solutions(want)
+        return {s: (fl[k], zs[k]) for k, s in enumerate(want)}
 
     def _frontier_hash(self):
         """crc32 of the (sorted) open frontier: bounds, depths, fixings — identical on every rank at the split."""

@@ -65,7 +65,8 @@ EXPORTS = ("nep_model_create", "nep_model_destroy", "nep_model_get_info", "nep_l
            "nep_lp_get_flows_split",
            "nep_last_error", "nep_api_version", "nep_lp_get_diag", "nep_debug_build", "nep_debug_state",
            "nep_debug_presolve", "nep_lp_set_params", "nep_lp_get_flows", "nep_lp_routing_entries",
-           "nep_lp_allocation_entries", "nep_lp_score_check", "nep_round_leaf", "nep_lp_copy_routing")
+           "nep_lp_allocation_entries", "nep_lp_score_check", "nep_round_leaf", "nep_lp_copy_routing",
+           "nep_lp_get_solutions")
 SCORE_FIELDS = ("network_delay", "nodes_used", "node_cost", "bad_c_x", "bad_memory", "bad_handle", "bad_cpu",
                 "bad_n_c", "bad_budget", "handle_maxdev", "cpu_maxexcess")
 
@@ -97,6 +98,7 @@ def load_library(path=None):
                                     ctypes.POINTER(i32)]
     lib.nep_lp_copy_state.argtypes = [vp, i32, i32]
     lib.nep_lp_copy_routing.argtypes = [vp, i32, vp, i32]
+    lib.nep_lp_get_solutions.argtypes = [vp, i32, pi32, _dp]
     lib.nep_get_stats.argtypes = [vp, ctypes.POINTER(Stats)]
     lib.nep_reset_stats.argtypes = [vp]
     lib.nep_reset_stats.restype = None
@@ -333,6 +335,14 @@ class LPModel:
                                                         _ptr(x, ctypes.c_float) if dense_x else None),
                "nep_lp_get_solution")
         return z, x
+
+    def solutions(self, slots):
+        """z_int of several finished slots, [len(slots), n_int], in one device round trip (nep_lp_get_solutions)."""
+        slots = np.ascontiguousarray(np.asarray(slots, dtype=np.int32).reshape(-1))
+        out = np.zeros((len(slots), self.n_int))
+        _check(self._lib, self._lib.nep_lp_get_solutions(self._h, len(slots), _ptr(slots, ctypes.c_int32), _ptr(out)),
+               "nep_lp_get_solutions")
+        return out
 
     def rows(self, slot):
         R = self.info.n_rows

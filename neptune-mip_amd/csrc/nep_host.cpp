@@ -109,7 +109,6 @@ struct Model {
   std::vector<uint8_t> allow;        // scratch [F*N]
   std::vector<uint8_t> allow2;       // scratch [F*N] (CPU cover test)
   bool x_cost_free = true;     // no routing entry carries objective cost (step 2; W == 0)
-  int32_t *d_exact = nullptr;  // per submitted node: the box fixes the objective (Ctrl::exact)
   // node presolve as a sparse change of the base box (presolve_setup / presolve_node)
   bool base_ok = false;
   std::vector<double> base_lb, base_ub, base_amin, base_amax;
@@ -137,8 +136,10 @@ struct Model {
   int32_t *d_new = nullptr;     // slots being initialised by nep_lp_submit
   double *d_base_lb = nullptr, *d_base_ub = nullptr;
   uint8_t *d_base_mask = nullptr;
-  int32_t *d_chg_off = nullptr, *d_chg_idx = nullptr;   // packed bound changes of the nodes being submitted
-  double *d_chg_lb = nullptr, *d_chg_ub = nullptr;
+  // a submit's uploads, one copy each: [slots | change offsets | change indices | exact flags] and
+  // [change lower bounds | change upper bounds] (capacity: every integer variable of every slot)
+  int32_t *d_sub_i = nullptr;
+  double *d_sub_d = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   nep_stats stats{};
   // scratch of the auxiliary kernels (nep_aux.hip), allocated on first use
@@ -168,6 +169,7 @@ struct Model {
   std::vector<int32_t> launched;
   Ctrl *h_ctrl = nullptr;
   float *h_flows = nullptr;     // pinned staging of nep_lp_get_flows(_split): [2][max_batch][F*N] + slots
+  double *h_sols = nullptr;     // pinned staging of nep_lp_get_solutions: [max_batch][n_int] + statuses
   // pinned staging of nep_lp_submit's uploads (slots, change offsets / indices / bounds, exact flags): the
   // call returns without waiting for them; the next submit waits on ev_sub before rewriting the staging
   int32_t *h_sub_i = nullptr;
@@ -181,6 +183,7 @@ struct Model {
     if (h_ctrl) (void)hipHostFree(h_ctrl);
     if (h_act) (void)hipHostFree(h_act);
     if (h_flows) (void)hipHostFree(h_flows);
+    if (h_sols) (void)hipHostFree(h_sols);
     if (h_sub_i) (void)hipHostFree(h_sub_i);
     if (h_sub_d) (void)hipHostFree(h_sub_d);
     if (ev_sub) (void)hipEventDestroy(ev_sub);
@@ -777,7 +780,6 @@ int setup_dense(Model &m, const nep_model_desc &d) {
   v.prm = m.d_prm;
   if ((rc = dalloc(m, &m.d_slots, (size_t)B))) return rc;
   if ((rc = dalloc(m, &m.d_new, (size_t)B))) return rc;
-  if ((rc = dalloc(m, &m.d_exact, (size_t)B))) return rc;
   {
     const double *p = nullptr;
     if ((rc = upload(m, &p, m.base_lb))) return rc;
@@ -788,10 +790,8 @@ int setup_dense(Model &m, const nep_model_desc &d) {
     if ((rc = upload(m, &q, m.base_mask))) return rc;
     m.d_base_mask = const_cast<uint8_t *>(q);
   }
-  if ((rc = dalloc(m, &m.d_chg_off, (size_t)B + 1))) return rc;
-  if ((rc = dalloc(m, &m.d_chg_idx, (size_t)B * v.sint))) return rc;
-  if ((rc = dalloc(m, &m.d_chg_lb, (size_t)B * v.sint))) return rc;
-  if ((rc = dalloc(m, &m.d_chg_ub, (size_t)B * v.sint))) return rc;
+  if ((rc = dalloc(m, &m.d_sub_i, (size_t)3 * B + 1 + (size_t)B * v.sint))) return rc;
+  if ((rc = dalloc(m, &m.d_sub_d, (size_t)2 * B * v.sint))) return rc;
   HIPCHK(hipMemsetAsync(v.ctrl, 0, sizeof(Ctrl) * B, m.stream));
   HIPCHK(hipMemsetAsync(v.x, 0, sizeof(float) * B * v.sx, m.stream));
   HIPCHK(hipMemsetAsync(v.xa, 0, sizeof(float) * B * v.sx, m.stream));
@@ -1232,23 +1232,19 @@ int submit(Model &m, int n, const int32_t *slots, const double *lbi, const doubl
   std::copy(exact.begin(), exact.end(), he);
   std::copy(cl.begin(), cl.end(), hl);
   std::copy(cu.begin(), cu.end(), hu);
-  HIPCHK(hipMemcpyAsync(m.d_new, hf, nf * sizeof(int32_t), hipMemcpyHostToDevice, m.aux));
-  HIPCHK(hipMemcpyAsync(m.d_chg_off, ho, off.size() * sizeof(int32_t), hipMemcpyHostToDevice, m.aux));
-  if (!ci.empty()) {
-    HIPCHK(hipMemcpyAsync(m.d_chg_idx, hc, ci.size() * sizeof(int32_t), hipMemcpyHostToDevice, m.aux));
-    HIPCHK(hipMemcpyAsync(m.d_chg_lb, hl, cl.size() * sizeof(double), hipMemcpyHostToDevice, m.aux));
-    HIPCHK(hipMemcpyAsync(m.d_chg_ub, hu, cu.size() * sizeof(double), hipMemcpyHostToDevice, m.aux));
-  }
-  HIPCHK(hipMemcpyAsync(m.d_exact, he, nf * sizeof(int32_t), hipMemcpyHostToDevice, m.aux));
+  HIPCHK(hipMemcpyAsync(m.d_sub_i, m.h_sub_i, need_i * sizeof(int32_t), hipMemcpyHostToDevice, m.aux));
+  if (need_d) HIPCHK(hipMemcpyAsync(m.d_sub_d, m.h_sub_d, need_d * sizeof(double), hipMemcpyHostToDevice, m.aux));
+  int32_t *dn = m.d_sub_i, *doff = dn + nf, *didx = doff + off.size(), *dex = didx + ci.size();
+  double *dlb = m.d_sub_d, *dub = dlb + cl.size();
   // the staging is free again once these copies are done (the next submit waits for this event only, not
   // for the initialisation kernels below)
   HIPCHK(hipEventRecord(m.ev_sub, m.aux));
-  HIPCHK(launch_node_bounds(v, m.d_new, nf, m.d_base_lb, m.d_base_ub, m.d_base_mask, m.d_chg_off, m.d_chg_idx,
-                            m.d_chg_lb, m.d_chg_ub, max_chg, m.aux));
-  HIPCHK(launch_init_slot(v, m.d_new, m.d_exact, nf, o.warm_start != 0, m.eta, m.omega0, m.aux));
-  HIPCHK(launch_x_pass(v, m.d_new, nf, false, true, true, true, 0, m.aux));
-  HIPCHK(launch_node_pass(v, m.d_new, nf, false, true, true, true, 0, m.aux));
-  HIPCHK(launch_scalar_pass(v, m.d_new, nf, false, true, true, true, 0, o.check_every, m.aux));
+  HIPCHK(launch_node_bounds(v, dn, nf, m.d_base_lb, m.d_base_ub, m.d_base_mask, doff, didx, dlb, dub, max_chg,
+                            m.aux));
+  HIPCHK(launch_init_slot(v, dn, dex, nf, o.warm_start != 0, m.eta, m.omega0, m.aux));
+  HIPCHK(launch_x_pass(v, dn, nf, false, true, true, true, 0, m.aux));
+  HIPCHK(launch_node_pass(v, dn, nf, false, true, true, true, 0, m.aux));
+  HIPCHK(launch_scalar_pass(v, dn, nf, false, true, true, true, 0, o.check_every, m.aux));
   // the new slots join the block after the one in flight: `stream` waits for their initialisation
   HIPCHK(hipEventRecord(m.ev_aux, m.aux));
   HIPCHK(hipStreamWaitEvent(m.stream, m.ev_aux, 0));
@@ -1631,6 +1627,35 @@ int nep_lp_advance(void *model, int32_t min_done, int32_t *n_done, int32_t *done
 int nep_lp_active(void *model) {
   if (!model) return fail(NEP_ERR_ARG, "null model");
   return (int)static_cast<Model *>(model)->act.size();
+}
+
+int nep_lp_get_solutions(void *model, int32_t n, const int32_t *slots, double *z_out) {
+  if (!model || (n > 0 && (!slots || !z_out))) return fail(NEP_ERR_ARG, "null argument");
+  Model &m = *static_cast<Model *>(model);
+  if (n <= 0) return NEP_OK;
+  if (n > m.max_batch) return fail(NEP_ERR_ARG, "n > max_batch");
+  for (int b = 0; b < n; ++b) {
+    if (slots[b] < 0 || slots[b] >= m.max_batch) return fail(NEP_ERR_ARG, "slot out of range");
+    if (m.busy[slots[b]]) return fail(NEP_ERR_STATE, "slot is still iterating");
+  }
+  const size_t ni = (size_t)m.il.n_int;
+  if (!m.h_sols) {
+    void *hp = nullptr;
+    if (hipHostMalloc(&hp, sizeof(double) * m.max_batch * (ni + 1)) != hipSuccess)
+      return fail(NEP_ERR_NOMEM, "hipHostMalloc (solutions)");
+    m.h_sols = static_cast<double *>(hp);
+  }
+  int32_t *hst = reinterpret_cast<int32_t *>(m.h_sols + (size_t)m.max_batch * ni);
+  for (int b = 0; b < n; ++b)
+    HIPCHK(hipMemcpyAsync(hst + b, &m.v.ctrl[slots[b]].status, sizeof(int32_t), hipMemcpyDeviceToHost, m.aux));
+  HIPCHK(hipStreamSynchronize(m.aux));
+  for (int b = 0; b < n; ++b) {   // (the certified point for a certified LP, else the iterate: solution_z)
+    const double *z = (hst[b] == NEP_LP_OPTIMAL ? m.v.zr : m.v.zi) + (size_t)slots[b] * m.v.sint;
+    HIPCHK(hipMemcpyAsync(m.h_sols + b * ni, z, ni * sizeof(double), hipMemcpyDeviceToHost, m.aux));
+  }
+  HIPCHK(hipStreamSynchronize(m.aux));
+  std::memcpy(z_out, m.h_sols, sizeof(double) * n * ni);
+  return NEP_OK;
 }
 
 int nep_lp_get_solution(void *model, int32_t slot, double *z_int, float *x_dense) {

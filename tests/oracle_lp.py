@@ -146,6 +146,9 @@ class OracleLP:
         xd = x[:self.nx].reshape(self.F, self.N, self.N).transpose(1, 0, 2).astype(np.float32) if dense_x else None
         return z, xd
 
+    def solutions(self, slots):
+        return np.array([self.solution(s, dense_x=False)[0] for s in np.asarray(slots).reshape(-1)])
+
     def routing(self, slot):
         from core.engine.routing import SparseRouting
         return SparseRouting.from_dense(self.solution(slot, dense_x=True)[1])

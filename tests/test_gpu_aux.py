@@ -92,3 +92,17 @@ def test_flows_entries_and_checks(name, k):
                 assert sc["nodes_used"] == int((n != 0).sum())
     finally:
         m.close()
+
+
+@pytest.mark.parametrize("name,k", CASES[:2])
+def test_batched_solutions_equal_single_reads(name, k):
+    """nep_lp_get_solutions (API 8, the B&B's one read per advance) returns, slot for slot, what
+    nep_lp_get_solution returns: the certified repaired point of a certified LP, else the iterate."""
+    m, data, variant, r = _solved(name, k)
+    try:
+        zs = m.solutions([2, 0, 1])
+        for row, slot in zip(zs, (2, 0, 1)):
+            z, _ = m.solution(slot, dense_x=False)
+            assert np.array_equal(row, z), slot
+    finally:
+        m.close()
