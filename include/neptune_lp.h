@@ -250,6 +250,11 @@ int nep_lp_copy_routing(void *dst_model, int32_t dst_slot, void *src_model, int3
 int nep_round_leaf(int32_t F, int32_t N, const double *c_fix, const double *n_fix, const float *flow, const double *zc,
                    const double *fn_mem, const double *node_mem, int32_t by_flow, double flow_threshold, double *c_out,
                    double *n_out);
+/* API 8: nep_round_leaf for `modes` (by_flow[k], flow_threshold[k]) pairs of one node in one call: c_out
+ * [modes][F*N], n_out [modes][N] (NULL without n), found[k] = 1 / 0 (< 0 returned on a bad argument). */
+int nep_round_leaves(int32_t F, int32_t N, const double *c_fix, const double *n_fix, const float *flow, const double *zc,
+                     const double *fn_mem, const double *node_mem, int32_t modes, const int32_t *by_flow,
+                     const double *flow_threshold, double *c_out, double *n_out, int32_t *found);
 
 const char *nep_last_error(void);
 int nep_api_version(void);

@@ -50,7 +50,7 @@ from collections import deque
 import numpy as np
 
 from .comm import LocalComm
-from .lp import LP_BOUND, LP_CUTOFF, LP_INFEASIBLE, LP_ITERATION_LIMIT, LP_OPTIMAL, round_leaf
+from .lp import LP_BOUND, LP_CUTOFF, LP_INFEASIBLE, LP_ITERATION_LIMIT, LP_OPTIMAL, round_leaf, round_leaves
 
 OPTIMAL, INFEASIBLE, LIMIT = "OPTIMAL", "INFEASIBLE", "LIMIT"
 _STATUS_NAME = {LP_OPTIMAL: "certified", LP_ITERATION_LIMIT: "limit", LP_INFEASIBLE: "infeasible",
@@ -241,6 +241,30 @@ class BranchAndBound:
         fx = np.zeros(self.lp.n_int, bool)
         fx[node.idx] = True
         return fx
+
+    def _round_all(self, node, flow, zc):
+        """_round for every rounding mode (self.round_modes) of one node in one native call."""
+        F, N, c0, c1 = self.F, self.N, self.c0, self.c1
+        fixed = np.full(F * N, -1.0)
+        sel = (node.idx >= c0) & (node.idx < c1)
+        fixed[node.idx[sel] - c0] = node.val[sel]
+        nfix = None
+        if self.n_range is not None:
+            n0, n1 = self.n_range
+            nfix = np.full(N, -1.0)
+            seln = (node.idx >= n0) & (node.idx < n1)
+            nfix[node.idx[seln] - n0] = node.val[seln]
+        modes = [(bf, self.flow_tol if mf is None else mf) for bf, mf in self.round_modes]
+        out = []
+        for r in round_leaves(fixed.reshape(F, N), nfix, np.asarray(flow).reshape(F, N), zc, self.fn_mem,
+                              self.node_mem, modes):
+            if r is None:
+                out.append(None)
+            elif r[1] is None:
+                out.append((np.arange(c0, c1), r[0]))
+            else:
+                out.append((np.concatenate([np.arange(c0, c1), np.arange(*self.n_range)]), np.concatenate(r)))
+        return out
 
     def _round(self, node, flow, zc=None, by_flow=True, min_flow=None):
         """Heuristic completion of a node (a leaf fixing every c and n), or None.
@@ -461,8 +485,7 @@ class BranchAndBound:
             flow = lp.flows([slot])[0]
             z, _ = lp.solution(slot, dense_x=False)
         me = (eng, slot, eng.gen[slot], node.nid)
-        for by_flow, min_flow in self.round_modes:
-            leaf = self._round(node, flow, z[self.c0:self.c1], by_flow, min_flow)
+        for leaf in self._round_all(node, flow, z[self.c0:self.c1]):
             if leaf is not None:
                 key = np.packbits(leaf[1] > 0.5).tobytes()
                 if key not in self.seen_leaves:

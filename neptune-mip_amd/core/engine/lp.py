@@ -66,7 +66,7 @@ EXPORTS = ("nep_model_create", "nep_model_destroy", "nep_model_get_info", "nep_l
            "nep_last_error", "nep_api_version", "nep_lp_get_diag", "nep_debug_build", "nep_debug_state",
            "nep_debug_presolve", "nep_lp_set_params", "nep_lp_get_flows", "nep_lp_routing_entries",
            "nep_lp_allocation_entries", "nep_lp_score_check", "nep_round_leaf", "nep_lp_copy_routing",
-           "nep_lp_get_solutions")
+           "nep_lp_get_solutions", "nep_round_leaves")
 SCORE_FIELDS = ("network_delay", "nodes_used", "node_cost", "bad_c_x", "bad_memory", "bad_handle", "bad_cpu",
                 "bad_n_c", "bad_budget", "handle_maxdev", "cpu_maxexcess")
 
@@ -99,6 +99,8 @@ def load_library(path=None):
     lib.nep_lp_copy_state.argtypes = [vp, i32, i32]
     lib.nep_lp_copy_routing.argtypes = [vp, i32, vp, i32]
     lib.nep_lp_get_solutions.argtypes = [vp, i32, pi32, _dp]
+    lib.nep_round_leaves.argtypes = [i32, i32, _dp, _dp, ctypes.POINTER(ctypes.c_float), _dp, _dp, _dp, i32, pi32, _dp,
+                                     _dp, _dp, pi32]
     lib.nep_get_stats.argtypes = [vp, ctypes.POINTER(Stats)]
     lib.nep_reset_stats.argtypes = [vp]
     lib.nep_reset_stats.restype = None
@@ -149,6 +151,29 @@ def round_leaf(c_fix, n_fix, flow, zc, fn_mem, node_mem, by_flow, flow_threshold
     if rc < 0:
         raise EngineUnavailable(f"nep_round_leaf failed ({rc})")
     return (c_out, n_out) if rc == 1 else None
+
+
+def round_leaves(c_fix, n_fix, flow, zc, fn_mem, node_mem, modes):
+    """round_leaf for several (by_flow, flow_threshold) modes of one node in one call (nep_round_leaves):
+    [(c, n or None) or None per mode]."""
+    lib = load_library()
+    c_fix = np.ascontiguousarray(c_fix, np.float64)
+    F, N = c_fix.shape
+    k = len(modes)
+    nf = None if n_fix is None else np.ascontiguousarray(n_fix, np.float64)
+    fl = np.ascontiguousarray(flow, np.float32)
+    zcv = None if zc is None else np.ascontiguousarray(zc, np.float64)
+    bf = np.array([1 if m[0] else 0 for m in modes], np.int32)
+    th = np.array([float(m[1]) for m in modes], np.float64)
+    c_out = np.zeros((k, F * N))
+    n_out = None if nf is None else np.zeros((k, N))
+    found = np.zeros(k, np.int32)
+    rc = lib.nep_round_leaves(F, N, _ptr(c_fix), _ptr(nf), _ptr(fl), _ptr(zcv), _ptr(np.ascontiguousarray(fn_mem, np.float64)),
+                              _ptr(np.ascontiguousarray(node_mem, np.float64)), k, _ptr(bf), _ptr(th), _ptr(c_out),
+                              _ptr(n_out), _ptr(found))
+    if rc < 0:
+        raise EngineUnavailable(f"nep_round_leaves failed ({rc})")
+    return [((c_out[q], None if n_out is None else n_out[q]) if found[q] else None) for q in range(k)]
 
 
 def _ptr(a, ctype=ctypes.c_double):
@@ -341,7 +366,7 @@ class LPModel:
         slots = np.ascontiguousarray(np.asarray(slots, dtype=np.int32).reshape(-1))
         out = np.zeros((len(slots), self.n_int))
         _check(self._lib, self._lib.nep_lp_get_solutions(self._h, len(slots), _ptr(slots, ctypes.c_int32), _ptr(out)),
-               "nep_lp_get_solutions")
+               "nep_lp_get_solutions", "nep_round_leaves")
         return out
 
     def rows(self, slot):

@@ -171,12 +171,14 @@ struct Model {
   float *h_flows = nullptr;     // pinned staging of nep_lp_get_flows(_split): [2][max_batch][F*N] + slots
   double *h_sols = nullptr;     // pinned staging of nep_lp_get_solutions: [max_batch][n_int] + statuses
   // pinned staging of nep_lp_submit's uploads (slots, change offsets / indices / bounds, exact flags): the
-  // call returns without waiting for them; the next submit waits on ev_sub before rewriting the staging
-  int32_t *h_sub_i = nullptr;
-  double *h_sub_d = nullptr;
-  size_t cap_sub_i = 0, cap_sub_d = 0;
-  hipEvent_t ev_sub = nullptr;
-  bool sub_pending = false;
+  // call returns without waiting for them; two stagings alternate, and a submit waits on the event of the
+  // one it rewrites (recorded after that staging's copies, two submits earlier: normally long done)
+  int32_t *h_sub_i[2] = {nullptr, nullptr};
+  double *h_sub_d[2] = {nullptr, nullptr};
+  size_t cap_sub_i[2] = {0, 0}, cap_sub_d[2] = {0, 0};
+  hipEvent_t ev_sub[2] = {nullptr, nullptr};
+  bool sub_pending[2] = {false, false};
+  int sub_k = 0;
   ~Model() {
     if (stream) (void)hipStreamSynchronize(stream);
     if (aux) (void)hipStreamSynchronize(aux);
@@ -184,9 +186,11 @@ struct Model {
     if (h_act) (void)hipHostFree(h_act);
     if (h_flows) (void)hipHostFree(h_flows);
     if (h_sols) (void)hipHostFree(h_sols);
-    if (h_sub_i) (void)hipHostFree(h_sub_i);
-    if (h_sub_d) (void)hipHostFree(h_sub_d);
-    if (ev_sub) (void)hipEventDestroy(ev_sub);
+    for (int k = 0; k < 2; ++k) {
+      if (h_sub_i[k]) (void)hipHostFree(h_sub_i[k]);
+      if (h_sub_d[k]) (void)hipHostFree(h_sub_d[k]);
+      if (ev_sub[k]) (void)hipEventDestroy(ev_sub[k]);
+    }
     for (void *p : allocs) (void)hipFree(p);
     for (hipGraphExec_t g : block_graph)
       if (g) (void)hipGraphExecDestroy(g);
@@ -1205,40 +1209,42 @@ int submit(Model &m, int n, const int32_t *slots, const double *lbi, const doubl
   // KB per node instead of the 2 x 8 x n_int bytes of bounds and the F x NP mask), staged through pinned
   // host memory so the call need not wait for the copies (nor for the initialisation kernels behind them)
   const size_t need_i = 2 * (size_t)nf + off.size() + ci.size(), need_d = cl.size() + cu.size();
-  if (m.sub_pending) HIPCHK(hipEventSynchronize(m.ev_sub));   // the previous submit's copies have read the staging
-  m.sub_pending = false;
-  if (need_i > m.cap_sub_i) {
-    if (m.h_sub_i) HIPCHK(hipHostFree(m.h_sub_i));
-    m.h_sub_i = nullptr;
-    m.cap_sub_i = std::max(need_i, 2 * m.cap_sub_i);
+  const int sk = m.sub_k;
+  m.sub_k ^= 1;
+  if (m.sub_pending[sk]) HIPCHK(hipEventSynchronize(m.ev_sub[sk]));   // that staging's copies have read it
+  m.sub_pending[sk] = false;
+  if (need_i > m.cap_sub_i[sk]) {
+    if (m.h_sub_i[sk]) HIPCHK(hipHostFree(m.h_sub_i[sk]));
+    m.h_sub_i[sk] = nullptr;
+    m.cap_sub_i[sk] = std::max(need_i, 2 * m.cap_sub_i[sk]);
     void *h = nullptr;
-    if (hipHostMalloc(&h, m.cap_sub_i * sizeof(int32_t)) != hipSuccess) return fail(NEP_ERR_NOMEM, "hipHostMalloc (submit)");
-    m.h_sub_i = static_cast<int32_t *>(h);
+    if (hipHostMalloc(&h, m.cap_sub_i[sk] * sizeof(int32_t)) != hipSuccess) return fail(NEP_ERR_NOMEM, "hipHostMalloc (submit)");
+    m.h_sub_i[sk] = static_cast<int32_t *>(h);
   }
-  if (need_d > m.cap_sub_d) {
-    if (m.h_sub_d) HIPCHK(hipHostFree(m.h_sub_d));
-    m.h_sub_d = nullptr;
-    m.cap_sub_d = std::max(need_d, 2 * m.cap_sub_d);
+  if (need_d > m.cap_sub_d[sk]) {
+    if (m.h_sub_d[sk]) HIPCHK(hipHostFree(m.h_sub_d[sk]));
+    m.h_sub_d[sk] = nullptr;
+    m.cap_sub_d[sk] = std::max(need_d, 2 * m.cap_sub_d[sk]);
     void *h = nullptr;
-    if (hipHostMalloc(&h, m.cap_sub_d * sizeof(double)) != hipSuccess) return fail(NEP_ERR_NOMEM, "hipHostMalloc (submit)");
-    m.h_sub_d = static_cast<double *>(h);
+    if (hipHostMalloc(&h, m.cap_sub_d[sk] * sizeof(double)) != hipSuccess) return fail(NEP_ERR_NOMEM, "hipHostMalloc (submit)");
+    m.h_sub_d[sk] = static_cast<double *>(h);
   }
-  if (!m.ev_sub) HIPCHK(hipEventCreateWithFlags(&m.ev_sub, hipEventDisableTiming));
-  int32_t *hf = m.h_sub_i, *ho = hf + nf, *hc = ho + off.size(), *he = hc + ci.size();
-  double *hl = m.h_sub_d, *hu = hl + cl.size();
+  if (!m.ev_sub[sk]) HIPCHK(hipEventCreateWithFlags(&m.ev_sub[sk], hipEventDisableTiming));
+  int32_t *hf = m.h_sub_i[sk], *ho = hf + nf, *hc = ho + off.size(), *he = hc + ci.size();
+  double *hl = m.h_sub_d[sk], *hu = hl + cl.size();
   std::copy(fresh.begin(), fresh.end(), hf);
   std::copy(off.begin(), off.end(), ho);
   std::copy(ci.begin(), ci.end(), hc);
   std::copy(exact.begin(), exact.end(), he);
   std::copy(cl.begin(), cl.end(), hl);
   std::copy(cu.begin(), cu.end(), hu);
-  HIPCHK(hipMemcpyAsync(m.d_sub_i, m.h_sub_i, need_i * sizeof(int32_t), hipMemcpyHostToDevice, m.aux));
-  if (need_d) HIPCHK(hipMemcpyAsync(m.d_sub_d, m.h_sub_d, need_d * sizeof(double), hipMemcpyHostToDevice, m.aux));
+  HIPCHK(hipMemcpyAsync(m.d_sub_i, hf, need_i * sizeof(int32_t), hipMemcpyHostToDevice, m.aux));
+  if (need_d) HIPCHK(hipMemcpyAsync(m.d_sub_d, hl, need_d * sizeof(double), hipMemcpyHostToDevice, m.aux));
   int32_t *dn = m.d_sub_i, *doff = dn + nf, *didx = doff + off.size(), *dex = didx + ci.size();
   double *dlb = m.d_sub_d, *dub = dlb + cl.size();
   // the staging is free again once these copies are done (the next submit waits for this event only, not
   // for the initialisation kernels below)
-  HIPCHK(hipEventRecord(m.ev_sub, m.aux));
+  HIPCHK(hipEventRecord(m.ev_sub[sk], m.aux));
   HIPCHK(launch_node_bounds(v, dn, nf, m.d_base_lb, m.d_base_ub, m.d_base_mask, doff, didx, dlb, dub, max_chg,
                             m.aux));
   HIPCHK(launch_init_slot(v, dn, dex, nf, o.warm_start != 0, m.eta, m.omega0, m.aux));
@@ -1249,7 +1255,7 @@ int submit(Model &m, int n, const int32_t *slots, const double *lbi, const doubl
   HIPCHK(hipEventRecord(m.ev_aux, m.aux));
   HIPCHK(hipStreamWaitEvent(m.stream, m.ev_aux, 0));
   m.act.insert(m.act.end(), fresh.begin(), fresh.end());   // (d_slots follows at the next launch_block)
-  m.sub_pending = true;
+  m.sub_pending[sk] = true;
   return NEP_OK;
 }
 

@@ -149,3 +149,17 @@ extern "C" int nep_round_leaf(int32_t F, int32_t N, const double *c_fix, const d
   std::copy(c.begin(), c.end(), c_out);
   return 1;
 }
+
+extern "C" int nep_round_leaves(int32_t F, int32_t N, const double *c_fix, const double *n_fix, const float *flow,
+                                const double *zc, const double *fn_mem, const double *node_mem, int32_t modes,
+                                const int32_t *by_flow, const double *flow_threshold, double *c_out, double *n_out,
+                                int32_t *found) {
+  if (modes < 0 || (modes > 0 && (!by_flow || !flow_threshold || !c_out || !found))) return NEP_ERR_ARG;
+  for (int k = 0; k < modes; ++k) {
+    const int rc = nep_round_leaf(F, N, c_fix, n_fix, flow, zc, fn_mem, node_mem, by_flow[k], flow_threshold[k],
+                                  c_out + (size_t)k * F * N, n_out ? n_out + (size_t)k * N : nullptr);
+    if (rc < 0) return rc;
+    found[k] = rc;
+  }
+  return NEP_OK;
+}

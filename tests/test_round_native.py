@@ -36,6 +36,13 @@ def test_native_rounding_matches_reference(with_n):
         eng = BranchAndBound.__new__(BranchAndBound)
         eng.F, eng.N, eng.c0, eng.c1, eng.n_range = F, N, ref.c0, ref.c1, ref.n_range
         eng.fn_mem, eng.node_mem, eng.flow_tol = ref.fn_mem, ref.node_mem, ref.flow_tol
+        eng.round_modes = ((False, None), (True, None), (True, 1.0 - 1e-6))
+        for z in (zc.ravel(), None):   # the batched call (_round_all) gives the single-mode calls' leaves
+            allm = eng._round_all(node, flow, z)
+            for (by_flow, min_flow), b in zip(eng.round_modes, allm):
+                a = eng._round(node, flow, z, by_flow, min_flow)
+                assert (a is None and b is None) or (a is not None and b is not None and np.array_equal(a[0], b[0])
+                                                     and np.array_equal(a[1], b[1]))
         for by_flow, min_flow in ((False, None), (True, None), (True, 1.0 - 1e-6)):
             for z in (zc.ravel(), None):
                 a = ref._round(node, flow, z, by_flow, min_flow)
