@@ -366,7 +366,7 @@ class LPModel:
         slots = np.ascontiguousarray(np.asarray(slots, dtype=np.int32).reshape(-1))
         out = np.zeros((len(slots), self.n_int))
         _check(self._lib, self._lib.nep_lp_get_solutions(self._h, len(slots), _ptr(slots, ctypes.c_int32), _ptr(out)),
-               "nep_lp_get_solutions", "nep_round_leaves")
+               "nep_lp_get_solutions")
         return out
 
     def rows(self, slot):
