@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <climits>
 #include <cmath>
@@ -15,6 +16,8 @@
 #include <memory>
 #include <random>
 #include <string>
+#include <system_error>
+#include <thread>
 #include <vector>
 
 #include "../../include/neptune_lp.h"
@@ -77,6 +80,18 @@ struct Coo {
   }
 };
 
+// scratch of one presolve_node() call, reset after every node (one per thread)
+struct PresolveScratch {
+  std::vector<int> pos, fdelta, touched, ftouched;
+  std::vector<double> dmin, dmax;
+  std::vector<uint8_t> rowmark;
+  std::vector<uint8_t> allow;   // [F*N] the node's allowed placements (CPU cover and score-row tests)
+  // the changes of the nodes this thread presolved in the current batch (capacity kept across batches: a
+  // rounding leaf's ~33k changes at 256x128 would otherwise page-fault fresh buffers on every submit)
+  std::vector<int32_t> ci;
+  std::vector<double> cl, cu;
+};
+
 struct Model {
   // problem
   int N = 0, F = 0, NP = 0, variant = 0, step = 1, has_n = 0, step2 = 0;
@@ -106,8 +121,6 @@ struct Model {
   // activity over the routing simplexes of a node's allowed destinations)
   bool score_x = false;
   std::vector<double> Dh;            // [N*N] delay matrix (step 2 with score_x only)
-  std::vector<uint8_t> allow;        // scratch [F*N]
-  std::vector<uint8_t> allow2;       // scratch [F*N] (CPU cover test)
   bool x_cost_free = true;     // no routing entry carries objective cost (step 2; W == 0)
   // node presolve as a sparse change of the base box (presolve_setup / presolve_node)
   bool base_ok = false;
@@ -115,9 +128,7 @@ struct Model {
   std::vector<uint8_t> base_mask;
   std::vector<int> base_cnt, Kcp, Kcr;
   std::vector<double> Kcv;
-  std::vector<int> pos, fdelta, touched, ftouched;   // scratch, reset after every node
-  std::vector<double> dmin, dmax;
-  std::vector<uint8_t> rowmark;
+  std::vector<PresolveScratch> psc;   // one per presolve thread (submit presolves a batch's nodes in parallel)
   double eta = 0, sigma_max = 0, omega0 = 1.0;
   // device
   hipStream_t stream = nullptr;
@@ -131,6 +142,7 @@ struct Model {
   std::vector<void *> allocs;
   double *d_prm = nullptr;      // {tol, cutoff} of the LPs in flight (DeviceView::prm)
   double prm_host[3] = {0, 0, 0};   // tol, cutoff, gap tol of the LPs in flight
+  bool prm_sent = false;            // d_prm holds prm_host (a submit with the same values skips the copy)
   int32_t *d_slots = nullptr;   // the slots currently iterating (mirror of `act`)
   int32_t *h_act = nullptr;     // pinned staging of `act` for the d_slots upload (launch_block only)
   int32_t *d_new = nullptr;     // slots being initialised by nep_lp_submit
@@ -950,6 +962,15 @@ bool presolve_full(const Model &m, const double *lbi, const double *ubi, std::ve
   return cpu_cover_ok(m, mask.data(), NP);
 }
 
+static void init_scratch(const Model &m, PresolveScratch &s) {
+  s.pos.assign(m.il.n_int, -1);
+  s.dmin.assign(m.dl.n_dual, 0.0);
+  s.dmax.assign(m.dl.n_dual, 0.0);
+  s.rowmark.assign(m.dl.n_dual, 0);
+  s.fdelta.assign(m.F, 0);
+  s.allow.assign((size_t)m.F * m.N, 0);
+}
+
 // once per model: the base box (natural bounds) and what presolve_node() needs
 void presolve_setup(Model &m) {
   const int n = m.il.n_int, F = m.F, NP = m.NP;
@@ -969,16 +990,13 @@ void presolve_setup(Model &m) {
     m.Kcr[at] = m.Kr[e];
     m.Kcv[at] = m.Kv[e];
   }
-  m.pos.assign(n, -1);
-  m.dmin.assign(m.dl.n_dual, 0.0);
-  m.dmax.assign(m.dl.n_dual, 0.0);
-  m.rowmark.assign(m.dl.n_dual, 0);
-  m.fdelta.assign(F, 0);
+  m.psc.resize(1);
+  init_scratch(m, m.psc[0]);
 }
 
 // One node as changes (index, lb, ub) of the base box, appended to ci/cl/cu.  Returns false (and
 // appends nothing) if the node is infeasible.
-bool presolve_node(Model &m, const double *lbi, const double *ubi, std::vector<int32_t> &ci,
+bool presolve_node(const Model &m, PresolveScratch &sc, const double *lbi, const double *ubi, std::vector<int32_t> &ci,
                    std::vector<double> &cl, std::vector<double> &cu) {
   const int n = m.il.n_int, N = m.N, F = m.F, NP = m.NP, oc = m.il.oc;
   if (!m.base_ok) return false;
@@ -987,7 +1005,7 @@ bool presolve_node(Model &m, const double *lbi, const double *ubi, std::vector<i
     const double l = lbi ? std::max(m.base_lb[k], lbi[k]) : m.base_lb[k];
     const double u = ubi ? std::min(m.base_ub[k], ubi[k]) : m.base_ub[k];
     if (l != m.base_lb[k] || u != m.base_ub[k]) {
-      m.pos[k] = (int)(ci.size() - c0);
+      sc.pos[k] = (int)(ci.size() - c0);
       ci.push_back(k);
       cl.push_back(l);
       cu.push_back(u);
@@ -1010,12 +1028,12 @@ bool presolve_node(Model &m, const double *lbi, const double *ubi, std::vector<i
       double nl = -INF, nu = INF;
       if (isf) nu = old + cu[t];
       else nl = old - cu[t];
-      if (m.pos[kc] >= 0) {
-        const size_t pc = c0 + m.pos[kc];
+      if (sc.pos[kc] >= 0) {
+        const size_t pc = c0 + sc.pos[kc];
         cu[pc] = std::min(cu[pc], nu);
         cl[pc] = std::max(cl[pc], nl);
       } else if (nu < m.base_ub[kc] || nl > m.base_lb[kc]) {
-        m.pos[kc] = (int)(ci.size() - c0);
+        sc.pos[kc] = (int)(ci.size() - c0);
         ci.push_back(kc);
         cl.push_back(std::max(m.base_lb[kc], nl));
         cu.push_back(std::min(m.base_ub[kc], nu));
@@ -1030,11 +1048,11 @@ bool presolve_node(Model &m, const double *lbi, const double *ubi, std::vector<i
       const int j = k - m.il.on;
       for (int f = 0; f < F; ++f) {
         const int kc = oc + f * N + j;
-        if (m.pos[kc] >= 0) {
-          double &u = cu[c0 + m.pos[kc]];
+        if (sc.pos[kc] >= 0) {
+          double &u = cu[c0 + sc.pos[kc]];
           u = std::min(u, 0.0);
         } else if (m.base_ub[kc] > 0.0) {
-          m.pos[kc] = (int)(ci.size() - c0);
+          sc.pos[kc] = (int)(ci.size() - c0);
           ci.push_back(kc);
           cl.push_back(m.base_lb[kc]);
           cu.push_back(0.0);
@@ -1043,76 +1061,81 @@ bool presolve_node(Model &m, const double *lbi, const double *ubi, std::vector<i
     }
   }
   bool ok = true;
-  std::vector<int> &touched = m.touched, &ftouched = m.ftouched;
+  std::vector<int> &touched = sc.touched, &ftouched = sc.ftouched;
   touched.clear();
   ftouched.clear();
+  // a node that changes many variables (a rounding leaf fixes every c and n) re-tests every row instead of
+  // tracking the touched ones: the bookkeeping costs more than the test
+  const bool dense = (ci.size() - c0) * 8 > (size_t)m.dl.n_dual;
   auto touch = [&](int r) {
-    if (!m.rowmark[r]) { m.rowmark[r] = 1; touched.push_back(r); }
+    if (!dense && !sc.rowmark[r]) { sc.rowmark[r] = 1; touched.push_back(r); }
   };
   for (size_t t = c0; t < ci.size(); ++t) {
     const int k = ci[t];
-    const double l = cl[t], u = cu[t], bl = m.base_lb[k], bu = m.base_ub[k];
+    const double l = cl[t], u = cu[t];
     if (l > u + 1e-12) ok = false;
     if (k >= oc && k < oc + F * N) {
       const int f = (k - oc) / N, j = (k - oc) % N;
       const int now = u > 0.0, was = m.base_mask[(size_t)f * NP + j];
       if (now != was) {
-        if (m.fdelta[f] == 0) ftouched.push_back(f);
-        m.fdelta[f] += now - was;
+        if (sc.fdelta[f] == 0) ftouched.push_back(f);
+        sc.fdelta[f] += now - was;
         const double dfx = (now - was) * m.ftot[f];
         for (int r : {m.dl.o1 + f * N + j, m.dl.o2 + f * N + j}) {
           if (m.dl.o1 < 0) break;
           touch(r);
-          m.dmax[r] += dfx;
+          sc.dmax[r] += dfx;
         }
       }
     }
+    const double bl = m.base_lb[k], bu = m.base_ub[k];
     for (int e = m.Kcp[k]; e < m.Kcp[k + 1]; ++e) {
       const int r = m.Kcr[e];
       const double a = m.Kcv[e];
       touch(r);
-      m.dmin[r] += std::min(a * l, a * u) - std::min(a * bl, a * bu);
-      m.dmax[r] += std::max(a * l, a * u) - std::max(a * bl, a * bu);
+      sc.dmin[r] += std::min(a * l, a * u) - std::min(a * bl, a * bu);
+      sc.dmax[r] += std::max(a * l, a * u) - std::max(a * bl, a * bu);
     }
   }
-  if (ok && !ftouched.empty()) {
-    // the CPU cover test (cpu_cover_ok) over the node's allowed placements; a box that closes no placement
-    // has the base box's (tested in presolve_full)
-    m.allow2.assign((size_t)F * N, 0);
+  const bool cover = ok && !ftouched.empty();
+  if (cover || (ok && m.score_x)) {
+    // the node's allowed placements: the base mask with the node's c changes over it
     for (int f = 0; f < F; ++f)
-      for (int j = 0; j < N; ++j) m.allow2[(size_t)f * N + j] = m.base_mask[(size_t)f * NP + j];
+      std::memcpy(&sc.allow[(size_t)f * N], &m.base_mask[(size_t)f * NP], (size_t)N);
     for (size_t t = c0; t < ci.size(); ++t) {
       const int k = ci[t];
-      if (k >= oc && k < oc + F * N) m.allow2[k - oc] = cu[t] > 0.0;
+      if (k >= oc && k < oc + F * N) sc.allow[k - oc] = cu[t] > 0.0;
     }
-    ok = cpu_cover_ok(m, m.allow2.data(), N);
   }
+  // the CPU cover test (cpu_cover_ok) over the node's allowed placements; a box that closes no placement
+  // has the base box's (tested in presolve_full)
+  if (cover) ok = cpu_cover_ok(m, sc.allow.data(), N);
   if (ok && m.score_x) {
     // The score / delay row (constraints_step2.py:57-88) over x: every routing row carries mass 1 on its
     // allowed destinations, so its activity is at least sum_r wsc[r] min_{j allowed} D[src_r, j].  Closed
     // placements can push that above the right-hand side (e.g. a step-1 delay of 0 admits only local
     // serving): such a node is infeasible, which PDHG cannot prove (DESIGN.md §4 "Infeasibility").
-    m.allow.assign((size_t)F * N, 0);
-    for (int f = 0; f < F; ++f)
-      for (int j = 0; j < N; ++j) m.allow[(size_t)f * N + j] = m.base_mask[(size_t)f * NP + j];
-    for (size_t t = c0; t < ci.size(); ++t) {
-      const int k = ci[t];
-      if (k >= oc && k < oc + F * N) m.allow[k - oc] = cu[t] > 0.0;
-    }
     const int rs = m.dl.oS;
     touch(rs);
-    m.dmin[rs] += score_row_xmin(m, m.allow.data(), N);
+    sc.dmin[rs] += score_row_xmin(m, sc.allow.data(), N);
   }
   for (int f : ftouched) {
-    if (m.base_cnt[f] + m.fdelta[f] == 0) ok = false;   // every routing row of f empty
-    m.fdelta[f] = 0;
+    if (m.base_cnt[f] + sc.fdelta[f] == 0) ok = false;   // every routing row of f empty
+    sc.fdelta[f] = 0;
   }
-  for (int r : touched) {
-    if (ok && !row_range_ok(m, r, m.base_amin[r] + m.dmin[r], m.base_amax[r] + m.dmax[r])) ok = false;
-    m.dmin[r] = m.dmax[r] = 0.0;
-    m.rowmark[r] = 0;
+  if (dense) {
+    for (int r = 0; r < m.dl.n_dual; ++r)
+      if (ok && !row_range_ok(m, r, m.base_amin[r] + sc.dmin[r], m.base_amax[r] + sc.dmax[r])) ok = false;
+    std::fill(sc.dmin.begin(), sc.dmin.end(), 0.0);
+    std::fill(sc.dmax.begin(), sc.dmax.end(), 0.0);
+  } else {
+    for (int r : touched) {
+      if (ok && !row_range_ok(m, r, m.base_amin[r] + sc.dmin[r], m.base_amax[r] + sc.dmax[r])) ok = false;
+      sc.dmin[r] = sc.dmax[r] = 0.0;
+      sc.rowmark[r] = 0;
+    }
   }
-  for (size_t t = c0; t < ci.size(); ++t) m.pos[ci[t]] = -1;
+  for (size_t t = c0; t < ci.size(); ++t) sc.pos[ci[t]] = -1;
   if (!ok) {
     ci.resize(c0);
     cl.resize(c0);
@@ -1149,6 +1172,88 @@ nep_lp_opts resolve_opts(const nep_lp_opts *opts) {
   return o;
 }
 
+// tol / cutoff / gap tol of every LP in flight (device memory, read by the graph-replayed blocks): copied on
+// the auxiliary stream when they change
+static hipError_t set_prm(Model &m, double tol, double cutoff, double gap_tol) {
+  if (m.prm_sent && m.prm_host[0] == tol && m.prm_host[1] == cutoff && m.prm_host[2] == gap_tol) return hipSuccess;
+  m.prm_host[0] = tol;
+  m.prm_host[1] = cutoff;
+  m.prm_host[2] = gap_tol;
+  m.prm_sent = true;
+  return hipMemcpyAsync(m.d_prm, m.prm_host, sizeof(m.prm_host), hipMemcpyHostToDevice, m.aux);
+}
+
+// presolve threads for a submit of n nodes: NEP_PRESOLVE_THREADS (default 8, 1 = serial), only for large
+// models (below ~8k integer variables a node presolves in tens of microseconds, less than a thread start)
+static int presolve_threads(const Model &m, int n) {
+  static const int cap = [] {
+    const char *e = std::getenv("NEP_PRESOLVE_THREADS");
+    const int v = e ? std::atoi(e) : 8;
+    const int hw = (int)std::thread::hardware_concurrency();
+    return std::max(1, std::min(v, hw > 0 ? hw : 1));
+  }();
+  if (n < 2 || m.il.n_int < 8192) return 1;
+  return std::min(cap, n);
+}
+
+// one presolved node box: its changes of the base box (m.psc[t].ci/cl/cu [off, off + cnt)), feasibility and
+// whether it fixes the objective
+struct NodeBox {
+  int t = 0;
+  size_t off = 0, cnt = 0;
+  bool ok = false, ex = false;
+};
+
+// Presolve n nodes on the host — over the nodes in parallel when they are large (a rounding leaf at
+// 256x128 changes ~33k bounds, ~1 ms of work; presolve_threads) — into box[0 .. n-1].
+static void presolve_batch(Model &m, int n, const double *lbi, const double *ubi, std::vector<NodeBox> &box) {
+  const size_t ni = (size_t)m.il.n_int;
+  box.assign(n, NodeBox{});
+  auto one = [&](int b, int t) {
+    PresolveScratch &sc = m.psc[t];
+    NodeBox &nb = box[b];
+    const double *L = lbi ? lbi + (size_t)b * ni : nullptr, *U = ubi ? ubi + (size_t)b * ni : nullptr;
+    nb.t = t;
+    nb.off = sc.ci.size();
+    nb.ok = presolve_node(m, sc, L, U, sc.ci, sc.cl, sc.cu);
+    nb.cnt = sc.ci.size() - nb.off;
+    // the box fixes the objective when the routing carries no cost and every c and n is fixed (a
+    // leaf): mf / mt / allocated / deallocated then follow from c at their cheapest (the repair)
+    bool ex = nb.ok && m.x_cost_free && !m.fac;
+    const int n_fix_end = m.has_n ? m.il.on + m.N : m.il.oc + m.F * m.N;
+    for (int k = m.il.oc; ex && k < m.il.oc + m.F * m.N; ++k)
+      ex = L && U && std::max(L[k], m.nat_lb[k]) == std::min(U[k], m.nat_ub[k]);
+    for (int k = m.has_n ? m.il.on : n_fix_end; ex && k < n_fix_end; ++k)
+      ex = L && U && std::max(L[k], m.nat_lb[k]) == std::min(U[k], m.nat_ub[k]);
+    nb.ex = ex;
+  };
+  const int nt = presolve_threads(m, n);
+  while ((int)m.psc.size() < nt) {
+    m.psc.emplace_back();
+    init_scratch(m, m.psc.back());
+  }
+  for (int t = 0; t < nt; ++t) {
+    m.psc[t].ci.clear();
+    m.psc[t].cl.clear();
+    m.psc[t].cu.clear();
+  }
+  if (nt <= 1) {
+    for (int b = 0; b < n; ++b) one(b, 0);
+  } else {
+    std::atomic<int> next{0};
+    auto work = [&](int t) {
+      for (int b; (b = next.fetch_add(1)) < n;) one(b, t);
+    };
+    std::vector<std::thread> th;
+    try {
+      for (int t = 1; t < nt; ++t) th.emplace_back(work, t);
+    } catch (const std::system_error &) {   // (fewer threads: this one drains the rest)
+    }
+    work(0);
+    for (auto &t : th) t.join();
+  }
+}
+
 // Start n node LPs: presolve each on the host, upload its bounds and destination mask, initialise
 // the slot (cold or warm) and add it to the iterating set.  status[b] = NEP_LP_INFEASIBLE for a
 // node presolve proves infeasible (it does not iterate), else NEP_LP_ITERATION_LIMIT.
@@ -1171,35 +1276,23 @@ int submit(Model &m, int n, const int32_t *slots, const double *lbi, const doubl
   v.max_iters = o.max_iters;
   v.bound_res = o.bound_res;
   // tol / cutoff of every LP in flight: device memory, read by the (graph-replayed) blocks
-  m.prm_host[0] = o.tol;
-  m.prm_host[1] = o.cutoff;
-  m.prm_host[2] = o.gap_tol;
-  HIPCHK(hipMemcpyAsync(m.d_prm, m.prm_host, sizeof(m.prm_host), hipMemcpyHostToDevice, m.aux));
-  std::vector<int32_t> fresh, off(1, 0), ci, exact;
-  std::vector<double> cl, cu;
-  const size_t ni = (size_t)m.il.n_int;
+  HIPCHK(set_prm(m, o.tol, o.cutoff, o.gap_tol));
+  std::vector<NodeBox> box;
+  presolve_batch(m, n, lbi, ubi, box);
+  std::vector<int32_t> fresh, off(1, 0), exact;
   int max_chg = 0;
   for (int b = 0; b < n; ++b) {
     const int s = slots[b];
-    const size_t c0 = ci.size();
-    const bool ok = presolve_node(m, lbi ? lbi + (size_t)b * ni : nullptr, ubi ? ubi + (size_t)b * ni : nullptr, ci, cl, cu);
-    status[b] = ok ? NEP_LP_ITERATION_LIMIT : NEP_LP_INFEASIBLE;
-    if (!ok) continue;
+    const NodeBox &nb = box[b];
+    status[b] = nb.ok ? NEP_LP_ITERATION_LIMIT : NEP_LP_INFEASIBLE;
+    if (!nb.ok) continue;
     m.busy[s] = 1;
     fresh.push_back(s);
-    // the box fixes the objective when the routing carries no cost and every c and n is fixed (a
-    // leaf): mf / mt / allocated / deallocated then follow from c at their cheapest (the repair)
-    bool ex = m.x_cost_free && !m.fac;
-    const double *L = lbi ? lbi + (size_t)b * ni : nullptr, *U = ubi ? ubi + (size_t)b * ni : nullptr;
-    const int n_fix_end = m.has_n ? m.il.on + m.N : m.il.oc + m.F * m.N;
-    for (int k = m.il.oc; ex && k < m.il.oc + m.F * m.N; ++k)
-      ex = L && U && std::max(L[k], m.nat_lb[k]) == std::min(U[k], m.nat_ub[k]);
-    for (int k = m.has_n ? m.il.on : n_fix_end; ex && k < n_fix_end; ++k)
-      ex = L && U && std::max(L[k], m.nat_lb[k]) == std::min(U[k], m.nat_ub[k]);
-    exact.push_back(ex ? 1 : 0);
-    off.push_back((int32_t)ci.size());
-    max_chg = std::max(max_chg, (int)(ci.size() - c0));
+    exact.push_back(nb.ex ? 1 : 0);
+    off.push_back(off.back() + (int32_t)nb.cnt);
+    max_chg = std::max(max_chg, (int)nb.cnt);
   }
+  const size_t nchg = (size_t)off.back();
   if (fresh.empty()) {
     HIPCHK(hipStreamSynchronize(m.aux));
     return NEP_OK;
@@ -1208,7 +1301,7 @@ int submit(Model &m, int n, const int32_t *slots, const double *lbi, const doubl
   // the node boxes on the device: base box copy + the packed changes scattered over it (a few
   // KB per node instead of the 2 x 8 x n_int bytes of bounds and the F x NP mask), staged through pinned
   // host memory so the call need not wait for the copies (nor for the initialisation kernels behind them)
-  const size_t need_i = 2 * (size_t)nf + off.size() + ci.size(), need_d = cl.size() + cu.size();
+  const size_t need_i = 2 * (size_t)nf + off.size() + nchg, need_d = 2 * nchg;
   const int sk = m.sub_k;
   m.sub_k ^= 1;
   if (m.sub_pending[sk]) HIPCHK(hipEventSynchronize(m.ev_sub[sk]));   // that staging's copies have read it
@@ -1230,18 +1323,24 @@ int submit(Model &m, int n, const int32_t *slots, const double *lbi, const doubl
     m.h_sub_d[sk] = static_cast<double *>(h);
   }
   if (!m.ev_sub[sk]) HIPCHK(hipEventCreateWithFlags(&m.ev_sub[sk], hipEventDisableTiming));
-  int32_t *hf = m.h_sub_i[sk], *ho = hf + nf, *hc = ho + off.size(), *he = hc + ci.size();
-  double *hl = m.h_sub_d[sk], *hu = hl + cl.size();
+  int32_t *hf = m.h_sub_i[sk], *ho = hf + nf, *hc = ho + off.size(), *he = hc + nchg;
+  double *hl = m.h_sub_d[sk], *hu = hl + nchg;
   std::copy(fresh.begin(), fresh.end(), hf);
   std::copy(off.begin(), off.end(), ho);
-  std::copy(ci.begin(), ci.end(), hc);
   std::copy(exact.begin(), exact.end(), he);
-  std::copy(cl.begin(), cl.end(), hl);
-  std::copy(cu.begin(), cu.end(), hu);
+  for (int b = 0, q = 0; b < n; ++b) {   // the feasible nodes' changes, in batch order
+    const NodeBox &nb = box[b];
+    if (!nb.ok) continue;
+    const PresolveScratch &sc = m.psc[nb.t];
+    std::memcpy(hc + off[q], sc.ci.data() + nb.off, nb.cnt * sizeof(int32_t));
+    std::memcpy(hl + off[q], sc.cl.data() + nb.off, nb.cnt * sizeof(double));
+    std::memcpy(hu + off[q], sc.cu.data() + nb.off, nb.cnt * sizeof(double));
+    ++q;
+  }
   HIPCHK(hipMemcpyAsync(m.d_sub_i, hf, need_i * sizeof(int32_t), hipMemcpyHostToDevice, m.aux));
   if (need_d) HIPCHK(hipMemcpyAsync(m.d_sub_d, hl, need_d * sizeof(double), hipMemcpyHostToDevice, m.aux));
-  int32_t *dn = m.d_sub_i, *doff = dn + nf, *didx = doff + off.size(), *dex = didx + ci.size();
-  double *dlb = m.d_sub_d, *dub = dlb + cl.size();
+  int32_t *dn = m.d_sub_i, *doff = dn + nf, *didx = doff + off.size(), *dex = didx + nchg;
+  double *dlb = m.d_sub_d, *dub = dlb + nchg;
   // the staging is free again once these copies are done (the next submit waits for this event only, not
   // for the initialisation kernels below)
   HIPCHK(hipEventRecord(m.ev_sub[sk], m.aux));
@@ -1773,10 +1872,7 @@ int nep_lp_set_params(void *model, double tol, double cutoff) {
   Model &m = *static_cast<Model *>(model);
   if (tol > 0) m.run.tol = tol;
   m.run.cutoff = cutoff;
-  m.prm_host[0] = m.run.tol;
-  m.prm_host[1] = m.run.cutoff;
-  m.prm_host[2] = m.run.gap_tol;
-  HIPCHK(hipMemcpyAsync(m.d_prm, m.prm_host, sizeof(m.prm_host), hipMemcpyHostToDevice, m.aux));
+  HIPCHK(set_prm(m, m.run.tol, m.run.cutoff, m.run.gap_tol));
   HIPCHK(hipStreamSynchronize(m.aux));
   return NEP_OK;
 }
@@ -1884,8 +1980,8 @@ int nep_debug_presolve(const nep_model_desc *desc, int32_t n, const double *lbi,
   const size_t ni = (size_t)m.il.n_int;
   std::vector<double> lb, ub;
   std::vector<uint8_t> mask;
-  std::vector<int32_t> ci;
-  std::vector<double> cl, cu;
+  std::vector<NodeBox> box;
+  presolve_batch(m, n, lbi, ubi, box);   // (the submit path: in parallel for large models)
   for (int b = 0; b < n; ++b) {
     const double *l = lbi ? lbi + b * ni : nullptr, *u = ubi ? ubi + b * ni : nullptr;
     ok_full[b] = presolve_full(m, l, u, lb, ub, mask) ? 1 : 0;
@@ -1893,17 +1989,16 @@ int nep_debug_presolve(const nep_model_desc *desc, int32_t n, const double *lbi,
       std::memcpy(box_full + 2 * b * ni, lb.data(), ni * sizeof(double));
       std::memcpy(box_full + (2 * b + 1) * ni, ub.data(), ni * sizeof(double));
     }
-    ci.clear();
-    cl.clear();
-    cu.clear();
-    ok_node[b] = presolve_node(m, l, u, ci, cl, cu) ? 1 : 0;
+    const NodeBox &nb = box[b];
+    const PresolveScratch &sc = m.psc[nb.t];
+    ok_node[b] = nb.ok ? 1 : 0;
     if (box_node) {
       double *bl = box_node + 2 * b * ni, *bu = box_node + (2 * b + 1) * ni;
       std::memcpy(bl, m.base_lb.data(), ni * sizeof(double));
       std::memcpy(bu, m.base_ub.data(), ni * sizeof(double));
-      for (size_t t = 0; t < ci.size(); ++t) {
-        bl[ci[t]] = cl[t];
-        bu[ci[t]] = cu[t];
+      for (size_t t = nb.off; t < nb.off + nb.cnt; ++t) {
+        bl[sc.ci[t]] = sc.cl[t];
+        bu[sc.ci[t]] = sc.cu[t];
       }
     }
   }

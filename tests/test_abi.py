@@ -97,6 +97,47 @@ def test_node_presolve_incremental_equals_full(name, k):
         np.testing.assert_array_equal(box_f[b], box_n[b])
 
 
+def test_parallel_node_presolve_equals_full():
+    """Above ~8k integer variables nep_lp_submit presolves a batch's nodes on several host threads
+    (nep_host.cpp presolve_batch; rounding leaves fix every c and n and take the dense row re-test): each
+    node must still decide feasibility and produce the box the from-scratch presolve does."""
+    from core.engine.heuristics import capacity_greedy
+    from core.engine.lp import debug_build, debug_presolve
+    from core.utils import data_to_solver_input
+    from core.utils.synthetic import synthetic_payload
+    N, F = 128, 64
+    data = data_to_solver_input(synthetic_payload(N, F, seed=3), with_db=False)
+    n_int = debug_build(data, "MinDelayAndUtilization", step=1, alpha=0.5)["n_int"]
+    assert n_int >= 8192
+    rng = np.random.default_rng(5)
+    d = data
+    leaves = capacity_greedy(d.workload_matrix, d.node_delay_matrix, d.core_per_req_matrix,
+                             np.reshape(d.node_cores_matrix, N), np.reshape(d.function_memory_matrix, F),
+                             np.reshape(d.node_memory_matrix, N), np.asarray(d.node_cores_matrix, float).reshape(N))
+    B = 12
+    lb = np.full((B, n_int), -np.inf)
+    ub = np.full((B, n_int), np.inf)
+    for b in range(B):
+        if b % 3 == 0:                     # a rounding leaf: every c and n fixed (the capacity greedy's)
+            c, n = leaves[(b // 3) % len(leaves)][:2]
+            c, n = np.asarray(c, float).reshape(-1), np.asarray(n, float).copy()
+            if b % 6 == 0:                 # (an open placement on a closed node: infeasible)
+                n[int(np.nonzero(c.reshape(F, N).max(0))[0][0])] = 0.0
+            lb[b, :F * N] = ub[b, :F * N] = c
+            lb[b, F * N:] = ub[b, F * N:] = n
+        elif b % 3 == 1:                   # a branching node: a few fixings
+            idx = rng.choice(n_int, 6, replace=False)
+            lb[b, idx] = ub[b, idx] = rng.integers(0, 2, idx.size)
+        else:                              # every placement of one function closed: infeasible (C4)
+            f = int(rng.integers(F))
+            ub[b, f * N:(f + 1) * N] = 0.0
+    ok_f, ok_n, box_f, box_n = debug_presolve(data, "MinDelayAndUtilization", lb, ub, step=1, alpha=0.5)
+    np.testing.assert_array_equal(ok_f, ok_n)
+    assert not ok_f[2::3].any() and not ok_f[0::6].any() and ok_n[1] and ok_n[3::6].all()
+    for b in np.nonzero(ok_f)[0]:
+        np.testing.assert_array_equal(box_f[b], box_n[b])
+
+
 def test_request_unknown_solver_type_raises():
     """core.request resolves solver.type through the SOLVERS whitelist (the reference: eval, main.py:44);
     an unknown type raises before any engine call (the reference's server answers HTTP 500)."""
