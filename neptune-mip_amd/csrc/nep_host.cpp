@@ -43,6 +43,7 @@ hipError_t launch_compact_f32(const float *vals, int rows, int cols, int64_t ld,
 hipError_t launch_compact_f64(const double *vals, int rows, int cols, int64_t ld, double thr, int round3,
                               int32_t *cnt, int32_t *off, int32_t *orow, int32_t *ocol, double *oval, bool count_only,
                               hipStream_t s);
+hipError_t launch_copy_segments(const SlotCopy &c, hipStream_t s);
 hipError_t launch_score_check(const DeviceView &v, int slot, const double *zi, double *cpu_fj, double *fpart,
                               double *jpart, const double *node_cost, double budget, double *out, hipStream_t s);
 }  // namespace nep
@@ -1809,6 +1810,8 @@ int nep_lp_get_rows(void *model, int32_t slot, float *xbar, int32_t *row_f, int3
   return NEP_OK;
 }
 
+static_assert(sizeof(Ctrl) % 4 == 0, "copy_segments copies 4-byte words");
+
 int nep_lp_copy_state(void *model, int32_t src, int32_t dst) {
   if (!model) return fail(NEP_ERR_ARG, "null model");
   Model &m = *static_cast<Model *>(model);
@@ -1819,27 +1822,29 @@ int nep_lp_copy_state(void *model, int32_t src, int32_t dst) {
   if (m.busy[src]) return fail(NEP_ERR_STATE, "source slot is still iterating");
   if (src == dst) return NEP_OK;
   const DeviceView &v = m.v;
-  HIPCHK(hipMemcpyAsync(v.x + dst * v.sx, v.x + src * v.sx, v.sx * sizeof(float), hipMemcpyDeviceToDevice, m.aux));
-  HIPCHK(hipMemcpyAsync(v.theta + dst * m.R, v.theta + src * m.R, m.R * sizeof(float), hipMemcpyDeviceToDevice,
-                        m.aux));
-  HIPCHK(hipMemcpyAsync(v.zi + dst * v.sint, v.zi + src * v.sint, v.sint * sizeof(double), hipMemcpyDeviceToDevice,
-                        m.aux));
-  HIPCHK(hipMemcpyAsync(v.y + dst * v.sdual, v.y + src * v.sdual, v.sdual * sizeof(double), hipMemcpyDeviceToDevice,
-                        m.aux));
-  HIPCHK(hipMemcpyAsync(v.kty + dst * v.skty, v.kty + src * v.skty, v.skty * sizeof(float), hipMemcpyDeviceToDevice,
-                        m.aux));
+  // every per-slot array of the iterate, in one launch (copy_segments)
+  SlotCopy c{};
+  auto seg = [&](auto *base, int64_t stride) {
+    c.src[c.n] = reinterpret_cast<const char *>(base + src * stride);
+    c.dst[c.n] = reinterpret_cast<char *>(base + dst * stride);
+    c.bytes[c.n] = stride * (int64_t)sizeof(*base);
+    ++c.n;
+  };
+  seg(v.x, v.sx);
+  seg(v.theta, (int64_t)m.R);
+  seg(v.zi, v.sint);
+  seg(v.y, v.sdual);
+  seg(v.kty, v.skty);
   // the certificate's repaired point travels with the status it belongs to: solution_z() of a copied
   // certified slot returns the source's repaired point, not the destination's stale one
-  HIPCHK(hipMemcpyAsync(v.zr + dst * v.sint, v.zr + src * v.sint, v.sint * sizeof(double), hipMemcpyDeviceToDevice,
-                        m.aux));
-  HIPCHK(hipMemcpyAsync(v.rpart + dst * v.srpart, v.rpart + src * v.srpart, v.srpart * sizeof(double),
-                        hipMemcpyDeviceToDevice, m.aux));
-  HIPCHK(hipMemcpyAsync(v.ctrl + dst, v.ctrl + src, sizeof(Ctrl), hipMemcpyDeviceToDevice, m.aux));
+  seg(v.zr, v.sint);
+  seg(v.rpart, v.srpart);
+  seg(v.ctrl, (int64_t)1);
   if (m.fac) {   // the x <= c duals and their per-(f, j) sums travel with the state
-    HIPCHK(hipMemcpyAsync(v.lam + dst * v.sx, v.lam + src * v.sx, v.sx * sizeof(float), hipMemcpyDeviceToDevice, m.aux));
-    HIPCHK(hipMemcpyAsync(v.lsum + dst * v.slsum, v.lsum + src * v.slsum, v.slsum * sizeof(float),
-                          hipMemcpyDeviceToDevice, m.aux));
+    seg(v.lam, v.sx);
+    seg(v.lsum, v.slsum);
   }
+  HIPCHK(launch_copy_segments(c, m.aux));
   // no host wait: every later use of src / dst is ordered behind these copies — host reads and submits run
   // on `aux`, and a slot iterates on `stream` only after its submit's initialisation (ev_aux)
   return NEP_OK;

@@ -176,4 +176,13 @@ struct DeviceView {
   double bound_res;                      // submit option copied into each new slot's Ctrl (init_slot)
 };
 
+// device-to-device segments copied by one launch (nep_aux.hip copy_segments; byte counts multiples of 4)
+struct SlotCopy {
+  static constexpr int kMax = 12;
+  const char *src[kMax];
+  char *dst[kMax];
+  int64_t bytes[kMax];
+  int n;
+};
+
 }  // namespace nep

@@ -106,3 +106,24 @@ def test_batched_solutions_equal_single_reads(name, k):
             assert np.array_equal(row, z), slot
     finally:
         m.close()
+
+
+@pytest.mark.parametrize("name,k", CASES[:2])
+def test_copy_state_copies_every_slot_array(name, k):
+    """nep_lp_copy_state copies a slot's iterate in one launch (nep_aux.hip copy_segments): afterwards the
+    destination reads back exactly what the source does — repaired point, routing x, duals
+    and the control block (status, iteration count, primal weight)."""
+    from core.engine.lp import debug_build
+    m, data, variant, r = _solved(name, k)
+    try:
+        _, _, step, kw = build_args(name, k)
+        n_dual = debug_build(data, variant, step=step, **kw)["n_dual"]
+        m.copy_state(0, 2)
+        z0, x0 = m.solution(0)
+        z2, x2 = m.solution(2)
+        assert np.array_equal(z0, z2) and np.array_equal(x0, x2)
+        assert np.array_equal(m.diag(0), m.diag(2))
+        s0, s2 = m.debug_state(0, n_dual), m.debug_state(2, n_dual)
+        assert np.array_equal(s0["y"], s2["y"])
+    finally:
+        m.close()
