@@ -2,37 +2,43 @@
 """bench.py — LP-relaxations/sec (+ certified objective gap) on the synthetic 512-node x
 256-function NEPTUNE instance (BASELINE.json `metric`; generator of SURVEY.md §8(d)).
 
-Workload.  Branch-and-bound node LP relaxations of the step-1 NeptuneMinDelayAndUtilization model
-(reference `core/solvers/neptune/neptune_step1.py:67-77`, rows `neptune/utils/constraints_step1.py`,
-objective `neptune/utils/objectives.py:30-52`).  Every node is a child of the root LP: it carries
-`--fix` seeded c[f,j] fixings (0 or 1, the branching decisions of a B&B) and is warm-started from
-the root's primal/dual state, as a B&B child is from its parent (`--cold`: from zero).  The engine
-keeps `--batch` node LPs in flight per GPU (nep_lp_submit / nep_lp_advance): a slot whose LP
-finishes takes the next node at once, as a B&B with an open-node queue does.  One *step* =
-`--batch` node LPs; the timed region streams `--steps` x `--batch` nodes through the slots and
-drains them, so every node of the timed region finishes inside it (the hard ones included: no node
-is left iterating outside the clock).  A node counts as an LP relaxation only if the engine
-certifies it: primal objective - Lagrangian bound <= tol*max(1,|bound|) and every row residual <=
-tol; nodes that stop at the node-LP iteration limit `--max-iters` keep a valid
-Lagrangian bound (usable for pruning) and are reported, not counted.  The root LP is solved before
-the timed region; the instance tensors live on the device before the timer starts; node bounds are
-uploaded inside the timed region, as the B&B host does per node.
+Workload (`value`).  The node LPs the product's own branch-and-bound submitted on this instance
+(step-1 NeptuneMinDelayAndUtilization, reference `core/solvers/neptune/neptune_step1.py:67-77`, rows
+`neptune/utils/constraints_step1.py`, objective `neptune/utils/objectives.py:30-52`), recorded by
+tools/record_bnb_trace.py into tests/golden/bnb_trace_512x256_s0.json.gz and REPLAYED in submission
+order: each recorded box (a branching node's fixings; a leaf's open c and n, every other c and n fixed to
+0) is solved as an LP relaxation of the REFERENCE model — the LP SCIP solves at that node
+(core/solvers/solver.py:35-40).  `--batch` node LPs are in flight per GPU (nep_lp_submit /
+nep_lp_advance): a slot whose LP finishes takes the next box at once.  A node starts from its parent's
+final PDHG state when a slot still holds it (slots are refilled oldest-finished first; finished parents
+with open children are parked), else from the root's.  One *step* = `--batch` node LPs; the timed region
+streams `--steps` x `--batch` of them through the slots and drains them (every node of the timed region
+finishes inside it).  A node counts only if the engine certifies it: repaired primal objective -
+Lagrangian bound <= tol*max(1,|bound|) and every row residual <= tol; nodes that stop at
+`--max-iters` keep a valid bound and are reported, not counted.  The root LP is solved before the timed
+region (its seconds are `lp.root_seconds`); the instance lives on the device before the timer starts;
+node bounds are uploaded inside it, as the B&B host does per node.  Secondary figures in the same JSON:
+`native_replay` (the same boxes on the model the product ran them on), `children_stream` (root children
+with `--fix` random c-fixings, the round-1..3 workload) and `bnb` (the product search itself).
 
-Multi-GPU (`torch.distributed.run`, one rank per GPU): every rank holds the same instance and
-solves its own node stream (subtree sharding); the only exchange is the B&B
-bound all-reduce(MIN) of 8 bytes per step.  value = certified LPs of all ranks / max-over-ranks
-wall time ("scaling": "weak").
+Multi-GPU.  `--gpus N` > 1 without a launcher environment starts N rank processes itself
+(torch.distributed.run, one rank per GPU, 127.0.0.1 rendezvous) before anything touches the GPU; under a
+launcher the world it reports must equal --gpus.  Every rank holds the same instance and takes replay
+entries rank, rank + world, ... (subtree sharding); the only exchange is the B&B bound
+all-reduce(MIN) of 8 bytes per timed stream.  value = certified LPs of all ranks / max-over-ranks wall
+time ("scaling": "weak").
 
 Roofline.  The dominant kernel is `x_pass` (csrc/nep_kernels.hip).  Its algorithmic bytes per LP
-iteration are 8*P (x read + x write, fp32), P = R*N routing entries after exact zero-workload
-source aggregation.  `achieved` = those bytes x the LPs one sampled launch carries / that launch's
-HIP-event duration on the engine's own stream, averaged over one steady-state launch per
-64-iteration block (nep_get_stats).  `traffic` is read from profiles/traffic.json (separate
-rocprofv3 --pmc passes, tools/traffic.py) when it was measured on this exact
-workload (else null), per LP-iteration and scaled to the LPs of the average sampled launch.
+iteration are SURVEY.md §8(d)'s B_iter = 4 (2P + 2FN + 2N + 2m) (x, c, n and the duals, each read and
+written, fp32 units; P = R*N routing entries after exact zero-workload aggregation, m = the dualised rows;
+nep_model_info.bytes_per_iter: 58.7 MB at 512x256).  `achieved` = B_iter x the LPs one sampled launch
+carries / that launch's HIP-event duration on the engine's own stream, averaged over one steady-state
+launch per block (nep_get_stats).  `traffic` is read from profiles/traffic.json (separate rocprofv3 --pmc
+passes, tools/traffic.py) when it was measured on this exact workload (else null), per
+LP-iteration and scaled to the LPs of the average sampled launch.
 
-CPU baseline.  The oracle (HiGHS on the reference's formulation restated as one CSR, oracle/)
-timed on rank 0's host, bounded by `--cpu-budget` seconds (see `cpu_baseline`).
+CPU baseline.  The oracle (HiGHS on the reference's formulation restated as one CSR, oracle/) timed on
+rank 0's host, bounded by `--cpu-budget` seconds (see `cpu_baseline`).
 """
 import argparse
 import json
@@ -97,8 +103,8 @@ def parse(argv=None):
     ap.add_argument("--cpu-budget", type=float, default=150.0,
                     help="seconds for the CPU baseline (0 = skip); the bench-size attempt gets what the fit leaves, "
                          ">= 30 s")
-    ap.add_argument("--cpu-workers", type=int, default=16,
-                    help="CPU baseline worker processes (capped at the host's cores; 16 = the GPU box's share)")
+    ap.add_argument("--cpu-workers", type=int, default=0,
+                    help="CPU baseline worker processes (0: the host's per-GPU share of its cores, cpu_baseline_workers)")
     ap.add_argument("--bnb-seconds", type=float, default=20.0,
                     help="time limit of the product branch-and-bound section (0 = skip)")
     ap.add_argument("--bnb-sizes", default="256x128:20,512x256:60",
@@ -189,6 +195,16 @@ def _dnf_probe(N, F, seed, fix, seconds):
     return out
 
 
+def cpu_baseline_workers():
+    """The CPU baseline's worker processes: this GPU's share of the host's cores — the cores this process may
+    run on, divided by the host's GPUs when it is a multi-GPU node (256 cores / 8 MI355X = 32 on the GPU box;
+    every core of a host with < 64).  Counted without initialising the GPU."""
+    cores = len(os.sched_getaffinity(0))
+    total = os.cpu_count() or cores
+    gpus = 8 if total >= 64 else 1
+    return max(1, min(cores, total // gpus))
+
+
 def cpu_baseline(N, F, seed, fix, budget, workers):
     """The reference formulation of the same generator, solved by the oracle (HiGHS LP; oracle/).
 
@@ -239,9 +255,9 @@ def cpu_baseline(N, F, seed, fix, budget, workers):
     p_exp = float(np.polyfit(xs, ys, 1)[0]) if len(pts) >= 2 else 1.0
     n_l, f_l, t_l, _ = pts[-1]
     scale = ((N * N * F) / (n_l * n_l * f_l)) ** p_exp
-    # pool throughput at the largest measured size
-    # (os.cpu_count() on the GPU box is the whole machine's; its share for this job is 16 CPUs)
-    w = max(1, min(workers, os.cpu_count() or 1))
+    # pool throughput at the largest measured size, on the host's per-GPU share of its cores
+    w = workers if workers > 0 else cpu_baseline_workers()
+    w = max(1, min(w, len(os.sched_getaffinity(0))))
     m, bnds = model_and_bounds(n_l, f_l, w, seed + 1)
     sts, _, wall, w_used = lp_batch_cpu(m, bnds, workers=w)
     pool_lps = len(sts) / wall
@@ -257,7 +273,10 @@ def cpu_baseline(N, F, seed, fix, budget, workers):
                  p_exp, min(3, len(pts)), t_l * scale, N, F, w_used, len(sts), n_l, f_l, wall, pool_lps, scale,
                  N, F, N, F, dnf.get("note", "one node LP solved by HiGHS in %.1f s" % dnf.get("lp_seconds", 0.0))))
     return {"value": value, "unit": "LP-relaxations/s", "cores": w_used, "kind": "port", "sample": sample,
-            "host_cpu_count": os.cpu_count(), "worker_processes": w_used,
+            "host_cpu_count": os.cpu_count(), "affinity_cpu_count": len(os.sched_getaffinity(0)),
+            "worker_processes": w_used,
+            "cores_note": "one single-threaded HiGHS process per core of this GPU's share of the host "
+                          "(host cores / 8 GPUs on a multi-GPU node, capped at the cores this process may use)",
             "extrapolated": True, "pool_lp_per_s_at": {"nodes": n_l, "functions": f_l, "value": pool_lps},
             "dnf_at_bench_size": dnf,
             "measured": [{"nodes": a, "functions": b, "seconds": t, "status": s} for a, b, t, s in pts]}
@@ -346,6 +365,16 @@ class ReplayStream:
         self.free = {name: list(range(a.batch)) for name in models}
         self.warm_parent = 0
 
+    def peek_entry(self):
+        """(repetition, entry) this rank replays next: entries rank, rank + world, ... of the trace (repeated)."""
+        rep, i = divmod(self.pos, len(self.lps))
+        return rep, self.lps[i]
+
+    def next_entry(self):
+        out = self.peek_entry()
+        self.pos += self.stride
+        return out
+
     def _model(self, e):
         return e["model"] if (self.native and e["model"] in self.models) else "leaf"
 
@@ -367,14 +396,13 @@ class ReplayStream:
         from core.engine.lp import LP_INFEASIBLE
         a = self.a
         while self.counter < self.limit:
-            rep, i = divmod(self.pos, len(self.lps))
-            e = self.lps[i]
+            rep, e = self.peek_entry()
             name = self._model(e)
             if not self.free[name]:
                 break                            # in order: the next node waits for a slot of its model
             m, root = self.models[name]
             slot = self.free[name].pop(0)
-            self.pos += self.stride
+            self.next_entry()
             key = (rep, e["id"])
             pkey = (name, (rep, e["parent"]))
             old = self.held.pop((name, slot), None)       # this slot's finished state is overwritten now
@@ -481,14 +509,62 @@ class NodeStream:
             self._refill(r["slots"].tolist())
 
 
-def main():
-    a = parse()
-    import numpy as np
-    import torch
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s_:
+        s_.bind(("127.0.0.1", 0))
+        return s_.getsockname()[1]
 
+
+def launch_ranks(n, argv):
+    """`--gpus n` > 1 without a launcher: start n rank processes (torch.distributed.run, one per GPU, rendezvous
+    on 127.0.0.1) running this script with the same arguments, as a CHILD process — this process has not
+    touched the GPU and never replaces itself — and return their exit code."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + list(argv)
+    log(f"launching {n} ranks: {' '.join(cmd[1:])}")
+    return subprocess.call(cmd)
+
+
+def rank_world(a):
+    """(rank, world, local rank) of this process.  The world a launcher started must be the one --gpus asks
+    for: a mismatch fails instead of measuring a different number of GPUs than the JSON line would claim."""
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
     local = int(os.environ.get("LOCAL_RANK", 0))
+    if world != a.gpus:
+        raise SystemExit(f"bench.py: --gpus {a.gpus} but the launcher started {world} rank(s)")
+    return rank, world, local
+
+
+def _probe_ranks(a, rank, world):
+    """NEP_BENCH_PROBE_RANKS=k (CPU tests, tests/test_bench_launch.py): join a gloo group, print this rank's
+    first k replay entries (ReplayStream's rank, rank + world, ... split) and exit before any GPU work."""
+    import gzip
+    import torch.distributed as td
+    td.init_process_group("gloo")
+    with gzip.open(trace_path(a), "rt") as fh:
+        trace = json.load(fh)
+    rs = ReplayStream({}, a, rank, world, trace)
+    ids = [rs.next_entry()[1]["id"] for _ in range(int(os.environ["NEP_BENCH_PROBE_RANKS"]))]
+    got = [None] * world
+    td.all_gather_object(got, {"rank": rank, "world": world, "ids": ids})
+    if rank == 0:
+        print(json.dumps({"probe": "ranks", "ranks": got, "n_gpus": world}), flush=True)
+    td.destroy_process_group()
+
+
+def main():
+    a = parse()
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        sys.exit(launch_ranks(a.gpus, sys.argv[1:]))
+    rank, world, local = rank_world(a)
+    if os.environ.get("NEP_BENCH_PROBE_RANKS"):
+        return _probe_ranks(a, rank, world)
+    import numpy as np
+    import torch
+
     dist = world > 1
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)

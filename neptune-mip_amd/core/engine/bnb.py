@@ -130,6 +130,7 @@ class _Engine:
         self.gen = [0] * lp.max_batch
         self.free = deque(range(lp.max_batch - self.reserved))
         self.root_ready = False
+        self.root_state = False      # root_slot holds the root LP's final state (a warm-start source)
         self.inflight = 0
 
 
@@ -335,14 +336,17 @@ class BranchAndBound:
         for eng, slot, node in items:
             warm, src = False, None
             if self.warm and eng.root_ready:
-                src = eng.root_slot
+                # (the root slot holds a state only when the root LP ended with one: an infeasible / cut-off
+                # root leaves it empty, and its nodes then start cold unless their parent's state is resident)
+                src = eng.root_slot if eng.root_state else None
                 if node.parent is not None:
                     pe, ps, pg = node.parent[:3]
                     if pe is eng and eng.gen[ps] == pg:
                         src = ps
-                if src != slot:
-                    copies.setdefault(eng.name, (eng, []))[1].append((src, slot))
-                warm = True
+                if src is not None:
+                    if src != slot:
+                        copies.setdefault(eng.name, (eng, []))[1].append((src, slot))
+                    warm = True
                 if (self.two and self.leaf_routing_warm and node.kind == LEAF and eng is self.L
                         and node.parent is not None and node.parent[0] is self.B
                         and self.B.gen[node.parent[1]] == node.parent[2]):
@@ -396,6 +400,10 @@ class BranchAndBound:
                     self.res.lp_status["presolve_infeasible"] += 1
                     self.res.lp_status_kind[_KIND_NAME[node.kind]]["presolve_infeasible"] += 1
                     eng.free.append(slot)
+                    if node.kind == REFROOT:
+                        # the reference root proven infeasible: every leaf (a sub-box of it) is infeasible too.
+                        # Mark its engine ready (without a root state) so the loop does not wait for it forever
+                        eng.root_ready = True
                 else:
                     self.inflight[(eng.name, slot)] = node
                     eng.inflight += 1
@@ -414,6 +422,7 @@ class BranchAndBound:
             # the reference root LP: its state warm-starts the leaves (their LPs run on this model)
             if self.warm and st not in (LP_INFEASIBLE, LP_CUTOFF):
                 lp.copy_state(slot, eng.root_slot)
+                eng.root_state = True
             eng.root_ready = True
             eng.free.append(slot)
             return inc
@@ -423,6 +432,7 @@ class BranchAndBound:
             res.timing["root"] = time.time() - self.t0
             if self.warm and st not in (LP_INFEASIBLE, LP_CUTOFF):
                 lp.copy_state(slot, eng.root_slot)   # every later node can start from the root
+                eng.root_state = True
             eng.root_ready = True
             me0 = (eng, slot, eng.gen[slot], node.nid)
             for idx, val in self.seed_leaves:
@@ -535,6 +545,10 @@ class BranchAndBound:
         res.objective = float(sol["objective"])
         res.z = np.asarray(sol["z"], np.float64)
         res.x = self.lp.routing_from_entries(sol["row"], sol["dst"], sol["val"])
+        if res.incumbent_slot is not None and res.incumbent_slot in self.keep:
+            # (warm=False keeps the LP incumbent in its own working slot: give it back)
+            self.keep.discard(res.incumbent_slot)
+            self.L.free.append(res.incumbent_slot)
         res.incumbent_slot = None
         res.heuristic_incumbents += 1
         self.inc_node = None

@@ -165,12 +165,15 @@ def round_leaves(c_fix, n_fix, flow, zc, fn_mem, node_mem, modes):
     zcv = None if zc is None else np.ascontiguousarray(zc, np.float64)
     bf = np.array([1 if m[0] else 0 for m in modes], np.int32)
     th = np.array([float(m[1]) for m in modes], np.float64)
+    # (every converted array is bound to a local first: _ptr passes a raw address, which does not keep a
+    # temporary copy alive through the call)
+    fm = np.ascontiguousarray(fn_mem, np.float64)
+    nm = np.ascontiguousarray(node_mem, np.float64)
     c_out = np.zeros((k, F * N))
     n_out = None if nf is None else np.zeros((k, N))
     found = np.zeros(k, np.int32)
-    rc = lib.nep_round_leaves(F, N, _ptr(c_fix), _ptr(nf), _ptr(fl), _ptr(zcv), _ptr(np.ascontiguousarray(fn_mem, np.float64)),
-                              _ptr(np.ascontiguousarray(node_mem, np.float64)), k, _ptr(bf), _ptr(th), _ptr(c_out),
-                              _ptr(n_out), _ptr(found))
+    rc = lib.nep_round_leaves(F, N, _ptr(c_fix), _ptr(nf), _ptr(fl), _ptr(zcv), _ptr(fm), _ptr(nm), k, _ptr(bf),
+                              _ptr(th), _ptr(c_out), _ptr(n_out), _ptr(found))
     if rc < 0:
         raise EngineUnavailable(f"nep_round_leaves failed ({rc})")
     return [((c_out[q], None if n_out is None else n_out[q]) if found[q] else None) for q in range(k)]

@@ -205,9 +205,10 @@ class NeptuneStepBase(Solver):
         used = C.sum(axis=0)
         if (used > 1e6 * n + 1e-9).any() or (used < n - 1e-6).any():
             return False
+        # C8 is one row per node, n[j] * node_costs[j] <= node_budget (constraints_step1.py:101-103), not a sum
         cost = np.asarray(getattr(d, "node_costs", np.zeros(len(n))), np.float64)
         budget = float(getattr(d, "node_budget", np.inf))
-        return float(cost @ n) <= budget + 1e-9
+        return bool((cost * n <= budget + 1e-9).all())
 
     def improve(self, layout):
         """improve(idx, val, value) -> [(idx, val)]: neighbour placements of a new incumbent leaf

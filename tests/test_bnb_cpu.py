@@ -224,3 +224,67 @@ def test_two_model_leaves_take_routing_warm_starts():
         assert res.routing_warm == getattr(lp, "routing_copies", 0)
         total += res.routing_warm
     assert total > 0
+
+
+class _RefRootInfeasibleLP:
+    """Wraps a StreamingOracleLP: the box with no fixings (the two-model search's reference root, REFROOT) is
+    reported infeasible by presolve; every other box is solved as usual."""
+
+    def __new__(cls, base):
+        from oracle_lp import LP_INFEASIBLE
+        orig = base.submit
+
+        def submit(slots, lb=None, ub=None, **kw):
+            st = orig(slots, lb, ub, **kw)
+            for b, s in enumerate(np.asarray(slots).reshape(-1)):
+                if lb is None or not np.isfinite(lb[b]).any():
+                    base._pend.pop(int(s), None)
+                    st[b] = LP_INFEASIBLE
+            return st
+        base.submit = submit
+        return base
+
+
+@pytest.mark.timeout(120)
+def test_two_model_search_ends_when_refroot_is_presolve_infeasible():
+    """a reference root (REFROOT) that presolve rejects used to leave the leaf engine 'not ready'
+    forever, and with no time limit the loop spun with pending leaves and nothing in flight.  It must end:
+    the leaves then start cold and the search still reaches the recorded MIP optimum (the other LPs here
+    are solved normally)."""
+    from core.engine.bnb import OPTIMAL, BranchAndBound
+    from oracle_lp import StreamingOracleLP
+    name, k = STEP1_N[0]
+    p, data = _data(name)
+    rec = G[name]["models"][k]
+    variant = VARIANT[p["solver"]["type"]]
+    alpha = p["solver"].get("args", {}).get("alpha", 0.5)
+    lp = _RefRootInfeasibleLP(StreamingOracleLP(data, variant, step=1, max_batch=10, alpha=alpha))
+    blp = StreamingOracleLP(data, variant, step=1, max_batch=9, alpha=alpha, relaxation=1)
+    res = BranchAndBound(lp, data.workload_matrix, data.function_memory_matrix, data.node_memory_matrix,
+                         batch=8, node_limit=20000, bound_lp=blp).solve()
+    assert res.lp_status_kind["refroot"]["presolve_infeasible"] == 1
+    if rec["status"] == 0:
+        assert res.status == OPTIMAL, res.as_dict()
+        assert _close(res.objective, rec["mip_objective"]), (res.objective, rec["mip_objective"])
+
+
+def test_check_placement_budget_is_per_node():
+    """C8 is n[j] * node_costs[j] <= node_budget per node (constraints_step1.py:101-103).  A
+    placement opening more than budget / cost = 60 nodes (every source served locally at 70 nodes) meets
+    every reference row and must pass the fp64 check (a summed budget rejected it)."""
+    from core.solvers.neptune.neptune_step import NeptuneStep1CPUMinDelayAndUtilization
+    from core.utils import data_to_solver_input
+    from core.utils.synthetic import synthetic_payload
+    N, F = 70, 2
+    data = data_to_solver_input(synthetic_payload(N, F, seed=0), with_db=False)
+    step = NeptuneStep1CPUMinDelayAndUtilization(alpha=0.5)
+    step.data = data
+    C = np.ones((F, N))
+    n = np.ones(N)
+    x = np.zeros((F, N, N))
+    x[:, np.arange(N), np.arange(N)] = 1.0
+    assert float(np.asarray(data.node_costs) @ n) > data.node_budget      # the summed form would reject it
+    assert step.check_placement(C, n, x)
+    n_bad = n.copy()
+    n_bad[0] = 0.0                                                          # C6 violated at node 0
+    assert not step.check_placement(C, n_bad, x)

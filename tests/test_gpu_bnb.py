@@ -69,7 +69,7 @@ def test_product_bnb_time_limited(n, f, seconds):
     assert scoring.cpu_usage_ok(data, x)
     mem = (np.asarray(data.function_memory_matrix)[:, None] * (c > 0.5)).sum(axis=0)
     assert np.all(mem <= np.asarray(data.node_memory_matrix) + 1e-9)
-    assert np.all(np.abs(x.sum(axis=2) - 1.0) < 1e-4)
+    assert np.all(np.abs(x.sum(axis=2) - 1.0) <= 1e-6)       # C4 at the parity bar
 
 
 with open(os.path.join(GOLDEN, "efttc.json")) as fh:
