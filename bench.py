@@ -95,6 +95,9 @@ def parse(argv=None):
     ap.add_argument("--native-steps", type=int, default=6,
                     help="with the replay stream: steps of the native-model replay timed after it (each recorded "
                          "box on the model the product ran it on; 0 = skip)")
+    ap.add_argument("--park", type=int, default=256,
+                    help="replay: slots per model beyond --batch that keep finished nodes' states while their children "
+                         "are still to come (warm start from the parent; 0: only free slots keep states)")
     ap.add_argument("--warm-ancestors", action="store_true",
                     help="replay: a node whose parent's state is gone starts from its closest resident ancestor's "
                          "(default: the root's, as the product B&B does)")
@@ -351,6 +354,7 @@ class ReplayStream:
     rank r takes entries r, r + world, ... (the trace repeated as often as the steps need)."""
 
     def __init__(self, models, a, rank, world, trace, native=False):
+        from collections import Counter, OrderedDict
         self.models, self.a, self.native = models, a, native
         self.lps = [e for e in trace["lps"] if e["parent"] is not None]
         self.parent_of = {e["id"]: e["parent"] for e in trace["lps"]}
@@ -359,10 +363,20 @@ class ReplayStream:
         self.counter = 0
         self.done = []          # (status, obj, primal_obj, iters) per completed node
         self.kinds = []         # (model, kind) per completed node
+        self.depth = []         # (depth, warm from parent) per completed node
         self.where = {}         # (model, node key) -> slot holding its final state
         self.held = {}          # (model, slot) -> node key
-        self.running = {}       # (model, slot) -> (node key, kind)
-        self.free = {name: list(range(a.batch)) for name in models}
+        self.running = {}       # (model, slot) -> (node key, kind, depth, warm from parent)
+        # `batch` LPs in flight per model, over batch + park slots: a finished node whose children (in this
+        # rank's share of the trace) are still to come keeps its slot — its state parked — until its last child
+        # started (the oldest parked state is evicted when every slot is taken)
+        park = max(0, int(getattr(a, "park", 0)))
+        self.free = {name: list(range(a.batch + park)) for name in models}
+        self.parked = {name: OrderedDict() for name in models}   # slot -> node key, oldest first
+        self.busy = {name: 0 for name in models}
+        mine = [self.lps[i] for i in range(rank, len(self.lps), world)]
+        self.kids = Counter(e["parent"] for e in mine)
+        self.kids_left = {}     # (model, node key) -> children of it not yet started
         self.warm_parent = 0
 
     def peek_entry(self):
@@ -398,16 +412,26 @@ class ReplayStream:
         while self.counter < self.limit:
             rep, e = self.peek_entry()
             name = self._model(e)
-            if not self.free[name]:
+            if self.busy[name] >= a.batch:
                 break                            # in order: the next node waits for a slot of its model
             m, root = self.models[name]
-            slot = self.free[name].pop(0)
+            if self.free[name]:
+                slot = self.free[name].pop(0)
+            else:                                # every slot parked: evict the oldest parked state
+                slot, _ = self.parked[name].popitem(last=False)
             self.next_entry()
             key = (rep, e["id"])
             pkey = (name, (rep, e["parent"]))
             old = self.held.pop((name, slot), None)       # this slot's finished state is overwritten now
             if old is not None:
                 self.where.pop((name, old), None)
+            left = self.kids_left.get(pkey)
+            if left is not None:                 # one child of the parent fewer to come: release its slot after the last
+                self.kids_left[pkey] = left - 1
+                if left - 1 <= 0 and pkey in self.where:
+                    ps = self.where[pkey]
+                    if self.parked[name].pop(ps, None) is not None:
+                        self.free[name].insert(0, ps)
             src = root
             if pkey not in self.where and self.ancestors:
                 # (--warm-ancestors: the closest ancestor whose final state a slot still holds)
@@ -416,7 +440,8 @@ class ReplayStream:
                     p = self.parent_of.get(p)
                 if p is not None:
                     pkey = (name, (rep, p))
-            if pkey in self.where:
+            warm_parent = pkey in self.where
+            if warm_parent:
                 src = self.where[pkey]
                 self.warm_parent += 1
             m.copy_state(src, slot)
@@ -432,9 +457,11 @@ class ReplayStream:
             if int(st[0]) == LP_INFEASIBLE:
                 self.done.append((LP_INFEASIBLE, float("inf"), float("nan"), 0))
                 self.kinds.append((name, e["kind"]))
+                self.depth.append((e["depth"], warm_parent))
                 self.free[name].append(slot)
             else:
-                self.running[(name, slot)] = (key, e["kind"])
+                self.running[(name, slot)] = (key, e["kind"], e["depth"], warm_parent)
+                self.busy[name] += 1
 
     def drain(self, n):
         """Stream the next n recorded nodes through the slots until every one of them finished."""
@@ -448,11 +475,18 @@ class ReplayStream:
                 for i, slot in enumerate(r["slots"].tolist()):
                     self.done.append((int(r["status"][i]), float(r["obj"][i]), float(r["primal_obj"][i]),
                                       int(r["iters"][i])))
-                    key, kind = self.running.pop((name, slot))
+                    key, kind, depth, wp = self.running.pop((name, slot))
+                    self.busy[name] -= 1
                     self.kinds.append((name, kind))
+                    self.depth.append((depth, wp))
                     self.where[(name, key)] = slot
                     self.held[(name, slot)] = key
-                    self.free[name].append(slot)
+                    k = self.kids.get(key[1], 0)
+                    if k > 0:                    # children to come: park the state
+                        self.kids_left[(name, key)] = k
+                        self.parked[name][slot] = key
+                    else:
+                        self.free[name].append(slot)
             self._refill()
 
 
@@ -582,9 +616,10 @@ def main():
     payload = synthetic_payload(N, F, seed=a.seed)
     data = data_to_solver_input(payload, with_db=False)
     alpha = payload["solver"]["args"]["alpha"]
-    root = B
+    park = max(0, a.park)
+    root = B + park          # (slots 0 .. B + park - 1: the streams' working and parking slots)
     t_build = time.perf_counter()
-    m = LPModel(data, "MinDelayAndUtilization", step=1, alpha=alpha, max_batch=B + 1)
+    m = LPModel(data, "MinDelayAndUtilization", step=1, alpha=alpha, max_batch=root + 1)
     log(f"rank {rank}: model {N}x{F}: R={m.info.n_rows} rows, P={m.info.x_entries} routing entries, "
         f"built in {time.perf_counter() - t_build:.1f}s")
     P = m.info.x_entries
@@ -622,7 +657,7 @@ def main():
             # the facility relaxation (the product's bound model) and its root, stopped as the product's is:
             # bound converged (bound_res 1e-2, gap_tol 1e-4) or the root budget (core/engine/bnb.py _submit)
             from core.engine.lp import RELAX_FACILITY
-            bm = LPModel(data, "MinDelayAndUtilization", step=1, alpha=alpha, max_batch=B + 1,
+            bm = LPModel(data, "MinDelayAndUtilization", step=1, alpha=alpha, max_batch=root + 1,
                          relaxation=RELAX_FACILITY)
             t_fr = time.perf_counter()
             fr = bm.solve([root], tol=a.tol, max_iters=a.root_max_iters, check_every=a.root_check_every,
@@ -664,6 +699,22 @@ def main():
         st = m.stats()
         util = n_it / max(1, st["lp_iterations"])       # this rank's LP iterations / slot-iterations run
         iq = [int(v) for v in np.percentile([r[3] for r in res], [50, 90, 100])] if res else [0, 0, 0]
+        split = None
+        dep = getattr(stream, "depth", None)
+        if dep is not None and len(dep) >= len(stream.done):
+            # iterations per node LP by warm-start source (parent's parked state vs the root's) and by depth
+            dd = dep[i0:]
+            split = {}
+            for tag, sel in (("parent", lambda d_, w_: w_), ("root", lambda d_, w_: not w_)):
+                its = [r[3] for r, (d_, w_) in zip(res, dd) if sel(d_, w_)]
+                ok_ = [r[0] == LP_OPTIMAL for r, (d_, w_) in zip(res, dd) if sel(d_, w_)]
+                split[tag] = {"lps": len(its), "mean_iters": float(np.mean(its)) if its else None,
+                              "certified_share": float(np.mean(ok_)) if ok_ else None}
+            for lo_, hi_ in ((0, 10), (10, 20), (20, 30), (30, 1000)):
+                for tag in ("parent", "root"):
+                    its = [r[3] for r, (d_, w_) in zip(res, dd) if lo_ <= d_ < hi_ and w_ == (tag == "parent")]
+                    split[f"depth{lo_}-{hi_ - 1}_{tag}"] = ({"lps": len(its), "mean_iters": float(np.mean(its))}
+                                                           if its else None)
         tot = torch.tensor([wall, n_ok, n_it, gmax, len(res), n_first, n_res], dtype=torch.float64, device=dev)
         if dist:
             mx = tot.clone()
@@ -674,7 +725,7 @@ def main():
         wall, n_ok, n_it, gmax, n_done, n_first, n_res = (float(t) for t in tot.tolist())
         return {"wall": wall, "certified": int(n_ok), "completed": int(n_done), "iterations": int(n_it),
                 "gmax": gmax, "first_check_certified": int(n_first), "resolved": int(n_res), "iters_p50_p90_max": iq,
-                "util": util, "stats": st}
+                "util": util, "stats": st, "warm_split_rank0": split}
 
     if a.warmup > 0:
         stream.drain(a.warmup * B)
@@ -770,6 +821,7 @@ def main():
                "resolved": prim["resolved"], "resolved_lp_per_s": prim["resolved"] / wall,
                "first_check_certified_share": prim["first_check_certified"] / max(1, n_done),
                "warm_from_parent_rank0": getattr(stream, "warm_parent", None),
+               "park_slots": a.park, "iters_by_warm_source_rank0": prim["warm_split_rank0"],
                "mean_iters": n_it / max(1, n_done), "iters_p50_p90_max": iq,
                "slot_utilisation_rank0": util,
                "root_obj": root_obj, "root_iters": root_iters, "root_seconds": root_seconds,

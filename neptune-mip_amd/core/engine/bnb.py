@@ -153,7 +153,7 @@ class BranchAndBound:
                  seed_leaves=None, integer_bound=None, improve=None, repair=None, node_bound_res=1e-2,
                  retry_res=math.inf, unit_flow_leaves=True, node_max_iters=None, bound_lp=None, bound_gap=1e-4,
                  trace=None, rebalance_every=8, primal=None, primal_every=0,
-                 leaf_routing_warm=False, root_check_every=64):
+                 leaf_routing_warm=False, root_check_every=64, objective_integral=False):
         self.lp = lp
         self.two = bound_lp is not None
         self.N, self.F = lp.N, lp.F
@@ -194,6 +194,10 @@ class BranchAndBound:
         self.root_slot = lp.max_batch - 1
         self.inc_slot = lp.max_batch - 2
         self.tol, self.gap, self.max_iters = tol, gap, max_iters
+        # every integral point has an integral objective (step 2's disruption objective, objectives.py:55-63;
+        # step-1 MinUtilization's node count): a node whose valid bound exceeds incumbent - 1 holds no better
+        # point, so it is pruned (SCIP's objective-integrality pruning)
+        self.objective_integral = bool(objective_integral)
         self.root_max_iters = max(max_iters, root_max_iters)
         self.check_every = check_every
         # the final incumbent's LP is re-solved (warm, from its own state) at polish_tol, so the
@@ -233,7 +237,13 @@ class BranchAndBound:
 
     # ---------------------------------------------------------------------------------------
     def _gap_abs(self, inc):
-        return self.gap * max(1.0, abs(inc)) if math.isfinite(inc) else 0.0
+        if not math.isfinite(inc):
+            return 0.0
+        g = self.gap * max(1.0, abs(inc))
+        if self.objective_integral:
+            # bound >= inc - 1 + delta prunes; delta covers the fp64 error of a Lagrangian bound of this size
+            g = max(g, 1.0 - min(0.5, 1e-6 + 1e-9 * abs(inc)))
+        return g
 
     def _ibound(self, idx, val):
         return -math.inf if self.integer_bound is None else float(self.integer_bound(idx, val))

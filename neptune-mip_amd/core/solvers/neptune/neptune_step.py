@@ -99,6 +99,12 @@ class NeptuneStepBase(Solver):
         fixings (+inf: none exists), or None."""
         return None
 
+    def objective_integral(self):
+        """Every integral point of the step model has an integral objective: step-1 MinUtilization (sum n,
+        objectives.py:24-27) and every step 2 (minimize_disruption, objectives.py:55-63: integer weights on
+        binaries and integers)."""
+        return self.step_id() != _lp.STEP1 or self.VARIANT == "MinUtilization"
+
     def objective_weights(self):
         """(cost per open node, coefficient of sum W D of the routing) of the step-1 objective, or None."""
         return None
@@ -259,7 +265,8 @@ class NeptuneStepBase(Solver):
                   improve=self.improve(layout), repair=self.routing_repair(layout),
                   node_bound_res=self.node_bound_res, unit_flow_leaves=self.unit_flow_leaves,
                   node_max_iters=max(1, int(self.lp_max_iters * self.node_iters_fraction)),
-                  bound_lp=bmodel, primal=self.primal_heuristic(layout, _row_map(model)))
+                  bound_lp=bmodel, primal=self.primal_heuristic(layout, _row_map(model)),
+                  objective_integral=self.objective_integral())
         kw.update(overrides)
         return BranchAndBound(model, data.workload_matrix, data.function_memory_matrix, data.node_memory_matrix, **kw)
 
@@ -537,6 +544,15 @@ class NeptuneStep2Base(NeptuneStepBase):
                 free = np.sort(keep[~opened & ~closed])[::-1]
                 best = float(keep[opened].sum()) + float(free[:max(0, Kint - int(opened.sum()))].sum())
                 R_lb = max(R_lb, O - best)
+                # additions: a function with no placement fixed open needs one, and it costs no addition only
+                # on an open node where it has an old placement (not closed) — at most K nodes hold those, so
+                # at most the K best nodes' counts of such functions (the forced-open ones included) avoid one
+                freef = ~one.reshape(F, N).any(axis=1)
+                cov = ((old & ~zero).reshape(F, N) & freef[:, None]).sum(axis=0).astype(np.float64)
+                cov[closed] = 0.0
+                rest = np.sort(cov[~opened & ~closed])[::-1]
+                cover = float(cov[opened].sum()) + float(rest[:max(0, Kint - int(opened.sum()))].sum())
+                A = max(A, add_fixed + max(0.0, float(freef.sum()) - cover))
             if create:
                 if FN - float(zero.sum()) < O:
                     return math.inf
@@ -544,8 +560,11 @@ class NeptuneStep2Base(NeptuneStepBase):
             ones_f = one.reshape(F, N).sum(axis=1)
             if float(np.maximum(ones_f, 1.0).sum()) > O + 1e-9:
                 return math.inf
-            R_max = O - float((one & old).sum())
-            return (2 * w + 1) * A - R_max
+            # R = O - kept: the fixed-open old placements are kept, and so is one old placement of every function
+            # without a fixed placement that needs no addition (at most A - add_fixed of them need one)
+            nfree = float((ones_f == 0).sum())
+            kept = float((one & old).sum()) + max(0.0, nfree - (A - add_fixed))
+            return (2 * w + 1) * A - (O - kept)
         return bound
 
     def improve(self, layout, top=4):

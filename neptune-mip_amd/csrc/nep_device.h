@@ -216,6 +216,33 @@ __device__ __forceinline__ double repaired_c_base(const DeviceView &v, int slot,
   if (v.has_n) b -= repaired_node_price(v, slot, j);
   return b;
 }
+// Step 2, reduced disruption block (DeviceView::dred): c[f, j]'s own cost once moved_from /
+// moved_to / allocated / deallocated take their LP optimum given c — integral moved bounds: old = 0 ->
+// mf = max(lmf, c) (w c if lmf = 0, else the constant w), mt = lmt; old = 1 -> mt = max(lmt, 1 - c)
+// (w (1 - c) if lmt = 0, else w), mf = lmf — plus sT per unit of sum c (allocated / deallocated, dred_interval).
+// cconst: the (f, j)'s constant part of that cost (the objective and the bound add it).
+__device__ __forceinline__ double dred_cost(const DeviceView &v, const double *lb, int idx, double &cconst) {
+  const double old = -v.lo[v.dl.oD1 + idx], w = v.w_dis;
+  const double lmf = lb[v.il.omf + idx], lmt = lb[v.il.omt + idx];
+  double c;
+  if (old < 0.5) {
+    c = lmf < 0.5 ? w : 0.0;
+    cconst = w * (lmf + lmt);
+  } else {
+    c = lmt < 0.5 ? -w : 0.0;
+    cconst = w * (lmf + 1.0);
+  }
+  return c + v.sT;
+}
+// the row sum c in [L, U] of the reduced block (D4's dual): L / U from the slot's allocated / deallocated box
+__device__ __forceinline__ void dred_bounds(const DeviceView &v, const double *lb, const double *ub, double &L,
+                                            double &U) {
+  double tlo, thi;
+  dred_interval(v.sigma4, lb[v.il.oa], ub[v.il.oa], lb[v.il.od], ub[v.il.od], tlo, thi);
+  L = v.sum_old + tlo;
+  U = v.sum_old + thi;
+}
+
 // the repaired column price s*[f, j] = y1 + y2 of C1/C2 (lam: the step-2 price of sum c); pre-update
 // duals and iterate (x_pass's certificate launch, before it updates them)
 __device__ __forceinline__ double repaired_col_price(const DeviceView &v, int slot, int f, int j, double lam) {
@@ -226,6 +253,11 @@ __device__ __forceinline__ double repaired_col_price(const DeviceView &v, int sl
   const double b = repaired_c_base(v, slot, f, j), s0 = y[v.dl.o1 + idx] + y[v.dl.o2 + idx];
   const double z = zi[il.oc + idx];
   if (!v.step2) return repair_box(b, s0, z, lb[il.oc + idx], ub[il.oc + idx], v.M, v.eps, (double)v.N);
+  if (v.dred) {   // c's own (linear) cost and the row sum c's dual, on c's box (moved bounds propagated)
+    double cc;
+    const double bd = b + dred_cost(v, lb, idx, cc) - y[v.dl.oD4];
+    return repair_box(bd, s0, z, lb[il.oc + idx], ub[il.oc + idx], v.M, v.eps, (double)v.N);
+  }
   const double old = -v.lo[v.dl.oD1 + idx];
   const double clo = fmax(lb[il.oc + idx], old - ub[il.omt + idx]), chi = fmin(ub[il.oc + idx], old + ub[il.omf + idx]);
   return repair_dblock(b, s0, z, lam, old, v.cost_int[il.omf + idx], lb[il.omf + idx], v.cost_int[il.omt + idx],

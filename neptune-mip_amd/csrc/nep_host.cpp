@@ -23,6 +23,11 @@
 #include "../../include/neptune_lp.h"
 #include "nep_internal.h"
 
+#include <csignal>
+#include <dlfcn.h>
+#include <execinfo.h>
+#include <unistd.h>
+
 namespace nep {
 hipError_t launch_x_pass(const DeviceView &v, const int32_t *slots, int nslots, bool check, bool init, bool first,
                          bool plain, int it, hipStream_t s);
@@ -100,6 +105,8 @@ struct Model {
   std::vector<double> rhoL;         // fac: row scale of the x[r, j] <= c[f, j] rows, per (f, j)
   std::vector<double> capn;         // [2][N] node memory, node cores
   double alpha = 0.5, M = 1e6, eps = 1e-6, sigma4 = -1, cost_n = 0, score_n_coef = 0, w_dis = 0;
+  int dred = 0;                     // step 2: the reduced disruption block (DeviceView::dred)
+  double sT = 0, sum_old = 0;       // dred: cost per unit of T = sum c - sum old; sum of the old allocation
   int R = 0, JB = 0, CPL = 1, max_batch = 1;
   DualLayout dl{};
   IntLayout il{};
@@ -447,6 +454,19 @@ int build(Model &m, const nep_model_desc &d) {
     m.lo[dl.oD4] = m.sigma4 * sum_old;
     m.hi[dl.oS] = score_rhs;
   }
+  // Step 2, reduced disruption block: with integral moved_from / moved_to bounds the LP optimum
+  // has mf = max(lb_mf, c - old), mt = max(lb_mt, old - c) — a linear cost in c per (f, j) — and the rows
+  // D3a/D3b/D4 force (create) d = 0, a = -T or (delete) a = 0, d = T for T = sum c - sum old, i.e. a cost
+  // sT * T on an interval of T.  The iteration then carries c (and n, x) only; NEP_STEP2_FULL=1 keeps the
+  // full rows (A/B).
+  if (m.step2) {
+    const char *e = std::getenv("NEP_STEP2_FULL");
+    m.dred = !(e && std::atoi(e) != 0);
+    for (int k = 0; k < FN && m.dred; ++k)   // (mf / mt are linear in c only for a binary old allocation)
+      m.dred = d.old_allocations[k] == 0.0 || d.old_allocations[k] == 1.0;
+    m.sT = m.sigma4 > 0 ? -(m.w_dis - 1.0) : (m.w_dis + 1.0);
+    m.sum_old = sum_old;
+  }
   m.mem_f.assign(d.function_memory, d.function_memory + F);
   m.node_cost.assign(d.node_cost, d.node_cost + N);
   m.node_budget = d.node_budget;
@@ -537,40 +557,59 @@ int build(Model &m, const nep_model_desc &d) {
   for (size_t k = 0; k < (size_t)F * N && m.x_coef_nonneg; ++k)
     m.x_coef_nonneg = m.W[k] >= 0.0 && !(cpr[k] < 0.0);
 
+  // the matrix the iteration runs on: K itself, or (step 2, reduced disruption block) K without the idle
+  // rows D1/D2/D3a/D3b and with D4 as the row sum c (coefficient 1 on every c, no a / d): scaling and step
+  // size are those of the reduced LP (presolve keeps the reference rows of K)
+  Coo Kred;
+  if (m.dred) {
+    for (size_t e = 0; e < K.v.size(); ++e) {
+      const int r = K.r[e], c = K.c[e];
+      if ((r >= dl.oD1 && r < dl.oD1 + FN) || (r >= dl.oD2 && r < dl.oD2 + FN) || r == dl.oD3a || r == dl.oD3b) continue;
+      if (r == dl.oD4) {
+        if (c >= il.oc && c < il.oc + FN) Kred.add(r, c, 1.0);
+        continue;
+      }
+      Kred.add(r, c, K.v[e]);
+    }
+  }
+  const Coo &KS = m.dred ? Kred : K;
   // Ruiz equilibration (10 sweeps, inf-norm) + Pock-Chambolle (alpha = 1) on rows and the
   // non-x columns; x columns keep scale 1 so every routing row stays a plain simplex.
-  m.rho.assign(o, 1.0);
-  m.gam.assign(il.n_int, 1.0);
   // facility relaxation: the rows x[r, j] - c[f, j] <= 0 of every routing row r of f (x entry 1, unscaled;
   // c entry -gam_c): one scale per (f, j), and nrow_f entries in c[f, j]'s column
   std::vector<int> nrow_f(F, 0);
   for (int r = 0; r < m.R; ++r) nrow_f[m.row_f[r]] += 1;
   if (m.fac) m.rhoL.assign(FN, 1.0);
-  std::vector<double> rnL(m.fac ? FN : 0);
-  std::vector<double> rn(o), cn(il.n_int);
-  for (int sweep = 0; sweep < 11; ++sweep) {
-    const bool pc = sweep == 10;
-    for (int k = 0; k < o; ++k) rn[k] = pc ? m.rho[k] * xsum[k] : m.rho[k] * xmax[k];
-    std::fill(cn.begin(), cn.end(), 0.0);
-    for (size_t e = 0; e < K.v.size(); ++e) {
-      const double a = std::fabs(m.rho[K.r[e]] * K.v[e] * m.gam[K.c[e]]);
-      if (pc) { rn[K.r[e]] += a; cn[K.c[e]] += a; }
-      else { rn[K.r[e]] = std::max(rn[K.r[e]], a); cn[K.c[e]] = std::max(cn[K.c[e]], a); }
+  auto ruiz = [&](const Coo &KK, std::vector<double> &rho, std::vector<double> &gam) {
+    rho.assign(o, 1.0);
+    gam.assign(il.n_int, 1.0);
+    std::vector<double> rnL(m.fac ? FN : 0);
+    std::vector<double> rn(o), cn(il.n_int);
+    for (int sweep = 0; sweep < 11; ++sweep) {
+      const bool pc = sweep == 10;
+      for (int k = 0; k < o; ++k) rn[k] = pc ? rho[k] * xsum[k] : rho[k] * xmax[k];
+      std::fill(cn.begin(), cn.end(), 0.0);
+      for (size_t e = 0; e < KK.v.size(); ++e) {
+        const double a = std::fabs(rho[KK.r[e]] * KK.v[e] * gam[KK.c[e]]);
+        if (pc) { rn[KK.r[e]] += a; cn[KK.c[e]] += a; }
+        else { rn[KK.r[e]] = std::max(rn[KK.r[e]], a); cn[KK.c[e]] = std::max(cn[KK.c[e]], a); }
+      }
+      for (int k = 0; k < (m.fac ? FN : 0); ++k) {
+        const double gc = gam[il.oc + k], a = m.rhoL[k] * gc;
+        rnL[k] = pc ? m.rhoL[k] * (1.0 + gc) : m.rhoL[k] * std::max(1.0, gc);
+        const int f = k / N;
+        if (pc) cn[il.oc + k] += nrow_f[f] * a;
+        else cn[il.oc + k] = std::max(cn[il.oc + k], a);
+      }
+      for (int k = 0; k < o; ++k)
+        if (rn[k] > 0) rho[k] /= std::sqrt(rn[k]);
+      for (int k = 0; k < (m.fac ? FN : 0); ++k)
+        if (rnL[k] > 0) m.rhoL[k] /= std::sqrt(rnL[k]);
+      for (int k = 0; k < il.n_int; ++k)
+        if (cn[k] > 0) gam[k] /= std::sqrt(cn[k]);
     }
-    for (int k = 0; k < (m.fac ? FN : 0); ++k) {
-      const double gc = m.gam[il.oc + k], a = m.rhoL[k] * gc;
-      rnL[k] = pc ? m.rhoL[k] * (1.0 + gc) : m.rhoL[k] * std::max(1.0, gc);
-      const int f = k / N;
-      if (pc) cn[il.oc + k] += nrow_f[f] * a;
-      else cn[il.oc + k] = std::max(cn[il.oc + k], a);
-    }
-    for (int k = 0; k < o; ++k)
-      if (rn[k] > 0) m.rho[k] /= std::sqrt(rn[k]);
-    for (int k = 0; k < (m.fac ? FN : 0); ++k)
-      if (rnL[k] > 0) m.rhoL[k] /= std::sqrt(rnL[k]);
-    for (int k = 0; k < il.n_int; ++k)
-      if (cn[k] > 0) m.gam[k] /= std::sqrt(cn[k]);
-  }
+  };
+  ruiz(KS, m.rho, m.gam);
 
   // ||K̃||_2 by power iteration on K̃ᵀK̃ (structured x part + COO part)
   {
@@ -604,7 +643,7 @@ int build(Model &m, const nep_model_desc &d) {
         }
         if (m.step2) yv[dl.oS] += srow;
       }
-      for (size_t e = 0; e < K.v.size(); ++e) yv[K.r[e]] += K.v[e] * m.gam[K.c[e]] * zs[K.c[e]];
+      for (size_t e = 0; e < KS.v.size(); ++e) yv[KS.r[e]] += KS.v[e] * m.gam[KS.c[e]] * zs[KS.c[e]];
       for (int k = 0; k < o; ++k) yv[k] *= m.rho[k];
       // g = K̃ᵀ y
       for (int k = 0; k < o; ++k) yv[k] *= m.rho[k];   // now ρ y
@@ -632,7 +671,7 @@ int build(Model &m, const nep_model_desc &d) {
             gs[il.oc + k] -= m.rhoL[k] * t;
           }
         }
-      for (size_t e = 0; e < K.v.size(); ++e) gs[K.c[e]] += K.v[e] * yv[K.r[e]];
+      for (size_t e = 0; e < KS.v.size(); ++e) gs[KS.c[e]] += KS.v[e] * yv[KS.r[e]];
       for (int k = 0; k < il.n_int; ++k) gs[k] *= m.gam[k];
       double dot = 0.0;
       for (size_t k = 0; k < zx.size(); ++k) dot += zx[k] * gx[k];
@@ -659,12 +698,28 @@ int build(Model &m, const nep_model_desc &d) {
         cn2 += m.row_m[r] * cx * cx;
       }
     }
-    for (int k = 0; k < il.n_int; ++k) cn2 += std::pow(m.gam[k] * m.cost_int[k], 2);
+    for (int k = 0; k < il.n_int; ++k) {
+      double ck = m.cost_int[k];
+      if (m.dred) {   // the reduced LP's costs at natural bounds: c carries mf / mt (w, -w) and sT; the rest 0
+        ck = 0.0;
+        if (k >= il.oc && k < il.oc + FN) ck = (d.old_allocations[k - il.oc] > 0.5 ? -m.w_dis : m.w_dis) + m.sT;
+        else if (il.on >= 0 && k >= il.on) ck = m.cost_int[k];
+      }
+      cn2 += std::pow(m.gam[k] * ck, 2);
+    }
     for (int k = 0; k < o; ++k) {
+      if (m.dred && ((k >= dl.oD1 && k < dl.oD1 + FN) || (k >= dl.oD2 && k < dl.oD2 + FN) || k == dl.oD3a ||
+                     k == dl.oD3b))
+        continue;   // (idle rows of the reduced LP)
       double b = 0.0;
       if (std::isfinite(m.lo[k])) b = std::max(b, std::fabs(m.lo[k]));
       if (std::isfinite(m.hi[k])) b = std::max(b, std::fabs(m.hi[k]));
       if (m.fac && k >= dl.o3 && k < dl.o5 + N) b = m.capn[k < dl.o5 ? k - dl.o3 : N + k - dl.o5];   // (hi = 0)
+      if (m.dred && k == dl.oD4) {   // the row sum c in [L, U] at the natural allocated / deallocated bounds
+        double tlo, thi;
+        dred_interval(m.sigma4, m.nat_lb[il.oa], m.nat_ub[il.oa], m.nat_lb[il.od], m.nat_ub[il.od], tlo, thi);
+        b = std::max(std::fabs(m.sum_old + tlo), std::fabs(m.sum_old + thi));
+      }
       bn2 += std::pow(m.rho[k] * b, 2);
     }
     m.omega0 = (cn2 > 0.0 && bn2 > 0.0) ? std::sqrt(cn2) / std::sqrt(bn2) : 1.0;
@@ -700,6 +755,7 @@ int setup_device(Model &m, int max_batch, void *stream) {
   v.has_n = m.has_n; v.step2 = m.step2; v.variant = m.variant; v.fac = m.fac;
   v.M = m.M; v.eps = m.eps; v.sigma4 = m.sigma4; v.cost_n = m.cost_n; v.score_n_coef = m.score_n_coef;
   v.w_dis = m.w_dis;
+  v.dred = m.dred; v.sT = m.sT; v.sum_old = m.sum_old;
   v.dl = m.dl; v.il = m.il;
   v.rs_suff = 0.2; v.rs_nec = 0.9; v.rs_art = 0.36; v.omega_smooth = 0.5;   // necessary 0.9: DESIGN.md §4
   if (const char *e = std::getenv("NEP_RESTART")) std::sscanf(e, "%lf,%lf,%lf", &v.rs_suff, &v.rs_nec, &v.rs_art);
@@ -1216,6 +1272,7 @@ struct NodeBox {
   int t = 0;
   size_t off = 0, cnt = 0;
   bool ok = false, ex = false;
+  bool bad = false;   // reduced step 2: a fractional moved_from / moved_to bound (not representable)
 };
 
 // Presolve n nodes on the host — over the nodes in parallel when they are large (a rounding leaf at
@@ -1240,6 +1297,26 @@ static void presolve_batch(Model &m, int n, const double *lbi, const double *ubi
     for (int k = m.has_n ? m.il.on : n_fix_end; ex && k < n_fix_end; ++k)
       ex = L && U && std::max(L[k], m.nat_lb[k]) == std::min(U[k], m.nat_ub[k]);
     nb.ex = ex;
+    if (nb.ok && m.dred) {
+      // the reduced disruption block needs integral moved_from / moved_to bounds (binaries: every B&B box
+      // has them) and a non-empty interval of T = sum c - sum old (dred_interval)
+      const IntLayout &il = m.il;
+      const int FN = m.F * m.N;
+      double la = m.base_lb[il.oa], ua = m.base_ub[il.oa], ld = m.base_lb[il.od], ud = m.base_ub[il.od];
+      for (size_t q = nb.off; q < nb.off + nb.cnt; ++q) {
+        const int k = sc.ci[q];
+        if (k >= il.omf && k < il.omt + FN) {
+          if (std::floor(sc.cl[q]) != sc.cl[q] || std::floor(sc.cu[q]) != sc.cu[q]) nb.bad = true;
+        } else if (k == il.oa) {
+          la = sc.cl[q]; ua = sc.cu[q];
+        } else if (k == il.od) {
+          ld = sc.cl[q]; ud = sc.cu[q];
+        }
+      }
+      double tlo, thi;
+      dred_interval(m.sigma4, la, ua, ld, ud, tlo, thi);
+      if (tlo > thi) nb.ok = false;
+    }
   };
   const int nt = presolve_threads(m, n);
   while ((int)m.psc.size() < nt) {
@@ -1293,6 +1370,11 @@ int submit(Model &m, int n, const int32_t *slots, const double *lbi, const doubl
   HIPCHK(set_prm(m, o.tol, o.cutoff, o.gap_tol));
   std::vector<NodeBox> box;
   presolve_batch(m, n, lbi, ubi, box);
+  for (int b = 0; b < n; ++b)
+    if (box[b].bad)
+      return fail(NEP_ERR_ARG, "step-2 node box " + std::to_string(b) +
+                               ": moved_from / moved_to bounds must be integral (binary variables; NEP_STEP2_FULL=1 "
+                               "iterates the full disruption rows)");
   std::vector<int32_t> fresh, off(1, 0), exact;
   int max_chg = 0;
   for (int b = 0; b < n; ++b) {
@@ -1687,8 +1769,56 @@ extern "C" {
 int nep_api_version(void) { return NEP_API_VERSION; }
 const char *nep_last_error(void) { return g_err.c_str(); }
 
+// NEP_SEGV_TRACE=1 (debug aid, DESIGN.md §6 "PMC pass crash"): a SIGSEGV handler that prints every frame's
+// library and nearest exported symbol (dladdr) and the memory mappings around the faulting address, then
+// re-raises with the previous disposition.  Installed at the first model creation.
+static struct sigaction g_prev_segv;
+static void segv_trace(int sig, siginfo_t *si, void *ctx) {
+  void *fr[64];
+  const int n = backtrace(fr, 64);
+  char line[512];
+  int len = snprintf(line, sizeof line, "[nep] SIGSEGV at %p, %d frames\n", si ? si->si_addr : nullptr, n);
+  (void)!write(2, line, len);
+  for (int k = 0; k < n; ++k) {
+    Dl_info di{};
+    if (dladdr(fr[k], &di) && di.dli_fname) {
+      len = snprintf(line, sizeof line, "[nep]  #%d %p %s+0x%lx (%s+0x%lx)\n", k, fr[k], di.dli_fname,
+                     (unsigned long)((char *)fr[k] - (char *)di.dli_fbase), di.dli_sname ? di.dli_sname : "?",
+                     di.dli_saddr ? (unsigned long)((char *)fr[k] - (char *)di.dli_saddr) : 0ul);
+    } else {
+      len = snprintf(line, sizeof line, "[nep]  #%d %p ?\n", k, fr[k]);
+    }
+    (void)!write(2, line, len);
+  }
+  if (FILE *f = std::fopen("/proc/self/maps", "r")) {
+    const unsigned long a = (unsigned long)(si ? si->si_addr : nullptr);
+    char ml[512];
+    while (std::fgets(ml, sizeof ml, f)) {
+      unsigned long lo = 0, hi = 0;
+      if (std::sscanf(ml, "%lx-%lx", &lo, &hi) == 2 && hi + (1ul << 22) > a && lo < a + (1ul << 22))
+        (void)!write(2, ml, std::strlen(ml));
+    }
+    std::fclose(f);
+  }
+  sigaction(SIGSEGV, &g_prev_segv, nullptr);
+  raise(sig);
+  (void)ctx;
+}
+static void maybe_install_segv_trace() {
+  static bool done = false;
+  const char *e = std::getenv("NEP_SEGV_TRACE");
+  if (done || !e || std::atoi(e) == 0) return;
+  done = true;
+  struct sigaction sa{};
+  sa.sa_sigaction = segv_trace;
+  sa.sa_flags = SA_SIGINFO;
+  sigemptyset(&sa.sa_mask);
+  sigaction(SIGSEGV, &sa, &g_prev_segv);
+}
+
 int nep_model_create(const nep_model_desc *desc, int32_t max_batch, void *hip_stream, void **out_model) {
   if (!desc || !out_model) return fail(NEP_ERR_ARG, "null argument");
+  maybe_install_segv_trace();
   if (max_batch <= 0) return fail(NEP_ERR_ARG, "max_batch must be positive");
   std::unique_ptr<Model> m(new Model());
   int rc = build(*m, *desc);
@@ -1940,7 +2070,10 @@ int nep_lp_get_diag(void *model, int32_t slot, double *out16) {
   Model &m = *static_cast<Model *>(model);
   if (slot < 0 || slot >= m.max_batch) return fail(NEP_ERR_ARG, "slot out of range");
   Ctrl c;
-  HIPCHK(hipMemcpy(&c, m.v.ctrl + slot, sizeof(Ctrl), hipMemcpyDeviceToHost));
+  // read on the auxiliary stream: submits and state copies are enqueued there without a host
+  // wait, so a blocking copy on the null stream could see a slot's Ctrl before they ran
+  HIPCHK(hipMemcpyAsync(&c, m.v.ctrl + slot, sizeof(Ctrl), hipMemcpyDeviceToHost, m.aux));
+  HIPCHK(hipStreamSynchronize(m.aux));
   const double vals[16] = {c.pobj, c.lagr, c.best_lagr, c.pres, c.gap, c.omega, c.tau, c.sigma, c.eta,
                            (double)c.k, (double)c.k_since_restart, (double)c.status, (double)c.active,
                            c.last_restart_fpr, c.prev_fpr, m.sigma_max};
@@ -1953,11 +2086,14 @@ int nep_debug_state(void *model, int32_t slot, double *y, double *kz, float *kty
   Model &m = *static_cast<Model *>(model);
   if (slot < 0 || slot >= m.max_batch) return fail(NEP_ERR_ARG, "slot out of range");
   const DeviceView &v = m.v;
-  if (y) HIPCHK(hipMemcpy(y, v.y + slot * v.sdual, v.sdual * sizeof(double), hipMemcpyDeviceToHost));
-  if (kz) HIPCHK(hipMemcpy(kz, v.kz + slot * v.sdual, v.sdual * sizeof(double), hipMemcpyDeviceToHost));
-  if (kty) HIPCHK(hipMemcpy(kty, v.kty + slot * v.skty, v.skty * sizeof(float), hipMemcpyDeviceToHost));
-  if (lb) HIPCHK(hipMemcpy(lb, v.lb + slot * v.sint, v.sint * sizeof(double), hipMemcpyDeviceToHost));
-  if (ub) HIPCHK(hipMemcpy(ub, v.ub + slot * v.sint, v.sint * sizeof(double), hipMemcpyDeviceToHost));
+  // (stream-ordered behind the submits / copies on the auxiliary stream, as nep_lp_get_diag)
+  const hipMemcpyKind d2h = hipMemcpyDeviceToHost;
+  if (y) HIPCHK(hipMemcpyAsync(y, v.y + slot * v.sdual, v.sdual * sizeof(double), d2h, m.aux));
+  if (kz) HIPCHK(hipMemcpyAsync(kz, v.kz + slot * v.sdual, v.sdual * sizeof(double), d2h, m.aux));
+  if (kty) HIPCHK(hipMemcpyAsync(kty, v.kty + slot * v.skty, v.skty * sizeof(float), d2h, m.aux));
+  if (lb) HIPCHK(hipMemcpyAsync(lb, v.lb + slot * v.sint, v.sint * sizeof(double), d2h, m.aux));
+  if (ub) HIPCHK(hipMemcpyAsync(ub, v.ub + slot * v.sint, v.sint * sizeof(double), d2h, m.aux));
+  HIPCHK(hipStreamSynchronize(m.aux));
   return NEP_OK;
 }
 
@@ -1999,7 +2135,12 @@ int nep_debug_presolve(const nep_model_desc *desc, int32_t n, const double *lbi,
   std::vector<double> lb, ub;
   std::vector<uint8_t> mask;
   std::vector<NodeBox> box;
-  presolve_batch(m, n, lbi, ubi, box);   // (the submit path: in parallel for large models)
+  presolve_batch(m, n, lbi, ubi, box);
+  for (int b = 0; b < n; ++b)
+    if (box[b].bad)
+      return fail(NEP_ERR_ARG, "step-2 node box " + std::to_string(b) +
+                               ": moved_from / moved_to bounds must be integral (binary variables; NEP_STEP2_FULL=1 "
+                               "iterates the full disruption rows)");   // (the submit path: in parallel for large models)
   for (int b = 0; b < n; ++b) {
     const double *l = lbi ? lbi + b * ni : nullptr, *u = ubi ? ubi + b * ni : nullptr;
     ok_full[b] = presolve_full(m, l, u, lb, ub, mask) ? 1 : 0;

@@ -38,7 +38,32 @@
 #define NEP_SPARSE_ANCHOR 1
 #endif
 
+#if defined(__HIPCC__) || defined(__HIP__)
+#define NEP_HD __host__ __device__
+#else
+#define NEP_HD
+#endif
+
 namespace nep {
+
+// Step 2, reduced disruption block: the interval of T = sum c - sum old on which the rows D3a/D3b/D4
+// (constraints_step2.py:19-55) admit allocated / deallocated within their box, and their LP optimum on it.
+//   create (sigma4 = +1):  a <= -T, d <= T, a + d >= -T, a, d <= 0   =>  d = 0, a = -T:  T in [max(0, -ua), -la],
+//                          feasible only if ld <= 0 <= ud; cost (w - 1) a = -(w - 1) T
+//   delete (sigma4 = -1):  a <= -T, d <= T, a + d >= T,  a, d <= 0   =>  a = 0, d = T:   T in [ld, min(0, ud)],
+//                          feasible only if la <= 0 <= ua; cost (w + 1) d = (w + 1) T
+// An empty interval (lo > hi) means the box is infeasible.
+NEP_HD inline void dred_interval(double sigma4, double la, double ua, double ld, double ud, double &tlo, double &thi) {
+  if (sigma4 > 0) {
+    const bool ok = ld <= 0.0 && ud >= 0.0;
+    tlo = ok ? (-ua > 0.0 ? -ua : 0.0) : 1.0;
+    thi = ok ? -la : 0.0;
+  } else {
+    const bool ok = la <= 0.0 && ua >= 0.0;
+    tlo = ok ? ld : 1.0;
+    thi = ok ? (ud < 0.0 ? ud : 0.0) : 0.0;
+  }
+}
 
 // The Halpern anchor is always a point on the routing simplexes (it is set right after a plain
 // PDHG step, or from the initial projection), so its rows are sparse: a row keeps up to kAnchorK
@@ -130,6 +155,12 @@ struct DeviceView {
   int has_n, step2, variant;
   int fac;                               // NEP_RELAX_FACILITY model (nep_fac.hip): x <= c, c <= n, no big-M pairs
   double M, eps, sigma4, cost_n, score_n_coef, w_dis;
+  // step 2 with the disruption block reduced (DESIGN.md §4 "Step-2 reduced disruption block"): moved_from /
+  // moved_to / allocated / deallocated are not iterated — their LP optimum is a function of c (integral moved
+  // bounds: a linear cost per (f, j); allocated / deallocated: one linear cost sT per unit of T = sum c - sum
+  // old on an interval of T) — rows D1/D2/D3a/D3b are idle and D4's dual prices the row sum c in [L, U]
+  int dred;
+  double sT, sum_old;
   DualLayout dl;
   IntLayout il;
   // static

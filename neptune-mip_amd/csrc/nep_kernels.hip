@@ -251,7 +251,7 @@ void x_pass(DeviceView v, const int32_t *__restrict__ slots, int plain, int it, 
   float *lR = reinterpret_cast<float *>(lPm + NP);
   // the price of sum c the step-2 repair aims at (pre-update duals of D3a / D3b / D4)
   double lam_rep = 0.0;
-  if (CHECK && v.step2) {
+  if (CHECK && v.step2 && !v.dred) {
     double lamk[kNLam];
     dblock_lambdas(v, v.y + slot * v.sdual, lamk);
     lam_rep = repair_lambda(lamk);
@@ -437,8 +437,27 @@ void x_pass(DeviceView v, const int32_t *__restrict__ slots, int plain, int it, 
     }
     if (lane == 0) th_row[r] = theta;
     float xn[E];
+    if (CHECK && cnt_f > 0) {
+      // certificate iterations: the threshold again in fp64 over the support the fp32 search found, so the
+      // stored row — the certificate's point — sums to 1 within the fp32 rounding of its entries (C4,
+      // constraints_step1.py:27-34).  An fp32 threshold over ~N active entries leaves |sum - 1| ~ N ulps: 1.2e-5
+      // on the pooled rows of the Alibaba-shape 1024x512 models (W == 0: one row of 1024 entries per function)
+      double s64 = 0.0;
+      int c64 = 0;
 #pragma unroll
-    for (int e = 0; e < E; ++e) xn[e] = ((mbits >> e) & 1u) ? fmaxf(vv[e] - theta, 0.f) : 0.f;
+      for (int e = 0; e < E; ++e) {
+        const bool in = ((mbits >> e) & 1u) && vv[e] > theta;
+        if (in) s64 += (double)vv[e];
+        c64 += __popcll(__ballot(in));
+      }
+      s64 = wave_sum_d(s64);
+      const double th64 = c64 > 0 ? (s64 - 1.0) / (double)c64 : (double)theta;
+#pragma unroll
+      for (int e = 0; e < E; ++e) xn[e] = ((mbits >> e) & 1u) ? fmaxf((float)((double)vv[e] - th64), 0.f) : 0.f;
+    } else {
+#pragma unroll
+      for (int e = 0; e < E; ++e) xn[e] = ((mbits >> e) & 1u) ? fmaxf(vv[e] - theta, 0.f) : 0.f;
+    }
     if (CHECK && ri.src < 0) {   // the pooled row of f: its flow, for the certificate's pooled shift
 #pragma unroll
       for (int e = 0; e < E; ++e) {
@@ -621,7 +640,7 @@ void x_pass(DeviceView v, const int32_t *__restrict__ slots, int plain, int it, 
   double lamk[kNLam], dlk[kNLam], dlkr[kNLam], dtlo = 0.0, dthi = 0.0;
 #pragma unroll
   for (int q = 0; q < kNLam; ++q) { lamk[q] = 0.0; dlk[q] = dlkr[q] = 0.0; }
-  if (CHECK && v.step2) dblock_lambdas(v, y, lamk);
+  if (CHECK && v.step2 && !v.dred) dblock_lambdas(v, y, lamk);
   for (int j = threadIdx.x; j < N; j += kWave * TW) {
     float Sf = 0.f, Uf = 0.f;   // (plain iterations: Sf is the reflected column sum)
     double Sd = 0.0, Ud = 0.0;
@@ -654,7 +673,20 @@ void x_pass(DeviceView v, const int32_t *__restrict__ slots, int plain, int it, 
       y1 = y2 = y3 = y6 = y7 = 0.0;
     }
     double kty_c = -v.M * y1 - y2 + memf * y3 + y6 + y7;
-    if (CHECK) {
+    // reduced step-2 block: c's own cost (which the objective-off Lagrangian takes out of rc as well), and the
+    // row sum c's dual (D4's slot) in its reduced cost
+    double dcost = 0.0, dconst = 0.0;
+    if (__builtin_expect(v.dred, 0)) {
+      dcost = dred_cost(v, lb, idx, dconst);
+      kty_c += yD4;
+    }
+    if (CHECK && v.dred) {
+      // the bound's small-variable terms at the repaired duals, as on step 1 with c's own cost and constant
+      const double sr = lKr[j];
+      const double rcr = price_rc(repaired_c_base(v, slot, f, j) + csd * dcost - yD4, sr, v.M);
+      a.lagrR += fmin(lb[il.oc + idx] * rcr, ub[il.oc + idx] * rcr) - v.eps * fmax(sr, 0.0) + csd * dconst;
+      a.lagr += csd * dconst;
+    } else if (CHECK) {
       // the bound's small-variable terms at the repaired duals (DESIGN.md §4 "Dual repair"), and on
       // step 2 the disruption block kept exact (dblock_item) at both the PDHG and the repaired duals
       const double sr = lKr[j];
@@ -679,7 +711,7 @@ void x_pass(DeviceView v, const int32_t *__restrict__ slots, int plain, int it, 
       }
     }
     double yd1 = 0.0, yd2 = 0.0;
-    if (v.step2) {
+    if (v.step2 && !v.dred) {
       yd1 = ysrc[dl.oD1 + idx];
       yd2 = ysrc[dl.oD2 + idx];
       if (pol_enter) {   // D1/D2 rows of this f: kept, the feasibility problem's from 0
@@ -690,8 +722,10 @@ void x_pass(DeviceView v, const int32_t *__restrict__ slots, int plain, int it, 
       kty_c += -yd1 + yd2 - yD3a + yD3b + v.sigma4 * yD4;
     }
     const double c_old = NEP_INLINE_REFLECT ? zi[il.oc + idx] : 0.0;
-    const double cn = primal_step<CHECK>(v, zi, zia, lb, ub, il.oc + idx, csd * v.cost_int[il.oc + idx] - kty_c, taud,
-                                         copy_anchor, halp, lamd, a, v.step2);
+    ZPre pc = primal_pre(v, zi, zia, lb, ub, il.oc + idx, copy_anchor);
+    if (v.dred) pc.cost = dcost;
+    const double cn = primal_step_p<CHECK>(zi, zia, il.oc + idx, csd * pc.cost - kty_c, pc, taud, copy_anchor, halp,
+                                           lamd, a, v.step2 && !v.dred);
     const double c2 = 2.0 * cn - c_old;   // reflected c
     double y1n, y2n;
     if (NEP_INLINE_REFLECT) {
@@ -701,7 +735,9 @@ void x_pass(DeviceView v, const int32_t *__restrict__ slots, int plain, int it, 
       y1n = dual_step<CHECK, INIT>(v, y, ya, kz, kza, dl.o1 + idx, S - v.M * cn, y1, sigma, copy_anchor, halp, lamd, a);
       y2n = dual_step<CHECK, INIT>(v, y, ya, kz, kza, dl.o2 + idx, S - cn, y2, sigma, copy_anchor, halp, lamd, a);
     }
-    if (v.step2 && !NEP_INLINE_REFLECT) {
+    if (v.dred) {
+      // (moved_from / moved_to are not iterated: their LP optimum follows from c, the certificate below)
+    } else if (v.step2 && !NEP_INLINE_REFLECT) {
       const double mfn = primal_step<CHECK>(v, zi, zia, lb, ub, il.omf + idx, csd * v.cost_int[il.omf + idx] - yd1, taud,
                                             copy_anchor, halp, lamd, a, true);
       const double mtn = primal_step<CHECK>(v, zi, zia, lb, ub, il.omt + idx, csd * v.cost_int[il.omt + idx] - yd2, taud,
@@ -745,6 +781,10 @@ void x_pass(DeviceView v, const int32_t *__restrict__ slots, int plain, int it, 
         const double mfr = fmax(lb[il.omf + idx], cr - old), mtr = fmax(lb[il.omt + idx], old - cr);
         v.zr[slot * v.sint + il.omf + idx] = mfr;
         v.zr[slot * v.sint + il.omt + idx] = mtr;
+        if (v.dred) {   // (not iterated: the iterate carries the last certificate's values)
+          zi[il.omf + idx] = mfr;
+          zi[il.omt + idx] = mtr;
+        }
         a.res = fmax(a.res, fmax(mfr - ub[il.omf + idx], mtr - ub[il.omt + idx]));
         a.pobj += v.cost_int[il.omf + idx] * mfr + v.cost_int[il.omt + idx] * mtr;
       }
@@ -1048,7 +1088,7 @@ __global__ __launch_bounds__(256) void scalar_pass(DeviceView v, const int32_t *
   // triples, one per thread).  A vertex is accepted within 1e-9 of every half-space: accepting a
   // slightly infeasible one can only lower the minimum, so the bound stays valid.
   __shared__ double gmin[kNLam][256];
-  if (CHECK && v.step2) {
+  if (CHECK && v.step2 && !v.dred) {
     const DualLayout &dl = v.dl;
     const IntLayout &il = v.il;
     const double *lbs = v.lb + slot * v.sint, *ubs = v.ub + slot * v.sint;
@@ -1133,6 +1173,7 @@ __global__ __launch_bounds__(256) void scalar_pass(DeviceView v, const int32_t *
   a.dsy = tot[NTS + BS_DIST_Y];
   a.lagrD = tot[NTS + BS_LAGR_D];
   double score_lagr = 0.0;   // the step-2 score row's bound term (pre-update dual)
+  double dred_lagr = 0.0;    // reduced step 2: the row sum c's bound term (pre-update dual)
 
   if (v.step2) {
     const double sumc = tot[NTS + BS_SUMC_NEW];
@@ -1148,6 +1189,17 @@ __global__ __launch_bounds__(256) void scalar_pass(DeviceView v, const int32_t *
       yD3a = yb[dl.oD3a]; yD3b = yb[dl.oD3b]; yD4 = yb[dl.oD4]; yS = yb[dl.oS];
     }
     const double csd = ctrl->polish ? 0.0 : 1.0;
+    if (v.dred) {
+      // reduced disruption block: the row sum c in [L, U] (D4's dual; dred_interval), a / d not iterated
+      double L, U;
+      dred_bounds(v, lb, ub, L, U);
+      if (CHECK) dred_lagr = row_lagr(yD4, L, U);
+      DPre p = dual_pre<INIT>(v, y, ya, kz, kza, dl.oD4, copy_anchor);
+      p.y = yD4;
+      p.lo = L;
+      p.hi = U;
+      dual_step_p<CHECK, INIT>(y, ya, kz, kza, dl.oD4, sumc, p, sigma, copy_anchor, halp, lam, a);
+    } else {
     // allocated (a): D3a coef -1, D4 coef +1 ; deallocated (d): D3b coef -1, D4 coef +1
     const double an = primal_step<CHECK>(v, zi, zia, lb, ub, il.oa, csd * v.cost_int[il.oa] - (-yD3a + yD4), tau,
                                          copy_anchor, halp, lam, a, true);
@@ -1157,6 +1209,7 @@ __global__ __launch_bounds__(256) void scalar_pass(DeviceView v, const int32_t *
     dual_step<CHECK, INIT>(v, y, ya, kz, kza, dl.oD3b, sumc - dn, yD3b, sigma, copy_anchor, halp, lam, a, true);
     dual_step<CHECK, INIT>(v, y, ya, kz, kza, dl.oD4, dn + an + v.sigma4 * sumc, yD4, sigma, copy_anchor, halp, lam,
                            a, true);
+    }
     if (CHECK) score_lagr = row_lagr(yS, v.lo[dl.oS], v.hi[dl.oS]);
     dual_step<CHECK, INIT>(v, y, ya, kz, kza, dl.oS, score, yS, sigma, copy_anchor, halp, lam, a);
     float *kty = v.kty + slot * v.skty;
@@ -1198,12 +1251,16 @@ __global__ __launch_bounds__(256) void scalar_pass(DeviceView v, const int32_t *
     pobj += v.cost_int[il.oa] * ar + v.cost_int[il.od] * dr;
     v.zr[slot * v.sint + il.oa] = ar;
     v.zr[slot * v.sint + il.od] = dr;
+    if (v.dred) { zi[il.oa] = ar; zi[il.od] = dr; }   // (not iterated: the last certificate's values)
     const double score_rep = tot[TS_SCORE] + tot[NTS + BS_SCORE_N_REP];
     res = fmax(res, row_viol(score_rep, v.lo[dl.oS], v.hi[dl.oS]) / v.rownorm[dl.oS]);
   }
   // the Lagrangian with every row dualised, or (step 2) the disruption block kept exact at the best
   // of the candidate prices (both are valid bounds)
   double lagr = a.lagr + a.lagrD;
+  // reduced step 2: the block's constant -sT sum old (the (f, j) constants are in a.lagr: x_pass)
+  const double dred_k0 = (v.dred && !ctrl->polish) ? -v.sT * v.sum_old : 0.0;
+  lagr += dred_k0;
   // Infeasibility (Farkas): with the objective off the Lagrangian L0(y) is positively
   // homogeneous in y and <= 0 at every y when the LP has a feasible point; L0(y) > 0 at a sign-feasible
   // y proves the node LP infeasible (L(t y) >= t L0(y) + min cost -> +inf).  The margin is far above the
@@ -1216,7 +1273,7 @@ __global__ __launch_bounds__(256) void scalar_pass(DeviceView v, const int32_t *
   } else {
     ctrl->infeas_hits = 0;
   }
-  if (v.step2) {
+  if (v.step2 && !v.dred) {
 #pragma unroll
     for (int q = 0; q < kNLam; ++q)
       if (isfinite(gmin[q][0])) lagr = fmax(lagr, a.lagr + tot[NTS + BS_LK0 + q] + gmin[q][0]);
@@ -1224,7 +1281,9 @@ __global__ __launch_bounds__(256) void scalar_pass(DeviceView v, const int32_t *
   // ... and the same bound at the repaired duals (DESIGN.md §4 "Dual repair"): the larger one stands
   if (!v.fac) {   // (the facility relaxation has no big-M pairs to repair)
     double lr = tot[TS_LAGR_REP] + tot[NTS + BS_LAGR_REP];
-    if (v.step2) {
+    if (v.dred) {
+      lr += score_lagr + dred_lagr + dred_k0;
+    } else if (v.step2) {
       double best = -INFINITY;
 #pragma unroll
       for (int q = 0; q < kNLam; ++q)
@@ -1333,6 +1392,15 @@ __global__ __launch_bounds__(256) void scalar_pass(DeviceView v, const int32_t *
     if (!polish_now && dz > 1e-10 && dy > 1e-10) {   // (entering polishing keeps the weight)
       double nw = exp(v.omega_smooth * log(dy / dz) + (1.0 - v.omega_smooth) * log(w));
       nw = fmin(fmax(nw, ctrl->omega_lo), ctrl->omega_hi);
+      ctrl->omega = nw;
+      ctrl->tau = ctrl->eta / nw;
+      ctrl->sigma = ctrl->eta * nw;
+    } else if (!polish_now && v.dred && dz <= 1e-10 && dy > 1e-10) {
+      // reduced step 2: the primal has not moved since the last restart while the dual has — the weight is so
+      // small that every primal step lands on the same box corner (the PDLP ratio dy / dz is +inf): raise it
+      // 10x (numpy mirror, small step-2 goldens at the reduced LP's initial weight: payload.json model 1 stalled
+      // at 60k iterations with the primal static, certifies in 1217 with this rule)
+      const double nw = fmin(w * 10.0, ctrl->omega_hi);
       ctrl->omega = nw;
       ctrl->tau = ctrl->eta / nw;
       ctrl->sigma = ctrl->eta * nw;

@@ -11,7 +11,7 @@ INF = np.inf
 
 class RefModel:
     def __init__(self, data, variant, step=1, alpha=0.5, soften_step1_sol=1.3, max_score=0.0,
-                 prev_network_delay=0.0, M=1e6, eps=1e-6):
+                 prev_network_delay=0.0, M=1e6, eps=1e-6, dred=None):
         D = np.asarray(data.node_delay_matrix, float)
         W = np.asarray(data.workload_matrix, float)
         F, N = W.shape
@@ -190,6 +190,22 @@ class RefModel:
         rn = np.where(np.isfinite(hi), np.maximum(rn, np.abs(np.where(np.isfinite(hi), hi, 0))), rn)
         np.maximum.at(rn, self.Kr, np.abs(self.Kv))
         self.rownorm = rn
+        # step 2, reduced disruption block (nep_host.cpp build): mf / mt / a / d follow from c, the
+        # iteration runs on K without D1/D2/D3a/D3b and with D4 as the row sum c (coefficient 1 on every c)
+        self.old = old
+        self.dred = bool(self.step2 and np.isin(old, (0.0, 1.0)).all()) if dred is None else bool(dred and self.step2)
+        self.sT = 0.0
+        if self.dred:
+            self.sT = -(w - 1) if self.sigma4 > 0 else (w + 1)
+            idle = np.zeros(o, bool)
+            idle[self.oD1:self.oD1 + FN] = idle[self.oD2:self.oD2 + FN] = True
+            idle[[self.oD3a, self.oD3b]] = True
+            keep = ~idle[self.Kr]
+            keep &= ~((self.Kr == self.oD4) & ((self.Kc < self.oc) | (self.Kc >= self.oc + FN)))
+            self.Kr, self.Kc, self.Kv = self.Kr[keep], self.Kc[keep], self.Kv[keep]
+            self.Kv = np.where(self.Kr == self.oD4, 1.0, self.Kv)
+            lo[idle] = -INF
+            hi[idle] = INF
         rho = np.ones(o)
         gam = np.ones(self.n_int)
         for sweep in range(11):
@@ -212,10 +228,35 @@ class RefModel:
         self.eta = 0.95 / self.sigma_max
         # initial primal weight ||c~|| / ||b~|| (scaled space), as nep_host.cpp build()
         cx = self.row_wobj[:, None] * np.where(self.row_src[:, None] >= 0, D[np.maximum(self.row_src, 0)], 0.0)
-        cn2 = (self.row_m[:, None] * cx * cx).sum() + ((gam * self.cost_int) ** 2).sum()
+        # (reduced step 2: the reduced LP's costs and row bounds at natural bounds, as nep_host.cpp build)
+        ci = self.cost_int
+        if self.dred:
+            ci, _, self.lo[self.oD4], self.hi[self.oD4] = self.dred_terms(self.nat_lb, self.nat_ub)
+        cn2 = (self.row_m[:, None] * cx * cx).sum() + ((gam * ci) ** 2).sum()
         bmag = np.maximum(np.where(np.isfinite(lo), np.abs(lo), 0.0), np.where(np.isfinite(hi), np.abs(hi), 0.0))
         bn2 = ((rho * bmag) ** 2).sum()
         self.omega0 = float(np.sqrt(cn2) / np.sqrt(bn2)) if cn2 > 0 and bn2 > 0 else 1.0
+
+    def dred_terms(self, lb, ub):
+        """Reduced step 2 at a box: the iteration's costs (c: its own linear cost, mf / mt / a / d: 0), the
+        objective's constant and the row sum c's bounds [L, U] (nep_device.h dred_cost / dred_bounds)."""
+        FN, w = self.F * self.N, float(self.F * self.N)
+        lmf, lmt = lb[self.omf:self.omf + FN], lb[self.omt:self.omt + FN]
+        old0 = self.old < 0.5
+        cost = self.cost_int.copy()
+        cost[self.omf:self.omt + FN] = 0.0
+        cost[self.oa] = cost[self.od] = 0.0
+        cost[self.oc:self.oc + FN] = np.where(old0, np.where(lmf < 0.5, w, 0.0), np.where(lmt < 0.5, -w, 0.0)) + self.sT
+        const = float(np.where(old0, w * (lmf + lmt), w * (lmf + 1.0)).sum()) - self.sT * self.old.sum()
+        la, ua, ld, ud = lb[self.oa], ub[self.oa], lb[self.od], ub[self.od]
+        if self.sigma4 > 0:
+            ok = ld <= 0 <= ud
+            tlo, thi = (max(0.0, -ua), -la) if ok else (1.0, 0.0)
+        else:
+            ok = la <= 0 <= ua
+            tlo, thi = (ld, min(0.0, ud)) if ok else (1.0, 0.0)
+        so = self.old.sum()
+        return cost, const, so + tlo, so + thi
 
     def _score_coef(self, D):
         out = np.zeros((self.R, self.N))
@@ -308,6 +349,9 @@ def solve(m, lbi=None, ubi=None, tol=1e-7, max_iters=100000, check_every=64, ver
         return dict(status=2, obj=INF, pobj=np.nan, iters=0)
     mask = fmask[m.row_f]
     ce = check_every
+    cost_int, const = m.cost_int, 0.0
+    if m.dred:
+        cost_int, const, m.lo[m.oD4], m.hi[m.oD4] = m.dred_terms(lb, ub)
     x = proj_simplex_rows(np.zeros((m.R, m.N)), mask)
     z = np.clip(np.zeros(m.n_int), lb, ub)
     y = np.zeros(m.n_dual)
@@ -331,7 +375,7 @@ def solve(m, lbi=None, ubi=None, tol=1e-7, max_iters=100000, check_every=64, ver
             tau, sig = eta / omega, eta * omega
             gx, gz = m.KT(y)
             rcx = cost_x - gx
-            rcz = m.cost_int - gz
+            rcz = cost_int - gz
             xn = proj_simplex_rows(x - tau * rcx, mask)
             zn = np.clip(z - tau * m.gam ** 2 * rcz, lb, ub)
             act = m.K(xn, zn)
@@ -347,8 +391,8 @@ def solve(m, lbi=None, ubi=None, tol=1e-7, max_iters=100000, check_every=64, ver
                 with np.errstate(invalid="ignore"):
                     rl = np.where(y > 0, np.where(np.isfinite(m.lo), y * m.lo, -INF),
                                   np.where(y < 0, np.where(np.isfinite(m.hi), y * m.hi, -INF), 0.0))
-                lag += rl.sum()
-                pobj = (cost_x * xn).sum() + (m.cost_int * zn).sum()
+                lag += rl.sum() + const
+                pobj = (cost_x * xn).sum() + (cost_int * zn).sum() + const
                 viol = np.maximum(np.maximum(m.lo - act, act - m.hi), 0.0) / m.rownorm
                 res = viol.max()
                 mvz = ((xn - x) ** 2).sum() + (((zn - z) / m.gam) ** 2).sum()
@@ -386,6 +430,8 @@ def solve(m, lbi=None, ubi=None, tol=1e-7, max_iters=100000, check_every=64, ver
                     dz, dy = np.sqrt(dsz), np.sqrt(dsy)
                     if dz > 1e-10 and dy > 1e-10:
                         omega = float(np.clip(np.exp(0.5 * np.log(dy / dz) + 0.5 * np.log(omega)), om_lo, om_hi))
+                    elif m.dred and dy > 1e-10:      # (reduced step 2: primal static -> weight x10, scalar_pass)
+                        omega = float(min(omega * 10.0, om_hi))
                     restart_pending = True
                     k_since = 0
                     ks_base = -1

@@ -56,8 +56,10 @@ def test_host_build_matches_mirror(name, k):
     np.testing.assert_allclose(got["rho"], ref.rho, rtol=1e-10)
     np.testing.assert_allclose(got["gam"], ref.gam, rtol=1e-10)
     np.testing.assert_allclose(got["rownorm"], ref.rownorm, rtol=1e-12)
-    # power iteration from different random starts: same operator norm to a few 1e-3
-    assert abs(got["eta"] / ref.eta - 1.0) < 5e-3
+    # power iteration from different random starts (60 steps each): the same operator norm within 1 % (the
+    # step size eta = 0.95 / ||K~|| keeps 5 % of headroom; the reduced step-2 operator's top singular values
+    # are close, so 60 steps agree to ~5e-3 there)
+    assert abs(got["eta"] / ref.eta - 1.0) < 1e-2
 
 
 @pytest.mark.parametrize("name,k", CASES)

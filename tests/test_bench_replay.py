@@ -79,3 +79,47 @@ def test_replay_reference_and_native(name):
         elif st1 != LP_INFEASIBLE:
             assert o1 >= o0 - 1e-7 * max(1.0, abs(o0)), (e, o0, o1)
     assert math.isfinite(sum(r[1] for r in vals[False] if r[0] == LP_OPTIMAL))
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_replay_parks_parent_states(name):
+    """--park: a finished node whose children are still to come keeps its slot (its state parked) beyond the
+    `batch` LPs in flight, so more nodes warm-start from their own parent; every LP still completes once, at
+    most `batch` at a time, and the values are those of the unparked replay (the oracle solves each box from
+    scratch, so only the slot bookkeeping differs)."""
+    import bench
+    from core.engine.bnb import BranchAndBound
+    from core.utils import data_to_solver_input
+    from oracle_lp import StreamingOracleLP
+    p = payload(name)
+    data = data_to_solver_input(p, workload_coeff=p.get("workload_coeff", 1), with_db=False)
+    variant = VARIANT[p["solver"]["type"]]
+    alpha = p["solver"].get("args", {}).get("alpha", 0.5)
+    N, F = len(data.nodes), len(data.functions)
+    trace = []
+    lp = StreamingOracleLP(data, variant, step=1, max_batch=6, alpha=alpha)
+    blp = StreamingOracleLP(data, variant, step=1, max_batch=5, alpha=alpha, relaxation=1)
+    BranchAndBound(lp, data.workload_matrix, data.function_memory_matrix, data.node_memory_matrix, batch=4,
+                   node_limit=20000, bound_lp=blp, trace=trace).solve()
+    body = [e for e in trace if e["parent"] is not None]
+    out = {}
+    for park in (0, 8):
+        a = types.SimpleNamespace(batch=2, tol=1e-6, max_iters=4096, check_every=12, warm_omega_floor=0.0,
+                                  functions=F, nodes=N, park=park)
+        ref = StreamingOracleLP(data, variant, step=1, max_batch=2 + park + 1, alpha=alpha)
+        ref.solve([2 + park])
+        s = bench.ReplayStream({"leaf": (ref, 2 + park)}, a, 0, 1, {"lps": trace})
+        peak = [0]
+        orig = ref.submit
+
+        def submit(*args, **kw):
+            r = orig(*args, **kw)
+            peak[0] = max(peak[0], ref.active())
+            return r
+        ref.submit = submit
+        s.drain(len(body))
+        assert len(s.done) == len(body) and peak[0] <= 2
+        assert len(s.depth) == len(s.done)
+        out[park] = s
+    assert out[8].warm_parent >= out[0].warm_parent
+    assert sorted(r[1] for r in out[8].done) == sorted(r[1] for r in out[0].done)

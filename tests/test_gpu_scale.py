@@ -38,30 +38,12 @@ def _solve_case(c, tol=SOLVE_TOL):
     return m, rr, res
 
 
-# step-2 cases whose LPs PDHG does not certify at 1e-6 within the budget (DESIGN.md §4 'Known limit',
-# tools/step2_split_probe.py): case -> (largest bound gap measured, why).  Their bounds must stay valid
-# and within that gap; the test then reports XFAIL, not a pass.  Every other LP must certify.
-KNOWN_UNCERTIFIED = {
-    "syn64x32_MDU_s2delete": (1e-5, "the routing x stalls 1.2e-2 above the optimum (no small-block repair "
-                                    "closes it: best objective over (c, moved, a, d, n) at that x is the same)"),
-    "syn64x32_MDU_s2create": (3e-4, "the Lagrangian bound stalls below the optimum 2.13e-4 (the 1/M-priced "
-                                    "routing flow and its C5 duals are not resolved)"),
-}
-
-
-def _check_lp(c, what, st, obj, iters, ref, known):
-    """Certified and within 1e-6 of HiGHS; or, for a KNOWN_UNCERTIFIED case, a VALID bound (<= HiGHS
-    + 1e-6) within the case's recorded gap — collected in `known` (never a B&B incumbent)."""
-    from core.engine.lp import LP_ITERATION_LIMIT, LP_OPTIMAL
-    if st == LP_OPTIMAL:
-        assert gap(obj, ref) <= TOL, f"{what}: {obj} vs HiGHS {ref}"
-        return
-    assert c["name"] in KNOWN_UNCERTIFIED, f"{what}: status {st} after {iters} iterations (HiGHS {ref})"
-    assert st == LP_ITERATION_LIMIT, f"{what}: status {st}"
-    assert obj <= ref + TOL * max(1.0, abs(ref)), f"{what}: bound {obj} above the LP value {ref}"
-    assert gap(obj, ref) <= KNOWN_UNCERTIFIED[c["name"]][0], f"{what}: bound {obj} vs HiGHS {ref}"
-    known.append(f"{what} gap {gap(obj, ref):.2e}")
-    print(f"UNCERTIFIED step-2 LP {what}: bound {obj} (HiGHS {ref}, gap {gap(obj, ref):.2e}) after {iters} iterations")
+def _check_lp(what, st, obj, iters, ref):
+    """Certified (NEP_LP_OPTIMAL) and within 1e-6 of HiGHS.  (Round 4 listed two 64x32 step-2 models whose LPs
+    did not certify, KNOWN_UNCERTIFIED; the reduced disruption block certifies them)"""
+    from core.engine.lp import LP_OPTIMAL
+    assert st == LP_OPTIMAL, f"{what}: status {st} after {iters} iterations (HiGHS {ref})"
+    assert gap(obj, ref) <= TOL, f"{what}: {obj} vs HiGHS {ref}"
 
 
 @pytest.mark.parametrize("name", sorted(CASES))
@@ -69,21 +51,17 @@ def test_scale_parity(name):
     from core.engine.lp import LP_OPTIMAL
     c = dict(CASES[name], name=name)
     m, rr, res = _solve_case(c)
-    known = []
     try:
-        ref = c["root"]["lp_objective"]
-        _check_lp(c, "root", int(rr["status"][0]), float(rr["obj"][0]), rr["iters"][0], ref, known)
+        _check_lp("root", int(rr["status"][0]), float(rr["obj"][0]), rr["iters"][0], c["root"]["lp_objective"])
         for b, nd in enumerate(c["nodes"]):
             st, obj = int(res["status"][b]), float(res["obj"][b])
             if nd["lp_objective"] is None:
                 assert st != LP_OPTIMAL, f"node {b}: HiGHS infeasible, engine optimal {obj}"
                 continue
-            _check_lp(c, f"node {b}", st, obj, res["iters"][b], nd["lp_objective"], known)
+            _check_lp(f"node {b}", st, obj, res["iters"][b], nd["lp_objective"])
         print(f"{name}: root {rr['iters'][0]} iterations, nodes {res['iters'].tolist()}")
     finally:
         m.close()
-    if known:
-        pytest.xfail(f"uncertified step-2 LPs ({KNOWN_UNCERTIFIED[name][1]}): " + ", ".join(known))
 
 
 def _full_size_check(payload, variant, fixings=0, seed=0):

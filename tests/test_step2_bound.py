@@ -130,14 +130,14 @@ def test_step2_relocation_prices_exactly(mode, seed):
 
 
 @pytest.mark.parametrize("mode", ["delete", "create"])
-@pytest.mark.parametrize("seed", range(4))
+@pytest.mark.parametrize("seed", range(16))
 def test_step2_integer_bound_with_node_cap(mode, seed):
     """MinUtilization step 2: at most K = max_score * soften nodes open (constraints_step2.py:71-73).
     Brute force over binary c (n = any c per node, n fixings respected): the bound never exceeds the
     best completion of a node's c / n fixings and is +inf when no completion exists."""
     from core.solvers.neptune.neptune_step import NeptuneStep2MinUtilization
     rng = np.random.default_rng(100 + seed)
-    F, N = 2, 4
+    F, N = (2, 4) if seed < 8 else (3, 4)     # (round 5: the K-node cover bound on additions, kept old placements)
     FN = F * N
     old = (rng.random(FN) < 0.45).astype(int)
     s = NeptuneStep2MinUtilization.__new__(NeptuneStep2MinUtilization)

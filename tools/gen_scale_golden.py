@@ -44,6 +44,12 @@ def cases():
     for mode, step in (("create", 3), ("delete", 2)):
         out.append(dict(name=f"syn64x32_MDU_s2{mode}", kind="synthetic", N=64, F=32, seed=0,
                         variant="MinDelayAndUtilization", step=step, mode=mode, max_score=0.05, children=4))
+        # round 5: more step-2 models (the reduced disruption block) — MinUtilization at 64x32 and
+        # MinDelayAndUtilization at 128x64, seed 1
+        out.append(dict(name=f"syn64x32_MU_s2{mode}", kind="synthetic", N=64, F=32, seed=0,
+                        variant="MinUtilization", step=step, mode=mode, max_score=8.0, children=4))
+        out.append(dict(name=f"syn128x64_MDU_s2{mode}", kind="synthetic", N=128, F=64, seed=1,
+                        variant="MinDelayAndUtilization", step=step, mode=mode, max_score=2.0, children=4))
     for t, v in (("NeptuneMinDelayAndUtilization", "MinDelayAndUtilization"), ("NeptuneMinDelay", "MinDelay"),
                  ("NeptuneMinUtilization", "MinUtilization")):
         out.append(dict(name=f"alibaba_{v}_s1", kind="alibaba", input=f"alibaba_{t}", variant=v, step=1, children=6))

@@ -38,10 +38,14 @@ for r in "$@"; do
       python3 tools/prof_summary.py /tmp/prof > "$O/kernel_stats_by_slots.csv"; cp /tmp/prof/*/*stats.csv "$O/" 2>/dev/null
       head -12 "$O/kernel_stats_by_slots.csv" | cut -c1-160 ;;
     traffic)
-      step pmc_fetch 120 rocprofv3 --pmc FETCH_SIZE -d /tmp/pmc_fetch -o run -- python3 tools/traffic.py run
-      step pmc_write 120 rocprofv3 --pmc WRITE_SIZE -d /tmp/pmc_write -o run -- python3 tools/traffic.py run
+      # (ROC_AQL_QUEUE_SIZE: the default 16384-packet HSA queue crashes rocprofiler-sdk's --pmc queue intercept,
+      # which reads a packet header one past the ring's end; DESIGN.md §6 "PMC pass crash")
+      export ROC_AQL_QUEUE_SIZE=65536
+      step pmc_fetch 240 rocprofv3 --pmc FETCH_SIZE -d /tmp/pmc_fetch -o run -- python3 tools/traffic.py run
+      step pmc_write 240 rocprofv3 --pmc WRITE_SIZE -d /tmp/pmc_write -o run -- python3 tools/traffic.py run
       python3 tools/traffic.py summarize /tmp/pmc_fetch /tmp/pmc_write > "$O/traffic.json"; cat "$O/traffic.json" ;;
     sq)
+      export ROC_AQL_QUEUE_SIZE=65536
       step pmc_sq 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU -d /tmp/pmc_sq -o run -- python3 tools/traffic.py run
       python3 tools/traffic.py sq /tmp/pmc_sq > "$O/sq.json"; cat "$O/sq.json" ;;
     probe:*) a=${r#probe:}; step probe 600 python -u tools/step2_probe.py ${a//,/ } ;;

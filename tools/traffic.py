@@ -7,11 +7,11 @@ On the GPU box, one counter per pass (FETCH_SIZE and WRITE_SIZE do not fit one T
 Then (anywhere):
   python3 tools/traffic.py summarize gpurun_out/pmc_fetch gpurun_out/pmc_write > profiles/traffic.json
 
-`run` builds bench.py's default model (same generator, seed, batch), starts `batch` node LPs on the
-first boxes of the bench's replay stream (tests/golden/bnb_trace_*.json.gz), cold (no root solve: a
-solve_batch of the lone root crashed rocprofv3's --pmc pass in round 4), and runs 4 blocks of PDHG
-iterations: a few hundred dispatches, x_pass steady-state launches with all `batch` LPs active, as in the
-bench's timed region.  Run it with NEP_AUX_PRIORITY=0.  `summarize` averages the counters
+`run` builds bench.py's default model (same generator, seed, batch), solves its root LP, starts `batch`
+node LPs on the first boxes of the bench's replay stream (tests/golden/bnb_trace_*.json.gz) warm from the
+root's state as the replay does, and runs 4 blocks of PDHG iterations: x_pass steady-state launches with all
+`batch` LPs active, as in the bench's timed region (`run cold`: no root solve, the nodes cold — the round-4
+workaround for the SIGSEGV of the first --pmc pass, DESIGN.md §6 "PMC pass crash").  `summarize` averages the counters
 over the steady-state x_pass launches (x_pass<CPL, false, false>, full grid) and converts them:
 FETCH_SIZE and WRITE_SIZE are KiB (rocprofiler-sdk derived_counters.xml); FETCH_SIZE is doubled for
 wide streaming reads on gfx950 (MI355X_MICROARCH.md, HBM).
@@ -35,14 +35,22 @@ def run():
     a = bench.parse([])
     p = synthetic_payload(a.nodes, a.functions, seed=a.seed)
     d = data_to_solver_input(p, with_db=False)
-    m = LPModel(d, "MinDelayAndUtilization", step=1, alpha=p["solver"]["args"]["alpha"], max_batch=a.batch)
+    cold = len(sys.argv) > 2 and sys.argv[2] == "cold"
+    m = LPModel(d, "MinDelayAndUtilization", step=1, alpha=p["solver"]["args"]["alpha"], max_batch=a.batch + 1)
+    root = a.batch
+    if not cold:
+        m.solve([root], tol=a.tol, max_iters=a.root_max_iters, check_every=a.root_check_every)
     with gzip.open(bench.trace_path(a), "rt") as fh:
         trace = json.load(fh)
-    rs = bench.ReplayStream({"leaf": (m, 0)}, a, 0, 1, trace)
+    rs = bench.ReplayStream({"leaf": (m, root)}, a, 0, 1, trace)
     boxes = [rs._box(m, e) for e in rs.lps[:a.batch]]
     lb = np.array([b[0] for b in boxes])
     ub = np.array([b[1] for b in boxes])
-    m.submit(np.arange(a.batch), lb, ub, tol=a.tol, max_iters=a.max_iters, check_every=a.check_every)
+    if not cold:
+        for s in range(a.batch):
+            m.copy_state(root, s)
+    m.submit(np.arange(a.batch), lb, ub, tol=a.tol, max_iters=a.max_iters, check_every=a.check_every,
+             warm_start=not cold)
     for _ in range(4):
         m.advance(0)
     print(json.dumps({"workload": bench.workload_name(a, "replay"), "active": m.active(), "P": m.info.x_entries}))
