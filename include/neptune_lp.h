@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define NEP_API_VERSION 8
+#define NEP_API_VERSION 9
 
 /* variants: neptune.py:41-66 (NeptuneMinDelay / MinUtilization / MinDelayAndUtilization) */
 enum { NEP_MIN_DELAY = 0, NEP_MIN_UTILIZATION = 1, NEP_MIN_DELAY_AND_UTILIZATION = 2 };
@@ -91,6 +91,10 @@ typedef struct {
   const double *max_delay;     /* [F] max_delay_matrix (input_to_data.py:136: 1000) */
   const double *old_allocations; /* [F*N] step 2 only (0/1) */
   int32_t relaxation;          /* API 7: NEP_RELAX_REFERENCE (0) or NEP_RELAX_FACILITY */
+  int32_t device_inputs;       /* API 9: 1 = every array above is DEVICE memory (e.g. the data_ptr() of contiguous
+                                  float64 PyTorch-ROCm tensors on the model's GPU); nep_model_create reads the
+                                  O(F N + N^2) instance from there and builds the model (scaling on the host, the
+                                  step size on the device).  0 = host arrays (nep_debug_* take host arrays only) */
 } nep_model_desc;
 
 typedef struct {

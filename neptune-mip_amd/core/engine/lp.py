@@ -18,7 +18,7 @@ STEP1, STEP2_DELETE, STEP2_CREATE = 1, 2, 3
 LP_OPTIMAL, LP_ITERATION_LIMIT, LP_INFEASIBLE, LP_CUTOFF, LP_NUMERICAL, LP_BOUND = 0, 1, 2, 3, 4, 5
 VARIANTS = {"MinDelay": MIN_DELAY, "MinUtilization": MIN_UTILIZATION,
             "MinDelayAndUtilization": MIN_DELAY_AND_UTILIZATION}
-API_VERSION = 8
+API_VERSION = 9
 RELAX_REFERENCE, RELAX_FACILITY = 0, 1
 
 _dp = ctypes.POINTER(ctypes.c_double)
@@ -35,7 +35,8 @@ class ModelDesc(ctypes.Structure):
                 ("big_m", ctypes.c_double), ("epsilon", ctypes.c_double),
                 ("delay", _dp), ("workload", _dp), ("core_per_req", _dp), ("function_memory", _dp),
                 ("node_memory", _dp), ("node_cores", _dp), ("node_cost", _dp), ("node_budget", ctypes.c_double),
-                ("max_delay", _dp), ("old_allocations", _dp), ("relaxation", ctypes.c_int32)]
+                ("max_delay", _dp), ("old_allocations", _dp), ("relaxation", ctypes.c_int32),
+                ("device_inputs", ctypes.c_int32)]
 
 
 class LpOpts(ctypes.Structure):
@@ -81,6 +82,10 @@ def load_library(path=None):
     p = path or LIB_PATH
     if not os.path.exists(p):
         raise EngineUnavailable(f"MI355X LP engine not built: {p} missing (run __graft_entry__.build())")
+    # One HIP runtime per process: PyTorch-ROCm ships its own libamdhip64 (soname libamdhip64.so.7), loaded
+    # by file name.  Loaded first, it satisfies the engine's libamdhip64.so.7 dependency; loaded after the
+    # engine's /opt/rocm copy, the process holds two runtimes and the second to initialise sees no device.
+    import torch  # noqa: F401
     lib = ctypes.CDLL(p)
     vp, i32, i64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64
     pi32, pi64 = ctypes.POINTER(i32), ctypes.POINTER(i64)
@@ -206,12 +211,31 @@ def _arrays(data, N, F):
 
 
 def _desc(k, N, F, variant, step, alpha, soften, max_score, prev_delay, budget, relaxation=RELAX_REFERENCE):
+    """The model descriptor over host numpy arrays, or (API 9, device_inputs = 1) over the device memory of
+    PyTorch-ROCm tensors (instance_tensors)."""
+    dev = not isinstance(k["delay"], np.ndarray)
+
     def dp(a):   # (structure fields keep their typed pointers)
-        return a.ctypes.data_as(_dp)
+        return ctypes.cast(ctypes.c_void_p(a.data_ptr()), _dp) if dev else a.ctypes.data_as(_dp)
     return ModelDesc(N, F, variant, step, float(alpha), float(soften), float(max_score), float(prev_delay), 1e6,
                      1e-6, dp(k["delay"]), dp(k["workload"]), dp(k["cpr"]), dp(k["fmem"]), dp(k["nmem"]),
                      dp(k["ncores"]), dp(k["ncost"]), float(budget), dp(k["maxd"]), dp(k["old"]),
-                     int(relaxation))
+                     int(relaxation), 1 if dev else 0)
+
+
+def instance_tensors(data, device=None):
+    """The instance of a Data (core/utils/data.py; input_to_data.py:88-111) as contiguous float64 PyTorch-ROCm
+    tensors on the GPU — the constraint data the engine's models are built from (nep_model_desc.device_inputs):
+    D [N, N], W [F, N], core_per_req [F, N], function memory [F], node memory / cores / costs [N], max delay
+    [F], old allocations [F, N].  Requires a GPU (the product path has no CPU fallback)."""
+    import torch
+    if not torch.cuda.is_available():
+        raise EngineUnavailable("no GPU visible: the engine's instance tensors live on the device")
+    dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
+    host = _arrays(data, len(data.nodes), len(data.functions))
+    out = {k: torch.from_numpy(v).to(dev).contiguous() for k, v in host.items()}
+    torch.cuda.synchronize(dev)   # (the library reads them on its own streams)
+    return out
 
 
 def debug_build(data, variant, step=STEP1, alpha=0.5, soften_step1_sol=1.3, max_score=0.0, prev_network_delay=0.0,
@@ -267,8 +291,11 @@ class LPModel:
         self.variant = VARIANTS[variant] if isinstance(variant, str) else int(variant)
         self.step = int(step)
         self._keep = _arrays(data, self.N, self.F)
+        # the instance as PyTorch-ROCm tensors: the library builds the model from their device memory
+        # (nep_model_desc.device_inputs, API 9)
+        self.tensors = instance_tensors(data)
         self.relaxation = int(relaxation)
-        d = _desc(self._keep, self.N, self.F, self.variant, self.step, alpha, soften_step1_sol, max_score,
+        d = _desc(self.tensors, self.N, self.F, self.variant, self.step, alpha, soften_step1_sol, max_score,
                   prev_network_delay, data.node_budget, self.relaxation)
         h = ctypes.c_void_p()
         _check(self._lib, self._lib.nep_model_create(ctypes.byref(d), int(max_batch), None, ctypes.byref(h)),

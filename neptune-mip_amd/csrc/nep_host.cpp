@@ -49,6 +49,10 @@ hipError_t launch_compact_f64(const double *vals, int rows, int cols, int64_t ld
                               int32_t *cnt, int32_t *off, int32_t *orow, int32_t *ocol, double *oval, bool count_only,
                               hipStream_t s);
 hipError_t launch_copy_segments(const SlotCopy &c, hipStream_t s);
+hipError_t launch_power_iteration(const DeviceView &v, int iters, double *zx, double *zs, double *gx, double *gs,
+                                  double *y, double *upart, double *spart, double *gfac, double *part, int nblk,
+                                  double *out, const int32_t *rp, const int32_t *ci, const double *cv,
+                                  const int32_t *cp, const int32_t *ri, const double *rv, hipStream_t s);
 hipError_t launch_score_check(const DeviceView &v, int slot, const double *zi, double *cpu_fj, double *fpart,
                               double *jpart, const double *node_cost, double budget, double *out, hipStream_t s);
 }  // namespace nep
@@ -106,6 +110,8 @@ struct Model {
   std::vector<double> capn;         // [2][N] node memory, node cores
   double alpha = 0.5, M = 1e6, eps = 1e-6, sigma4 = -1, cost_n = 0, score_n_coef = 0, w_dis = 0;
   int dred = 0;                     // step 2: the reduced disruption block (DeviceView::dred)
+  Coo Ks;                           // the small-variable part of the matrix the iteration runs on (scaling, power)
+  bool power_host = false;          // eta from the host power iteration (nep_debug_build) or the device's
   double sT = 0, sum_old = 0;       // dred: cost per unit of T = sum c - sum old; sum of the old allocation
   int R = 0, JB = 0, CPL = 1, max_batch = 1;
   DualLayout dl{};
@@ -248,7 +254,7 @@ int upload(Model &m, const T **dst, const std::vector<T> &src) {
 // ---------------------------------------------------------------------------------------------
 // model build
 // ---------------------------------------------------------------------------------------------
-int build(Model &m, const nep_model_desc &d) {
+int build(Model &m, const nep_model_desc &d, bool host_power = true) {
   const int N = d.n_nodes, F = d.n_functions;
   if (N <= 0 || F <= 0) return fail(NEP_ERR_ARG, "n_nodes and n_functions must be positive");
   if (N > 2048) return fail(NEP_ERR_ARG, "n_nodes > 2048 not supported by this build");
@@ -611,8 +617,10 @@ int build(Model &m, const nep_model_desc &d) {
   };
   ruiz(KS, m.rho, m.gam);
 
-  // ||K̃||_2 by power iteration on K̃ᵀK̃ (structured x part + COO part)
-  {
+  m.Ks = KS;   // (the device power iteration, power_device, runs on it after setup_device)
+  // ||K̃||_2 by power iteration on K̃ᵀK̃ (structured x part + COO part); nep_model_create runs the same passes on
+  // the device (power_device, nep_build.hip) from the same start vector
+  if (host_power) {
     std::vector<double> zx((size_t)m.R * N), zs(il.n_int), yv(o), gx((size_t)m.R * N), gs(il.n_int);
     std::mt19937_64 rng(12345);
     std::normal_distribution<double> nd;
@@ -682,6 +690,7 @@ int build(Model &m, const nep_model_desc &d) {
     }
     m.sigma_max = std::sqrt(std::max(lam, 1e-30));
     m.eta = 0.95 / m.sigma_max;
+    m.power_host = true;
   }
 
   // initial primal weight (PDLP): ||c~||_2 / ||b~||_2 in the scaled space.  The NEPTUNE objectives
@@ -873,6 +882,79 @@ int setup_dense(Model &m, const nep_model_desc &d) {
   HIPCHK(hipMemsetAsync(v.zi, 0, sizeof(double) * B * v.sint, m.stream));
   HIPCHK(hipMemsetAsync(v.y, 0, sizeof(double) * B * v.sdual, m.stream));
   HIPCHK(hipStreamSynchronize(m.stream));
+  return NEP_OK;
+}
+
+// The step size on the device (nep_build.hip): the host build's 60 power-iteration passes on K̃ᵀK̃ from the same
+// start vector (mt19937_64(12345) normals, routing entries first), in fp64 with fixed-order reductions, over the
+// device copies of the rows, delay and core_per_req matrices (fp32, as the iteration reads them) and the CSR / CSC
+// of the small-variable part.  Scratch is freed afterwards.
+static int power_device(Model &m) {
+  const DeviceView &v = m.v;
+  const int N = m.N, o = m.dl.n_dual, ni = m.il.n_int;
+  const size_t nx = (size_t)m.R * N;
+  std::vector<double> zx(nx), zs(ni);
+  {
+    std::mt19937_64 rng(12345);
+    std::normal_distribution<double> nd;
+    for (auto &t : zx) t = nd(rng);
+    for (auto &t : zs) t = nd(rng);
+  }
+  const Coo &K = m.Ks;
+  const size_t ne = K.v.size();
+  std::vector<int32_t> rp(o + 1, 0), ci(ne), cp(ni + 1, 0), ri(ne);
+  std::vector<double> cv(ne), rv(ne);
+  for (size_t e = 0; e < ne; ++e) { rp[K.r[e] + 1]++; cp[K.c[e] + 1]++; }
+  for (int k = 0; k < o; ++k) rp[k + 1] += rp[k];
+  for (int k = 0; k < ni; ++k) cp[k + 1] += cp[k];
+  {
+    std::vector<int32_t> fr(rp.begin(), rp.end() - 1), fc(cp.begin(), cp.end() - 1);
+    for (size_t e = 0; e < ne; ++e) {
+      const int a = fr[K.r[e]]++, b = fc[K.c[e]]++;
+      ci[a] = K.c[e]; cv[a] = K.v[e];
+      ri[b] = K.r[e]; rv[b] = K.v[e];
+    }
+  }
+  constexpr int kIters = 60, kBlk = 512;
+  std::vector<void *> tmp;
+  auto alloc = [&](size_t bytes) -> void * {
+    void *p = nullptr;
+    if (hipMalloc(&p, std::max<size_t>(bytes, 8)) != hipSuccess) return nullptr;
+    tmp.push_back(p);
+    return p;
+  };
+  auto release = [&]() { for (void *p : tmp) (void)hipFree(p); tmp.clear(); };
+  double *dzx = (double *)alloc(nx * 8), *dgx = (double *)alloc(nx * 8), *dzs = (double *)alloc(ni * 8);
+  double *dgs = (double *)alloc(ni * 8), *dy = (double *)alloc((size_t)o * 8);
+  double *dup = (double *)alloc((size_t)m.F * N * 8), *dsp = (double *)alloc((size_t)m.F * 8);
+  double *dgf = (double *)alloc((size_t)m.F * N * 8), *dpart = (double *)alloc(kBlk * 8);
+  double *dout = (double *)alloc((kIters + 1) * 8);
+  int32_t *drp = (int32_t *)alloc((o + 1) * 4), *dci = (int32_t *)alloc(ne * 4), *dcp = (int32_t *)alloc((ni + 1) * 4);
+  int32_t *dri = (int32_t *)alloc(ne * 4);
+  double *dcv = (double *)alloc(ne * 8), *drv = (double *)alloc(ne * 8);
+  for (void *p : tmp)
+    if (!p) { release(); return fail(NEP_ERR_NOMEM, "hipMalloc (device power iteration)"); }
+  hipError_t e = hipSuccess;
+  const hipMemcpyKind h2d = hipMemcpyHostToDevice;
+  if (e == hipSuccess) e = hipMemcpyAsync(dzx, zx.data(), nx * 8, h2d, m.stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(dzs, zs.data(), (size_t)ni * 8, h2d, m.stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(drp, rp.data(), rp.size() * 4, h2d, m.stream);
+  if (e == hipSuccess && ne) e = hipMemcpyAsync(dci, ci.data(), ne * 4, h2d, m.stream);
+  if (e == hipSuccess && ne) e = hipMemcpyAsync(dcv, cv.data(), ne * 8, h2d, m.stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(dcp, cp.data(), cp.size() * 4, h2d, m.stream);
+  if (e == hipSuccess && ne) e = hipMemcpyAsync(dri, ri.data(), ne * 4, h2d, m.stream);
+  if (e == hipSuccess && ne) e = hipMemcpyAsync(drv, rv.data(), ne * 8, h2d, m.stream);
+  if (e == hipSuccess)
+    e = launch_power_iteration(v, kIters, dzx, dzs, dgx, dgs, dy, dup, dsp, dgf, dpart, kBlk, dout, drp, dci, dcv, dcp,
+                               dri, drv, m.stream);
+  double lam = 0.0;
+  if (e == hipSuccess) e = hipMemcpyAsync(&lam, dout + kIters, 8, hipMemcpyDeviceToHost, m.stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(m.stream);
+  release();
+  if (e != hipSuccess) return fail(NEP_ERR_HIP, std::string("device power iteration: ") + hipGetErrorString(e));
+  m.sigma_max = std::sqrt(std::max(lam, 1e-30));
+  m.eta = 0.95 / m.sigma_max;
+  m.power_host = false;
   return NEP_OK;
 }
 
@@ -1816,18 +1898,60 @@ static void maybe_install_segv_trace() {
   sigaction(SIGSEGV, &sa, &g_prev_segv);
 }
 
-int nep_model_create(const nep_model_desc *desc, int32_t max_batch, void *hip_stream, void **out_model) {
-  if (!desc || !out_model) return fail(NEP_ERR_ARG, "null argument");
+// API 9: a descriptor whose arrays are device memory (nep_model_desc.device_inputs), staged to the host: the
+// build's aggregation, coefficients, presolve base box and scaling read the O(F N + N^2) instance there
+struct HostDesc {
+  nep_model_desc d{};
+  std::vector<double> delay, workload, cpr, fmem, nmem, ncores, ncost, maxd, old;
+};
+static int stage_device_desc(const nep_model_desc &in, HostDesc &h) {
+  h.d = in;
+  h.d.device_inputs = 0;
+  const size_t N = (size_t)std::max(0, in.n_nodes), F = (size_t)std::max(0, in.n_functions);
+  auto get = [&](const double *src, size_t n, std::vector<double> &dst, const double **out) -> hipError_t {
+    if (!src) { *out = nullptr; return hipSuccess; }
+    dst.resize(n);
+    *out = dst.data();
+    return n ? hipMemcpy(dst.data(), src, n * sizeof(double), hipMemcpyDeviceToHost) : hipSuccess;
+  };
+  hipError_t e = hipSuccess;
+  if (e == hipSuccess) e = get(in.delay, N * N, h.delay, &h.d.delay);
+  if (e == hipSuccess) e = get(in.workload, F * N, h.workload, &h.d.workload);
+  if (e == hipSuccess) e = get(in.core_per_req, F * N, h.cpr, &h.d.core_per_req);
+  if (e == hipSuccess) e = get(in.function_memory, F, h.fmem, &h.d.function_memory);
+  if (e == hipSuccess) e = get(in.node_memory, N, h.nmem, &h.d.node_memory);
+  if (e == hipSuccess) e = get(in.node_cores, N, h.ncores, &h.d.node_cores);
+  if (e == hipSuccess) e = get(in.node_cost, N, h.ncost, &h.d.node_cost);
+  if (e == hipSuccess) e = get(in.max_delay, F, h.maxd, &h.d.max_delay);
+  if (e == hipSuccess) e = get(in.old_allocations, F * N, h.old, &h.d.old_allocations);
+  if (e != hipSuccess) return fail(NEP_ERR_ARG, std::string("device_inputs: reading the instance arrays: ") +
+                                                    hipGetErrorString(e));
+  return NEP_OK;
+}
+
+int nep_model_create(const nep_model_desc *desc_in, int32_t max_batch, void *hip_stream, void **out_model) {
+  if (!desc_in || !out_model) return fail(NEP_ERR_ARG, "null argument");
   maybe_install_segv_trace();
+  HostDesc staged;
+  const nep_model_desc *desc = desc_in;
+  if (desc_in->device_inputs) {
+    const int rs = stage_device_desc(*desc_in, staged);
+    if (rs) return rs;
+    desc = &staged.d;
+  }
   if (max_batch <= 0) return fail(NEP_ERR_ARG, "max_batch must be positive");
   std::unique_ptr<Model> m(new Model());
-  int rc = build(*m, *desc);
+  // (NEP_HOST_POWER=1: the host power iteration instead of the device's, for A/B)
+  const char *hp = std::getenv("NEP_HOST_POWER");
+  const bool host_power = hp && std::atoi(hp) != 0;
+  int rc = build(*m, *desc, host_power);
   if (rc == NEP_OK) presolve_setup(*m);
   if (rc) return rc;
   rc = setup_device(*m, max_batch, hip_stream);
   if (rc) return rc;
   rc = setup_dense(*m, *desc);
   if (rc) return rc;
+  if (!host_power && (rc = power_device(*m))) return rc;
   *out_model = m.release();
   return NEP_OK;
 }
@@ -2099,6 +2223,7 @@ int nep_debug_state(void *model, int32_t slot, double *y, double *kz, float *kty
 
 int nep_debug_build(const nep_model_desc *desc, double *eta, double *rho, double *gam, double *rownorm, int32_t *dims) {
   if (!desc) return fail(NEP_ERR_ARG, "null argument");
+  if (desc->device_inputs) return fail(NEP_ERR_ARG, "nep_debug_build takes host arrays (device_inputs = 0)");
   Model m;
   int rc = build(m, *desc);
   if (rc) return rc;
@@ -2127,6 +2252,7 @@ void nep_reset_stats(void *model) {
 int nep_debug_presolve(const nep_model_desc *desc, int32_t n, const double *lbi, const double *ubi, int32_t *ok_full,
                        int32_t *ok_node, double *box_full, double *box_node) {
   if (!desc || n < 0 || !ok_full || !ok_node) return fail(NEP_ERR_ARG, "null argument");
+  if (desc->device_inputs) return fail(NEP_ERR_ARG, "nep_debug_presolve takes host arrays (device_inputs = 0)");
   Model m;
   int rc = build(m, *desc);
   if (rc) return rc;
