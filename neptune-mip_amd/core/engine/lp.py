@@ -74,6 +74,10 @@ SCORE_FIELDS = ("network_delay", "nodes_used", "node_cost", "bad_c_x", "bad_memo
 _lib = None
 
 
+def _host_inputs():
+    return os.environ.get("NEP_HOST_INPUTS", "0") not in ("", "0")
+
+
 def load_library(path=None):
     """Load (once) and type the shared library.  Raises EngineUnavailable when absent."""
     global _lib
@@ -85,7 +89,9 @@ def load_library(path=None):
     # One HIP runtime per process: PyTorch-ROCm ships its own libamdhip64 (soname libamdhip64.so.7), loaded
     # by file name.  Loaded first, it satisfies the engine's libamdhip64.so.7 dependency; loaded after the
     # engine's /opt/rocm copy, the process holds two runtimes and the second to initialise sees no device.
-    import torch  # noqa: F401
+    # (NEP_HOST_INPUTS=1: host-array descriptors and no PyTorch, the engine on /opt/rocm's runtime — for A/B)
+    if not _host_inputs():
+        import torch  # noqa: F401
     lib = ctypes.CDLL(p)
     vp, i32, i64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64
     pi32, pi64 = ctypes.POINTER(i32), ctypes.POINTER(i64)
@@ -293,9 +299,9 @@ class LPModel:
         self._keep = _arrays(data, self.N, self.F)
         # the instance as PyTorch-ROCm tensors: the library builds the model from their device memory
         # (nep_model_desc.device_inputs, API 9)
-        self.tensors = instance_tensors(data)
+        self.tensors = None if _host_inputs() else instance_tensors(data)
         self.relaxation = int(relaxation)
-        d = _desc(self.tensors, self.N, self.F, self.variant, self.step, alpha, soften_step1_sol, max_score,
+        d = _desc(self._keep if self.tensors is None else self.tensors, self.N, self.F, self.variant, self.step, alpha, soften_step1_sol, max_score,
                   prev_network_delay, data.node_budget, self.relaxation)
         h = ctypes.c_void_p()
         _check(self._lib, self._lib.nep_model_create(ctypes.byref(d), int(max_batch), None, ctypes.byref(h)),

@@ -1952,6 +1952,7 @@ int nep_model_create(const nep_model_desc *desc_in, int32_t max_batch, void *hip
   rc = setup_dense(*m, *desc);
   if (rc) return rc;
   if (!host_power && (rc = power_device(*m))) return rc;
+  if (const char *e = std::getenv("NEP_ETA_SCALE")) m->eta *= std::atof(e);   // (probe: tools/root_chaos_probe.py)
   *out_model = m.release();
   return NEP_OK;
 }
