@@ -76,6 +76,9 @@ def parse(argv=None):
                          "trace was recorded")
     ap.add_argument("--warm-omega-floor", type=float, default=0.0,
                     help="warm-start primal-weight floor x the parent's (0: engine default)")
+    ap.add_argument("--omega-ref", type=float, default=8.0,
+                    help="warm starts take their primal weight in [floor, cap] x (this x the model's cold-start weight "
+                         "omega0) (nep_lp_set_reference_weight; 0: relative to the parent's final weight)")
     ap.add_argument("--root-max-iters", type=int, default=400000)
     ap.add_argument("--check-every", type=int, default=48,
                     help="PDHG iterations per certificate check of the timed streams (replay: 12 / 24 / 48 -> 5.70 / "
@@ -113,6 +116,8 @@ def parse(argv=None):
     ap.add_argument("--bnb-sizes", default="256x128:20,512x256:60",
                     help="instances of the product B&B section (BASELINE configs 3 and 4), NxF[:seconds] "
                          "comma-separated (seconds: that instance's time limit, default --bnb-seconds)")
+    ap.add_argument("--dump", default=None, help="write per-node-LP records of the replay (kind, depth, warm source, "
+                    "status, iterations, final diagnostics of the uncertified) to this JSON file")
     ap.add_argument("--traffic", default=os.path.join(REPO, "profiles", "traffic.json"))
     return ap.parse_args(argv)
 
@@ -378,6 +383,8 @@ class ReplayStream:
         self.kids = Counter(e["parent"] for e in mine)
         self.kids_left = {}     # (model, node key) -> children of it not yet started
         self.warm_parent = 0
+        self.records = []       # (--dump) one record per completed node LP
+        self.status_of = {}
 
     def peek_entry(self):
         """(repetition, entry) this rank replays next: entries rank, rank + world, ... of the trace (repeated)."""
@@ -476,6 +483,13 @@ class ReplayStream:
                     self.done.append((int(r["status"][i]), float(r["obj"][i]), float(r["primal_obj"][i]),
                                       int(r["iters"][i])))
                     key, kind, depth, wp = self.running.pop((name, slot))
+                    if getattr(self.a, "dump", None):
+                        st_ = int(r["status"][i])
+                        rec = {"id": key[1], "kind": kind, "depth": depth, "warm_parent": wp, "status": st_,
+                               "iters": int(r["iters"][i]), "parent_status": self.status_of.get(self.parent_of.get(key[1]))}
+                        rec["diag"] = m.diag(slot)
+                        self.records.append(rec)
+                        self.status_of[key[1]] = st_
                     self.busy[name] -= 1
                     self.kinds.append((name, kind))
                     self.depth.append((depth, wp))
@@ -628,6 +642,9 @@ def main():
                  polish_after=float(a.root_polish_after))
     root_obj, root_status, root_iters = float(rr["obj"][0]), int(rr["status"][0]), int(rr["iters"][0])
     root_seconds = time.perf_counter() - t_root
+    root_omega = m.diag(root)["omega"]
+    if a.omega_ref > 0:
+        m.set_reference_weight(a.omega_ref * m.info.primal_weight0)
     log(f"rank {rank}: root LP status {root_status} obj {root_obj:.10g} after {root_iters} iterations "
         f"({time.perf_counter() - t_root:.2f}s)")
     if root_status != LP_OPTIMAL:
@@ -662,6 +679,8 @@ def main():
             t_fr = time.perf_counter()
             fr = bm.solve([root], tol=a.tol, max_iters=a.root_max_iters, check_every=a.root_check_every,
                         bound_res=1e-2, gap_tol=1e-4)
+            if a.omega_ref > 0:      # (as the product B&B sets it on both of its models)
+                bm.set_reference_weight(a.omega_ref * bm.info.primal_weight0)
             fac_root = {"status": int(fr["status"][0]), "obj": float(fr["obj"][0]), "iters": int(fr["iters"][0]),
                         "seconds": time.perf_counter() - t_fr}
             log(f"rank {rank}: facility-relaxation root: {fac_root}")
@@ -731,6 +750,9 @@ def main():
         stream.drain(a.warmup * B)
         log(f"rank {rank}: warmup: {len(stream.done)} node LPs completed")
     prim = timed(stream, a.steps, kind)
+    if a.dump and rank == 0 and getattr(stream, "records", None) is not None:
+        with open(a.dump, "w") as fh:
+            json.dump(stream.records, fh)
     st = prim["stats"]
     wall, n_ok, n_it, gmax, n_done = prim["wall"], prim["certified"], prim["iterations"], prim["gmax"], prim["completed"]
     iq, util = prim["iters_p50_p90_max"], prim["util"]
@@ -825,6 +847,8 @@ def main():
                "mean_iters": n_it / max(1, n_done), "iters_p50_p90_max": iq,
                "slot_utilisation_rank0": util,
                "root_obj": root_obj, "root_iters": root_iters, "root_seconds": root_seconds,
+               "primal_weight0": m.info.primal_weight0, "root_final_weight": root_omega,
+               "omega_ref": a.omega_ref * m.info.primal_weight0 if a.omega_ref > 0 else None,
                "root_polish": root_polish},
         "native_replay": native,
         "children_stream": second,

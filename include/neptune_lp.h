@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define NEP_API_VERSION 9
+#define NEP_API_VERSION 10
 
 /* variants: neptune.py:41-66 (NeptuneMinDelay / MinUtilization / MinDelayAndUtilization) */
 enum { NEP_MIN_DELAY = 0, NEP_MIN_UTILIZATION = 1, NEP_MIN_DELAY_AND_UTILIZATION = 2 };
@@ -125,6 +125,7 @@ typedef struct {
   int64_t x_entries;           /* R*N per LP */
   int64_t bytes_per_iter;      /* algorithmic HBM bytes of one PDHG iteration of one LP */
   double step_size;            /* eta = 0.95 / ||K||_2 (scaled) */
+  double primal_weight0;       /* API 10: the cold start's PDHG primal weight omega0 = ||c~|| / ||b~|| (scaled) */
 } nep_model_info;
 
 typedef struct {
@@ -179,6 +180,12 @@ int nep_lp_copy_state(void *model, int32_t src_slot, int32_t dst_slot);
 /* tol / cutoff of every LP in flight, effective from the next iteration block (a B&B lowers the
  * cutoff to each new incumbent without resubmitting). */
 int nep_lp_set_params(void *model, double tol, double cutoff);
+
+/* API 10: the primal-weight band of warm starts.  omega_ref > 0: a warm-started LP takes its weight in
+ * [warm_omega_floor, warm_omega_cap] x omega_ref (its parent's weight clamped into that band) instead of
+ * relative to its parent's final weight, which ratchets up along a lineage of warm starts (DESIGN.md §4
+ * "Warm-start primal weight"); 0 restores the parent-relative band.  Applies to later submits. */
+int nep_lp_set_reference_weight(void *model, double omega_ref);
 
 /* flow[b][f][j] = sum_i x[i,f,j] of finished slots (host float, n x F x N), computed on the device:
  * the branch-and-bound's branching / rounding input (replaces copying the R x N routing rows). */

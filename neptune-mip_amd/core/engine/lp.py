@@ -18,7 +18,7 @@ STEP1, STEP2_DELETE, STEP2_CREATE = 1, 2, 3
 LP_OPTIMAL, LP_ITERATION_LIMIT, LP_INFEASIBLE, LP_CUTOFF, LP_NUMERICAL, LP_BOUND = 0, 1, 2, 3, 4, 5
 VARIANTS = {"MinDelay": MIN_DELAY, "MinUtilization": MIN_UTILIZATION,
             "MinDelayAndUtilization": MIN_DELAY_AND_UTILIZATION}
-API_VERSION = 9
+API_VERSION = 10
 RELAX_REFERENCE, RELAX_FACILITY = 0, 1
 
 _dp = ctypes.POINTER(ctypes.c_double)
@@ -50,7 +50,7 @@ class LpOpts(ctypes.Structure):
 class ModelInfo(ctypes.Structure):
     _fields_ = [("n_int", ctypes.c_int32), ("n_rows", ctypes.c_int32), ("n_tiles", ctypes.c_int32),
                 ("max_batch", ctypes.c_int32), ("x_entries", ctypes.c_int64), ("bytes_per_iter", ctypes.c_int64),
-                ("step_size", ctypes.c_double)]
+                ("step_size", ctypes.c_double), ("primal_weight0", ctypes.c_double)]
 
 
 class Stats(ctypes.Structure):
@@ -67,7 +67,7 @@ EXPORTS = ("nep_model_create", "nep_model_destroy", "nep_model_get_info", "nep_l
            "nep_last_error", "nep_api_version", "nep_lp_get_diag", "nep_debug_build", "nep_debug_state",
            "nep_debug_presolve", "nep_lp_set_params", "nep_lp_get_flows", "nep_lp_routing_entries",
            "nep_lp_allocation_entries", "nep_lp_score_check", "nep_round_leaf", "nep_lp_copy_routing",
-           "nep_lp_get_solutions", "nep_round_leaves")
+           "nep_lp_get_solutions", "nep_round_leaves", "nep_lp_set_reference_weight")
 SCORE_FIELDS = ("network_delay", "nodes_used", "node_cost", "bad_c_x", "bad_memory", "bad_handle", "bad_cpu",
                 "bad_n_c", "bad_budget", "handle_maxdev", "cpu_maxexcess")
 
@@ -120,6 +120,7 @@ def load_library(path=None):
     lib.nep_debug_state.argtypes = [vp, i32, _dp, _dp, ctypes.POINTER(ctypes.c_float), _dp, _dp]
     lib.nep_debug_presolve.argtypes = [ctypes.POINTER(ModelDesc), i32, _dp, _dp, pi32, pi32, _dp, _dp]
     lib.nep_lp_set_params.argtypes = [vp, ctypes.c_double, ctypes.c_double]
+    lib.nep_lp_set_reference_weight.argtypes = [vp, ctypes.c_double]
     lib.nep_lp_get_flows.argtypes = [vp, i32, pi32, ctypes.POINTER(ctypes.c_float)]
     lib.nep_lp_get_flows_split.argtypes = [vp, i32, pi32, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float)]
     lib.nep_lp_routing_entries.argtypes = [vp, i32, ctypes.c_double, i32, i64, pi64, pi32, pi32, _dp]
@@ -511,6 +512,12 @@ class LPModel:
         _check(self._lib, self._lib.nep_debug_state(self._h, int(slot), _ptr(y), _ptr(kz), None, _ptr(lb), _ptr(ub)),
                "nep_debug_state")
         return {"y": y, "kz": kz, "lb": lb, "ub": ub}
+
+    def set_reference_weight(self, omega_ref):
+        """Warm starts take their primal weight in [floor, cap] x omega_ref (nep_lp_set_reference_weight, API 10);
+        0: relative to the parent's final weight."""
+        _check(self._lib, self._lib.nep_lp_set_reference_weight(self._h, float(omega_ref)),
+               "nep_lp_set_reference_weight")
 
     def copy_state(self, src, dst):
         _check(self._lib, self._lib.nep_lp_copy_state(self._h, int(src), int(dst)), "nep_lp_copy_state")

@@ -144,6 +144,7 @@ struct Model {
   std::vector<double> Kcv;
   std::vector<PresolveScratch> psc;   // one per presolve thread (submit presolves a batch's nodes in parallel)
   double eta = 0, sigma_max = 0, omega0 = 1.0;
+  double omega_ref = 0.0;           // nep_lp_set_reference_weight (0: warm-start band relative to the parent)
   // device
   hipStream_t stream = nullptr;
   bool own_stream = false;
@@ -1445,6 +1446,7 @@ int submit(Model &m, int n, const int32_t *slots, const double *lbi, const doubl
   DeviceView &v = m.v;
   v.warm_omega_floor = o.warm_omega_floor;
   v.warm_omega_cap = o.warm_omega_cap;
+  v.warm_omega_ref = m.omega_ref;
   v.polish_after = (o.polish_after < 0 || m.fac) ? -1 : (int64_t)o.polish_after;   // (fac: no polishing)
   v.max_iters = o.max_iters;
   v.bound_res = o.bound_res;
@@ -1972,6 +1974,7 @@ int nep_model_get_info(void *model, nep_model_info *info) {
   info->bytes_per_iter = 4 * (2 * (int64_t)m.R * m.N + 2 * (int64_t)m.F * m.N + 2 * (int64_t)m.N +
                               2 * ((int64_t)m.dl.n_dual + (m.fac ? (int64_t)m.R * m.N : 0)));
   info->step_size = m.eta;
+  info->primal_weight0 = m.omega0;
   return NEP_OK;
 }
 
@@ -2147,6 +2150,13 @@ int nep_lp_set_params(void *model, double tol, double cutoff) {
   m.run.cutoff = cutoff;
   HIPCHK(set_prm(m, m.run.tol, m.run.cutoff, m.run.gap_tol));
   HIPCHK(hipStreamSynchronize(m.aux));
+  return NEP_OK;
+}
+
+int nep_lp_set_reference_weight(void *model, double omega_ref) {
+  if (!model) return fail(NEP_ERR_ARG, "null model");
+  if (!(omega_ref >= 0.0) || !std::isfinite(omega_ref)) return fail(NEP_ERR_ARG, "omega_ref must be finite and >= 0");
+  static_cast<Model *>(model)->omega_ref = omega_ref;
   return NEP_OK;
 }
 

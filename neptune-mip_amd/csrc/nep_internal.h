@@ -196,6 +196,7 @@ struct DeviceView {
   const double *prm;
   double warm_omega_floor;               // warm starts: primal weight kept >= this x the parent's (0: off)
   double warm_omega_cap;                 // warm starts: primal weight kept <= this x the parent's (0: off)
+  double warm_omega_ref;                 // > 0: the floor / cap multiply this instead of the parent's weight
   int64_t polish_after;                  // submit option: polishing may start after this many iterations (-1: never)
   double polish_res;                     // polishing starts only with the primal residual <= this (NEP_POLISH, kPolishRes)
   int64_t polish_budget;                 // polishing iterations before going back to the LP (NEP_POLISH, kPolishBudget)

@@ -1472,6 +1472,15 @@ __global__ void init_slot(DeviceView v, const int32_t *__restrict__ slots, const
     if (!warm) ctrl->k_lineage = 0;
     if (warm && v.warm_omega_cap > 0 && ctrl->k_lineage >= kOmegaTrained)
       ctrl->omega_hi = fmax(ctrl->omega * v.warm_omega_cap, ctrl->omega_lo);
+    // With a model reference weight (nep_lp_set_reference_weight) the band is [floor, cap] x that reference and
+    // the parent's weight is clamped into it: relative to the parent, the band ratchets up along a lineage of
+    // warm starts (512x256 replay: uncertified node LPs at a median 80x the root's weight; 8.8 -> 11.4
+    // certified LP/s with the band fixed; DESIGN.md §4 "Warm-start primal weight")
+    if (warm && v.warm_omega_ref > 0) {
+      ctrl->omega_lo = v.warm_omega_floor > 0 ? v.warm_omega_ref * v.warm_omega_floor : omega0 * 1e-5;
+      ctrl->omega_hi = fmax(v.warm_omega_cap > 0 ? v.warm_omega_ref * v.warm_omega_cap : omega0 * 1e5, ctrl->omega_lo);
+      ctrl->omega = fmin(fmax(ctrl->omega, ctrl->omega_lo), ctrl->omega_hi);
+    }
     ctrl->tau = eta / ctrl->omega;
     ctrl->sigma = eta * ctrl->omega;
     ctrl->status = 1;
