@@ -44,13 +44,24 @@ def test_product_bnb_time_limited(n, f, seconds):
     st1.load_data(data)
     ub = st1.upper_bound()
     m = LPModel(data, "MinDelayAndUtilization", step=1, alpha=0.5, max_batch=34)
+    bm = None
     try:
-        res = BranchAndBound(m, data.workload_matrix, data.function_memory_matrix, data.node_memory_matrix,
-                             batch=32, tol=5e-7 if n < 512 else 1e-6, time_limit=seconds,
-                             root_max_iters=200000 if n < 512 else 400000, upper_bound=ub * (1 + 1e-6) + 1e-6,
-                             repair=st1.routing_repair(m.layout())).solve()
+        if n < 512:   # the one-model search (every node LP on the reference model)
+            res = BranchAndBound(m, data.workload_matrix, data.function_memory_matrix, data.node_memory_matrix,
+                                 batch=32, tol=5e-7, time_limit=seconds, root_max_iters=200000,
+                                 upper_bound=ub * (1 + 1e-6) + 1e-6, repair=st1.routing_repair(m.layout())).solve()
+        else:         # the product's step-1 search at config 4 (facility-relaxation bounds, the capacity-greedy
+            # root heuristic; NeptuneStepBase.branch_and_bound): the one-model search's rounding
+            # leaves can all fail the presolve's CPU cover here, depending on which optimal face the root lands on
+            st1 = NeptuneStep1CPUMinDelayAndUtilization(alpha=0.5, verbose=False, batch=32, lp_tol=1e-6,
+                                                        lp_max_iters=4096)
+            st1.load_data(data)
+            bm = st1.bound_model(data, 33)
+            res = st1.branch_and_bound(m, bm, time_limit=seconds, root_max_iters=400000).solve()
     finally:
         m.close()
+        if bm is not None:
+            bm.close()
     print(res.as_dict())
     # a stop decision ends the search within a block of the LPs in flight (they stop at their next check)
     assert res.seconds <= seconds + 30.0, res.as_dict()
