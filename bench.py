@@ -79,6 +79,9 @@ def parse(argv=None):
     ap.add_argument("--omega-ref", type=float, default=8.0,
                     help="warm starts take their primal weight in [floor, cap] x (this x the model's cold-start weight "
                          "omega0) (nep_lp_set_reference_weight; 0: relative to the parent's final weight)")
+    ap.add_argument("--polish-after", type=float, default=0.0,
+                    help="replay: warm-started node LPs start primal-feasibility polishing after this many iterations "
+                         "(0: the engine's default, 256; -1: never)")
     ap.add_argument("--root-max-iters", type=int, default=400000)
     ap.add_argument("--check-every", type=int, default=48,
                     help="PDHG iterations per certificate check of the timed streams (replay: 12 / 24 / 48 -> 5.70 / "
@@ -98,9 +101,11 @@ def parse(argv=None):
     ap.add_argument("--native-steps", type=int, default=6,
                     help="with the replay stream: steps of the native-model replay timed after it (each recorded "
                          "box on the model the product ran it on; 0 = skip)")
-    ap.add_argument("--park", type=int, default=256,
+    ap.add_argument("--park", type=int, default=1024,
                     help="replay: slots per model beyond --batch that keep finished nodes' states while their children "
-                         "are still to come (warm start from the parent; 0: only free slots keep states)")
+                         "are still to come (warm start from the parent; 0: only free slots keep states).  1024 (76 GB "
+                         "of slot state at 512x256): the same warm sources as 256, x_pass launches 6 %% shorter "
+                         "(profiles/r05/pad: the working slots' placement, not padding or allocation size)")
     ap.add_argument("--warm-ancestors", action="store_true",
                     help="replay: a node whose parent's state is gone starts from its closest resident ancestor's "
                          "(default: the root's, as the product B&B does)")
@@ -460,7 +465,7 @@ class ReplayStream:
             else:
                 kw = dict(max_iters=a.max_iters)
             st = m.submit([slot], lb[None], ub[None], tol=a.tol, check_every=a.check_every, warm_start=True,
-                          warm_omega_floor=a.warm_omega_floor, **kw)
+                          warm_omega_floor=a.warm_omega_floor, polish_after=a.polish_after, **kw)
             if int(st[0]) == LP_INFEASIBLE:
                 self.done.append((LP_INFEASIBLE, float("inf"), float("nan"), 0))
                 self.kinds.append((name, e["kind"]))

@@ -810,6 +810,7 @@ int setup_dense(Model &m, const nep_model_desc &d) {
   // per-slot arrays
   const int B = m.max_batch;
   v.sx = (int64_t)m.R * NP;
+  if (const char *e = std::getenv("NEP_SLOT_PAD")) v.sx += std::max(0, std::atoi(e)) / 64 * 64;   // (probe)
   v.smask = (int64_t)F * NP;
   v.sint = m.il.n_int;
   v.sdual = m.dl.n_dual;
@@ -818,8 +819,12 @@ int setup_dense(Model &m, const nep_model_desc &d) {
   v.sbpart = (int64_t)(F + m.JB) * NBS;
   v.snpart = (int64_t)F * (m.fac ? 3 : 2) * NP;   // fac: c, CPU share, reflected c (2ĉ - c) per (f, j)
   v.srpart = (int64_t)F * 2 * NP;
-  if ((rc = dalloc(m, &v.x, (size_t)B * v.sx))) return rc;
-  if ((rc = dalloc(m, &v.xa, (size_t)B * v.sx))) return rc;
+  {   // (probe: NEP_SLOT_OVERALLOC=k allocates the routing state for k x the slots; only B are used)
+    const char *e = std::getenv("NEP_SLOT_OVERALLOC");
+    const size_t k = e ? (size_t)std::max(1, std::atoi(e)) : 1;
+    if ((rc = dalloc(m, &v.x, k * B * v.sx))) return rc;
+    if ((rc = dalloc(m, &v.xa, k * B * v.sx))) return rc;
+  }
   if ((rc = dalloc(m, &v.acnt, (size_t)B * m.R))) return rc;
   if ((rc = dalloc(m, &v.aent, (size_t)B * m.R * kAnchorK))) return rc;
   if ((rc = dalloc(m, &v.theta, (size_t)B * m.R))) return rc;
