@@ -465,7 +465,7 @@ class ReplayStream:
             else:
                 kw = dict(max_iters=a.max_iters)
             st = m.submit([slot], lb[None], ub[None], tol=a.tol, check_every=a.check_every, warm_start=True,
-                          warm_omega_floor=a.warm_omega_floor, polish_after=a.polish_after, **kw)
+                          warm_omega_floor=a.warm_omega_floor, polish_after=getattr(a, "polish_after", 0.0), **kw)
             if int(st[0]) == LP_INFEASIBLE:
                 self.done.append((LP_INFEASIBLE, float("inf"), float("nan"), 0))
                 self.kinds.append((name, e["kind"]))

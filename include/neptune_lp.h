@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define NEP_API_VERSION 10
+#define NEP_API_VERSION 11
 
 /* variants: neptune.py:41-66 (NeptuneMinDelay / MinUtilization / MinDelayAndUtilization) */
 enum { NEP_MIN_DELAY = 0, NEP_MIN_UTILIZATION = 1, NEP_MIN_DELAY_AND_UTILIZATION = 2 };
@@ -266,6 +266,60 @@ int nep_round_leaf(int32_t F, int32_t N, const double *c_fix, const double *n_fi
 int nep_round_leaves(int32_t F, int32_t N, const double *c_fix, const double *n_fix, const float *flow, const double *zc,
                      const double *fn_mem, const double *node_mem, int32_t modes, const int32_t *by_flow,
                      const double *flow_threshold, double *c_out, double *n_out, int32_t *found);
+
+/* API 11: the branch-and-bound's tree search, native (csrc/nep_bnb.cpp; core/engine/bnb.py delegates its
+ * single-rank step-1 search here, DESIGN.md §7 "Native tree search").  Replaces the host loop of
+ * BranchAndBound.solve (core/engine/bnb.py) — the tree SCIP searches inside Solver.Solve()
+ * (core/solvers/solver.py:35-40): best-first open nodes, rounding leaves, retries of uncertified leaves,
+ * warm starts from the parent's slot or the root's state, one submit / advance stream per model (the leaf
+ * model = the reference LP; the optional bound model = the facility relaxation), prune / branch / round per
+ * finished LP.  The tree drives the models through this header's nep_lp_* calls only. */
+typedef struct {
+  int32_t c0, c1, n0, n1, n_int;   /* integer layout: c = z_int[c0:c1] (F x N), n = z_int[n0:n1] (n0 < 0: none) */
+  int32_t F, N;
+  int32_t warm;                    /* warm starts (reserves the leaf model's last two slots: root / incumbent state) */
+  int32_t check_every, root_check_every;
+  int32_t unit_flow_leaves;        /* a third rounding mode: (f, j) carrying a unit of flow */
+  int32_t objective_integral;      /* every integral point's objective is integral: prune at incumbent - 1 */
+  int32_t primal_at_root;          /* nep_bnb_run returns NEP_BNB_ROOT once the root branching node finished */
+  double tol, gap, bound_gap;      /* LP tolerance, relative MIP gap, the bound model's gap_tol */
+  int64_t max_iters, node_max_iters, root_max_iters;
+  double node_bound_res, retry_res, flow_tol;
+  double upper_bound;              /* a-priori cutoff (+inf: none) */
+  int64_t node_limit;
+  double time_limit;               /* seconds (<= 0: none) */
+} nep_bnb_params;
+
+typedef struct {
+  int64_t nodes, leaves, lps, certified, lp_iterations, unresolved, drained;
+  int64_t lp_status[7];            /* certified, bound, limit, infeasible, cutoff, numerical, presolve-infeasible */
+  int64_t lp_status_kind[4][7];    /* per node kind: node, leaf, retry, refroot */
+  int64_t advance_calls, inflight_sum, lp_incumbents, heuristic_incumbents, n_lp_iters;
+  double advance_seconds, finish_seconds, submit_seconds, drain_seconds, root_seconds;
+  double bound, incumbent;         /* at the end: best proven bound, incumbent value (+inf: none) */
+  int32_t incumbent_source;        /* 0 none, 1 a certified leaf LP, 2 nep_bnb_set_incumbent */
+  int32_t incumbent_slot;          /* leaf-model slot holding the incumbent LP's state (source 1) */
+  int32_t limit_hit, any_unresolved, unresolved_below;
+} nep_bnb_stats;
+
+#define NEP_BNB_DONE 0   /* the search ended (no open node, or a stop): stats / incumbent are final */
+#define NEP_BNB_ROOT 1   /* the root branching node finished: nep_bnb_event_data, then nep_bnb_add_leaf(where = 1) /
+                            nep_bnb_set_incumbent for the caller's primal heuristic, then nep_bnb_run again */
+
+void *nep_bnb_create(void *leaf_model, void *bound_model, const nep_bnb_params *params, const double *fn_mem,
+                     const double *node_mem);
+void nep_bnb_destroy(void *tree);
+/* a leaf (a full c / n assignment, or any box): where = 0 a seed leaf queued when the root LP finishes;
+ * where = 1 a leaf of the NEP_BNB_ROOT event's node, at the front of the leaf queue */
+int nep_bnb_add_leaf(void *tree, int32_t n, const int32_t *idx, const double *val, double bound, int32_t where);
+/* an incumbent found outside the tree (a checked heuristic point): its value becomes the cutoff */
+int nep_bnb_set_incumbent(void *tree, double value);
+int nep_bnb_event_data(void *tree, double *z_int, float *flow);
+int nep_bnb_run(void *tree, int32_t *event);
+int nep_bnb_get_stats(void *tree, nep_bnb_stats *out);
+int nep_bnb_get_lp_iters(void *tree, int64_t *out);
+/* the LP incumbent's integer vector and its leaf box (*n_fix = -1: no LP incumbent) */
+int nep_bnb_incumbent(void *tree, double *z_int, int32_t *n_fix, int32_t *idx, double *val);
 
 const char *nep_last_error(void);
 int nep_api_version(void);

@@ -44,6 +44,7 @@ and on termination (open + in-flight node count, SUM); at the end the owner of t
 import heapq
 import itertools
 import math
+import os
 import time
 from collections import deque
 
@@ -95,12 +96,13 @@ class BnBResult:
         self.rebalanced = 0             # open nodes this rank received from another rank
         self.advance_calls = 0
         self.inflight_sum = 0           # LPs in flight summed over the advance calls (mean: / advance_calls)
+        self.native = False             # the search ran on the native tree (csrc/nep_bnb.cpp)
 
     def as_dict(self):
         d = {k: getattr(self, k) for k in ("status", "objective", "bound", "nodes", "leaves", "lps", "certified",
                                            "lp_iterations", "unresolved", "seconds", "polished", "repaired",
                                            "lp_status", "lp_status_kind", "drained", "timing",
-                                           "heuristic_incumbents", "routing_warm")}
+                                           "heuristic_incumbents", "routing_warm", "native")}
         d["inflight_mean"] = self.inflight_sum / max(1, self.advance_calls)
         d["resolved"] = sum(v for k, v in self.lp_status.items() if k not in ("limit", "numerical"))
         it = np.asarray(self.lp_iters, np.float64)
@@ -153,7 +155,8 @@ class BranchAndBound:
                  seed_leaves=None, integer_bound=None, improve=None, repair=None, node_bound_res=1e-2,
                  retry_res=math.inf, unit_flow_leaves=True, node_max_iters=None, bound_lp=None, bound_gap=1e-4,
                  trace=None, rebalance_every=8, primal=None, primal_every=0,
-                 leaf_routing_warm=False, root_check_every=64, objective_integral=False, warm_weight_ref=8.0):
+                 leaf_routing_warm=False, root_check_every=64, objective_integral=False, warm_weight_ref=8.0,
+                 native=None):
         self.lp = lp
         self.two = bound_lp is not None
         self.N, self.F = lp.N, lp.F
@@ -203,6 +206,10 @@ class BranchAndBound:
         # (nep_lp_set_reference_weight; 512x256 replay 7.5 -> 12.2 certified LP/s, independent of the root's
         # chaotic final weight; DESIGN.md §4 "Warm-start primal weight"); 0: parent-relative
         self.warm_weight_ref = float(warm_weight_ref or 0.0)
+        # native tree search (csrc/nep_bnb.cpp, nep_bnb_*): the single-rank search without per-node Python
+        # callbacks runs its whole loop in the engine library (None: whenever eligible; NEP_BNB_PYTHON=1 keeps
+        # this module's loop, for A/B)
+        self.native = native
         for m_ in (lp, bound_lp):
             if m_ is not None and hasattr(m_, "set_reference_weight"):
                 m_.set_reference_weight(self.warm_weight_ref * m_.info.primal_weight0 if self.warm_weight_ref > 0 else 0.0)
@@ -726,7 +733,122 @@ class BranchAndBound:
         res.x = lp.routing_from_entries(row, dst, val)
 
     # ---------------------------------------------------------------------------------------
+    def _native_ok(self, comm):
+        if self.native is False or os.environ.get("NEP_BNB_PYTHON", "0") not in ("", "0"):
+            return False
+        eligible = (comm.world == 1 and self.trace is None and self.improve is None and self.integer_bound is None
+                    and not self.leaf_routing_warm and self.primal_every == 0 and hasattr(self.lp, "_h")
+                    and (self.bound_lp is None or hasattr(self.bound_lp, "_h")))
+        if self.native and not eligible:
+            raise ValueError("native tree search: single rank, no trace / improve / integer_bound / leaf routing warm "
+                             "starts / primal_every")
+        return eligible
+
+    def _solve_native(self):
+        """solve() on the native tree (nep_bnb_*, csrc/nep_bnb.cpp): the same search, its loop in the library;
+        this method handles the root's primal heuristic (NEP_BNB_ROOT) and the end (routing, polish, repair)."""
+        import ctypes
+        from .lp import BnbParams, BnbStats, _check, _ptr
+        t0 = self.t0 = time.time()
+        self.res = res = BnBResult()
+        lp, lib = self.lp, self.lp._lib
+        n0, n1 = self.n_range if self.n_range is not None else (-1, -1)
+        inf = math.inf
+        p = BnbParams(c0=self.c0, c1=self.c1, n0=n0, n1=n1, n_int=lp.n_int, F=self.F, N=self.N,
+                      warm=1 if self.warm else 0, check_every=int(self.check_every),
+                      root_check_every=int(self.root_check_every), unit_flow_leaves=1 if len(self.round_modes) > 2 else 0,
+                      objective_integral=1 if self.objective_integral else 0,
+                      primal_at_root=1 if self.primal is not None else 0, tol=self.tol, gap=self.gap,
+                      bound_gap=self.bound_gap, max_iters=int(self.max_iters), node_max_iters=int(self.node_max_iters),
+                      root_max_iters=int(self.root_max_iters), node_bound_res=float(self.node_bound_res or 0.0),
+                      retry_res=float(self.retry_res), flow_tol=float(self.flow_tol), upper_bound=float(self.ub0),
+                      node_limit=int(self.node_limit), time_limit=float(self.time_limit or 0.0))
+        tree = lib.nep_bnb_create(lp._h, self.bound_lp._h if self.two else None, ctypes.byref(p), _ptr(self.fn_mem),
+                                  _ptr(self.node_mem))
+        if not tree:
+            raise RuntimeError("nep_bnb_create failed")
+        bm = self.bound_lp if self.two else lp
+        try:
+            for idx, val in self.seed_leaves:
+                idx = np.ascontiguousarray(idx, np.int32)
+                val = np.ascontiguousarray(val, np.float64)
+                _check(lib, lib.nep_bnb_add_leaf(tree, len(idx), _ptr(idx), _ptr(val), -inf, 0), "nep_bnb_add_leaf")
+            ev = ctypes.c_int32()
+            while True:
+                _check(lib, lib.nep_bnb_run(tree, ctypes.byref(ev)), "nep_bnb_run")
+                if ev.value == 0:
+                    break
+                # NEP_BNB_ROOT: the primal heuristic on the root branching node's LP
+                t = time.time()
+                z = np.zeros(bm.n_int)
+                flow = np.zeros((self.F, self.N), np.float32)
+                _check(lib, lib.nep_bnb_event_data(tree, _ptr(z), _ptr(flow)), "nep_bnb_event_data")
+                inc = res.objective if res.objective is not None else inf
+                for item in self.primal(np.zeros(0, np.int64), np.zeros(0), z, flow):
+                    idx, val = np.ascontiguousarray(item[0], np.int32), np.ascontiguousarray(item[1], np.float64)
+                    sol = item[2] if len(item) > 2 else None
+                    if sol is not None and sol["objective"] < inc - self._gap_abs(inc):
+                        res.objective = inc = float(sol["objective"])
+                        res.z = np.asarray(sol["z"], np.float64)
+                        res.x = self.lp.routing_from_entries(sol["row"], sol["dst"], sol["val"])
+                        _check(lib, lib.nep_bnb_set_incumbent(tree, inc), "nep_bnb_set_incumbent")
+                        self.log(f"incumbent {inc:.10g} (capacity greedy)")
+                    _check(lib, lib.nep_bnb_add_leaf(tree, len(idx), _ptr(idx), _ptr(val), -inf, 1), "nep_bnb_add_leaf")
+                res.timing["primal"] += time.time() - t
+            st = BnbStats()
+            _check(lib, lib.nep_bnb_get_stats(tree, ctypes.byref(st)), "nep_bnb_get_stats")
+            its = np.zeros(max(1, st.n_lp_iters), np.int64)
+            _check(lib, lib.nep_bnb_get_lp_iters(tree, _ptr(its)), "nep_bnb_get_lp_iters")
+            res.lp_iters = its[:st.n_lp_iters].tolist()
+            if st.incumbent_source == 1:
+                n_fix = ctypes.c_int32()
+                z = np.zeros(lp.n_int)
+                idx = np.zeros(self._nb + 1, np.int32)
+                val = np.zeros(self._nb + 1)
+                _check(lib, lib.nep_bnb_incumbent(tree, _ptr(z), ctypes.byref(n_fix), _ptr(idx), _ptr(val)),
+                       "nep_bnb_incumbent")
+                res.objective, res.z = float(st.incumbent), z
+                res.incumbent_slot = int(st.incumbent_slot)
+                k = n_fix.value
+                self.inc_node = _Node(st.incumbent, idx[:k].astype(np.int64), val[:k].copy(), LEAF, None, 0)
+            elif st.incumbent_source == 0:
+                res.objective = None
+        finally:
+            lib.nep_bnb_destroy(tree)
+        names = ("certified", "bound", "limit", "infeasible", "cutoff", "numerical", "presolve_infeasible")
+        res.lp_status = {k: int(st.lp_status[i]) for i, k in enumerate(names)}
+        res.lp_status_kind = {kn: {k: int(st.lp_status_kind[q][i]) for i, k in enumerate(names)}
+                              for q, kn in ((NODE, "node"), (LEAF, "leaf"), (RETRY, "retry"), (REFROOT, "refroot"))}
+        for k in ("nodes", "leaves", "lps", "certified", "lp_iterations", "unresolved", "drained", "advance_calls",
+                  "inflight_sum", "heuristic_incumbents"):
+            setattr(res, k, int(getattr(st, k)))
+        res.heuristic_incumbents = int(st.heuristic_incumbents)
+        tm = res.timing
+        tm["advance"], tm["finish"], tm["submit"] = st.advance_seconds, st.finish_seconds, st.submit_seconds
+        tm["drain"], tm["root"] = st.drain_seconds, st.root_seconds
+        res.native = True
+        t_end = time.perf_counter()
+        res.bound = float(st.bound)
+        if res.objective is not None and res.incumbent_slot is not None:
+            res.x = lp.routing(res.incumbent_slot)
+            if self.polish_tol:
+                self._polish(res)
+        if res.objective is not None and self.repair is not None:
+            res.x, dobj, res.repaired = self.repair(res.x, res.z)
+            res.objective += dobj
+            if not res.repaired:
+                self.log("incumbent routing: CPU repair incomplete")
+        if res.objective is None:
+            res.status = LIMIT if (st.limit_hit or st.any_unresolved) else INFEASIBLE
+        else:
+            res.status = LIMIT if (st.limit_hit or st.unresolved_below) else OPTIMAL
+        res.timing["end"] = time.perf_counter() - t_end
+        res.seconds = time.time() - t0
+        return res
+
     def solve(self):
+        if self._native_ok(self.comm):
+            return self._solve_native()
         t0 = self.t0 = time.time()
         self.res = res = BnBResult()
         lp = self.lp

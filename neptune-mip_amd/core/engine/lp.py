@@ -18,7 +18,7 @@ STEP1, STEP2_DELETE, STEP2_CREATE = 1, 2, 3
 LP_OPTIMAL, LP_ITERATION_LIMIT, LP_INFEASIBLE, LP_CUTOFF, LP_NUMERICAL, LP_BOUND = 0, 1, 2, 3, 4, 5
 VARIANTS = {"MinDelay": MIN_DELAY, "MinUtilization": MIN_UTILIZATION,
             "MinDelayAndUtilization": MIN_DELAY_AND_UTILIZATION}
-API_VERSION = 10
+API_VERSION = 11
 RELAX_REFERENCE, RELAX_FACILITY = 0, 1
 
 _dp = ctypes.POINTER(ctypes.c_double)
@@ -59,6 +59,30 @@ class Stats(ctypes.Structure):
                 ("solve_ms", ctypes.c_double), ("lp_iterations", ctypes.c_int64)]
 
 
+class BnbParams(ctypes.Structure):
+    _fields_ = [("c0", ctypes.c_int32), ("c1", ctypes.c_int32), ("n0", ctypes.c_int32), ("n1", ctypes.c_int32),
+                ("n_int", ctypes.c_int32), ("F", ctypes.c_int32), ("N", ctypes.c_int32), ("warm", ctypes.c_int32),
+                ("check_every", ctypes.c_int32), ("root_check_every", ctypes.c_int32),
+                ("unit_flow_leaves", ctypes.c_int32), ("objective_integral", ctypes.c_int32),
+                ("primal_at_root", ctypes.c_int32), ("tol", ctypes.c_double), ("gap", ctypes.c_double),
+                ("bound_gap", ctypes.c_double), ("max_iters", ctypes.c_int64), ("node_max_iters", ctypes.c_int64),
+                ("root_max_iters", ctypes.c_int64), ("node_bound_res", ctypes.c_double),
+                ("retry_res", ctypes.c_double), ("flow_tol", ctypes.c_double), ("upper_bound", ctypes.c_double),
+                ("node_limit", ctypes.c_int64), ("time_limit", ctypes.c_double)]
+
+
+class BnbStats(ctypes.Structure):
+    _fields_ = [(k, ctypes.c_int64) for k in ("nodes", "leaves", "lps", "certified", "lp_iterations", "unresolved",
+                                              "drained")] + \
+               [("lp_status", ctypes.c_int64 * 7), ("lp_status_kind", (ctypes.c_int64 * 7) * 4)] + \
+               [(k, ctypes.c_int64) for k in ("advance_calls", "inflight_sum", "lp_incumbents", "heuristic_incumbents",
+                                              "n_lp_iters")] + \
+               [(k, ctypes.c_double) for k in ("advance_seconds", "finish_seconds", "submit_seconds", "drain_seconds",
+                                               "root_seconds", "bound", "incumbent")] + \
+               [(k, ctypes.c_int32) for k in ("incumbent_source", "incumbent_slot", "limit_hit", "any_unresolved",
+                                              "unresolved_below")]
+
+
 # every entry point declared in include/neptune_lp.h
 EXPORTS = ("nep_model_create", "nep_model_destroy", "nep_model_get_info", "nep_lp_solve_batch",
            "nep_lp_submit", "nep_lp_advance", "nep_lp_active",
@@ -67,7 +91,9 @@ EXPORTS = ("nep_model_create", "nep_model_destroy", "nep_model_get_info", "nep_l
            "nep_last_error", "nep_api_version", "nep_lp_get_diag", "nep_debug_build", "nep_debug_state",
            "nep_debug_presolve", "nep_lp_set_params", "nep_lp_get_flows", "nep_lp_routing_entries",
            "nep_lp_allocation_entries", "nep_lp_score_check", "nep_round_leaf", "nep_lp_copy_routing",
-           "nep_lp_get_solutions", "nep_round_leaves", "nep_lp_set_reference_weight")
+           "nep_lp_get_solutions", "nep_round_leaves", "nep_lp_set_reference_weight",
+           "nep_bnb_create", "nep_bnb_destroy", "nep_bnb_add_leaf", "nep_bnb_set_incumbent", "nep_bnb_event_data",
+           "nep_bnb_run", "nep_bnb_get_stats", "nep_bnb_get_lp_iters", "nep_bnb_incumbent")
 SCORE_FIELDS = ("network_delay", "nodes_used", "node_cost", "bad_c_x", "bad_memory", "bad_handle", "bad_cpu",
                 "bad_n_c", "bad_budget", "handle_maxdev", "cpu_maxexcess")
 
@@ -121,6 +147,17 @@ def load_library(path=None):
     lib.nep_debug_presolve.argtypes = [ctypes.POINTER(ModelDesc), i32, _dp, _dp, pi32, pi32, _dp, _dp]
     lib.nep_lp_set_params.argtypes = [vp, ctypes.c_double, ctypes.c_double]
     lib.nep_lp_set_reference_weight.argtypes = [vp, ctypes.c_double]
+    lib.nep_bnb_create.argtypes = [vp, vp, ctypes.POINTER(BnbParams), _dp, _dp]
+    lib.nep_bnb_create.restype = vp
+    lib.nep_bnb_destroy.argtypes = [vp]
+    lib.nep_bnb_destroy.restype = None
+    lib.nep_bnb_add_leaf.argtypes = [vp, i32, pi32, _dp, ctypes.c_double, i32]
+    lib.nep_bnb_set_incumbent.argtypes = [vp, ctypes.c_double]
+    lib.nep_bnb_event_data.argtypes = [vp, _dp, ctypes.POINTER(ctypes.c_float)]
+    lib.nep_bnb_run.argtypes = [vp, pi32]
+    lib.nep_bnb_get_stats.argtypes = [vp, ctypes.POINTER(BnbStats)]
+    lib.nep_bnb_get_lp_iters.argtypes = [vp, pi64]
+    lib.nep_bnb_incumbent.argtypes = [vp, _dp, pi32, pi32, _dp]
     lib.nep_lp_get_flows.argtypes = [vp, i32, pi32, ctypes.POINTER(ctypes.c_float)]
     lib.nep_lp_get_flows_split.argtypes = [vp, i32, pi32, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float)]
     lib.nep_lp_routing_entries.argtypes = [vp, i32, ctypes.c_double, i32, i64, pi64, pi32, pi32, _dp]

@@ -1,0 +1,814 @@
+// nep_bnb.cpp — the branch-and-bound's tree search, native (include/neptune_lp.h nep_bnb_*).
+//
+// The streaming best-first search of core/engine/bnb.py (BranchAndBound.solve, single rank) as a C++ client of
+// the engine's C ABI: the open-node heap, the rounding-leaf and retry queues, node selection, the warm-start
+// source of every submit (parent slot / root state), the per-engine slot free lists, each finished LP's
+// processing (prune, incumbent, retry, branching variable, rounding leaves, children) and the submit of the
+// next nodes all run here, one call per search (nep_bnb_run returns only for the events the Python caller
+// handles: the root's primal heuristic, the end).  It replaces, per finished node LP, ~30 Python / numpy calls
+// (the host share of the 64x32 search, DESIGN.md §7 "Native tree search").  Decision order and tie-breaks are
+// bnb.py's, so the two searches visit the same tree (tests/test_gpu_bnb_native.py compares them).
+//
+// Reference: SCIP's tree search inside pywraplp Solver.Solve() (core/solvers/solver.py:35-40).
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <deque>
+#include <limits>
+#include <memory>
+#include <queue>
+#include <string>
+#include <unordered_set>
+#include <vector>
+
+#include "../../include/neptune_lp.h"
+
+namespace {
+
+constexpr double INF = std::numeric_limits<double>::infinity();
+enum Kind { NODE = 0, LEAF = 1, RETRY = 2, REFROOT = 3 };
+// lp status columns of nep_bnb_stats.lp_status: certified, bound, limit, infeasible, cutoff, numerical, presolve
+int status_col(int st) {
+  switch (st) {
+    case NEP_LP_OPTIMAL: return 0;
+    case NEP_LP_BOUND: return 1;
+    case NEP_LP_ITERATION_LIMIT: return 2;
+    case NEP_LP_INFEASIBLE: return 3;
+    case NEP_LP_CUTOFF: return 4;
+    default: return 5;
+  }
+}
+
+struct Engine;
+struct Parent {
+  Engine *eng = nullptr;
+  int slot = -1;
+  int64_t gen = -1;
+};
+
+struct Node {
+  double bound;
+  std::vector<int32_t> idx;
+  std::vector<double> val;
+  int kind;
+  Parent parent;
+  int depth;
+};
+using NodeP = std::shared_ptr<Node>;
+
+struct Engine {
+  void *lp = nullptr;
+  int n_int = 0;                // this model's integer vector length (its boxes, solutions)
+  int max_batch = 0, reserved = 0, root_slot = -1, inc_slot = -1;
+  std::vector<int64_t> gen;
+  std::deque<int> free;
+  bool root_ready = false, root_state = false;
+  int inflight = 0;
+  std::vector<NodeP> running;   // slot -> node in flight
+};
+
+struct HeapItem {
+  double bound;
+  int negdepth;
+  int64_t seq;
+  NodeP node;
+  bool operator>(const HeapItem &o) const {   // min-heap on (bound, -depth, seq), as bnb.py's heapq tuples
+    if (bound != o.bound) return bound > o.bound;
+    if (negdepth != o.negdepth) return negdepth > o.negdepth;
+    return seq > o.seq;
+  }
+};
+
+double now_s() {
+  using namespace std::chrono;
+  return duration<double>(steady_clock::now().time_since_epoch()).count();
+}
+
+}  // namespace
+
+struct NepBnb {
+  nep_bnb_params p{};
+  Engine L, B;
+  bool two = false;
+  std::vector<double> fn_mem, node_mem;
+  std::priority_queue<HeapItem, std::vector<HeapItem>, std::greater<HeapItem>> heap;
+  std::deque<NodeP> pending, retry;
+  std::vector<NodeP> seeds;   // seed leaves, queued when the root finishes
+  NodeP refroot;
+  std::unordered_set<std::string> seen;
+  std::vector<double> unresolved_bounds;
+  std::vector<int64_t> lp_iters;
+  int64_t seq = 0;
+  double inc = INF;
+  int inc_source = 0;        // 0 none, 1 an LP leaf (inc_slot / kept slot), 2 external (nep_bnb_set_incumbent)
+  int inc_slot = -1;         // slot of the leaf engine holding the incumbent's state
+  int keep_slot = -1;        // (warm = 0) a working slot kept for the incumbent
+  NodeP inc_node;
+  std::vector<double> inc_z;
+  nep_bnb_stats st{};
+  double t0 = 0.0;
+  bool started = false, finished = false, limit_hit = false;
+  // the root event (primal heuristic at the root branching node)
+  bool root_event_pending = false, root_event_done = false;
+  std::vector<double> ev_z;
+  std::vector<float> ev_flow;
+  NodeP ev_node;
+  Parent ev_parent;
+  double ev_bound = -INF;
+  // scratch
+  std::vector<int32_t> sl, done_slots, sts;
+  std::vector<double> obj, pobj, lbv, ubv;
+  std::vector<int64_t> its;
+
+  int nb() const { return (p.c1 - p.c0) + (p.n0 >= 0 ? p.n1 - p.n0 : 0); }
+  double gap_abs(double incv) const {
+    if (!std::isfinite(incv)) return 0.0;
+    double g = p.gap * std::max(1.0, std::fabs(incv));
+    if (p.objective_integral) g = std::max(g, 1.0 - std::min(0.5, 1e-6 + 1e-9 * std::fabs(incv)));
+    return g;
+  }
+  bool pruned(double bound) const { return bound >= inc - gap_abs(inc); }
+  static std::string key_of(const std::vector<double> &val) {
+    std::string k((val.size() + 7) / 8, '\0');
+    for (size_t i = 0; i < val.size(); ++i)
+      if (val[i] > 0.5) k[i / 8] = (char)(k[i / 8] | (0x80 >> (i % 8)));
+    return k + std::to_string(val.size());
+  }
+  void push_heap(const NodeP &n) { heap.push(HeapItem{n->bound, -n->depth, seq++, n}); }
+  Engine *engines[2] = {nullptr, nullptr};
+  int n_engines() const { return two ? 2 : 1; }
+
+  void set_cutoffs() {
+    for (int e = 0; e < n_engines(); ++e) nep_lp_set_params(engines[e]->lp, p.tol, std::min(inc, p.upper_bound));
+  }
+
+  int submit(std::vector<std::pair<Engine *, std::pair<int, NodeP>>> &items);
+  int finish_block(Engine &eng, int nd);
+  int finish_one(Engine &eng, int slot, const NodeP &node, int status, double o, double po, int64_t iters,
+                 const float *flow, const double *z);
+  void round_all(const Node &node, const float *flow, const double *z, double bound, const Parent &me);
+  int branch_var(const Node &node, const float *flow, const double *z) const;
+  int drain_and_close();
+};
+
+namespace {
+
+void init_engine(Engine &e, void *lp, int reserved) {
+  nep_model_info info{};
+  nep_model_get_info(lp, &info);
+  e.lp = lp;
+  e.n_int = info.n_int;
+  e.max_batch = info.max_batch;
+  e.reserved = info.max_batch > reserved ? reserved : 0;
+  e.root_slot = info.max_batch - 1;
+  e.inc_slot = info.max_batch - 2;
+  e.gen.assign(info.max_batch, 0);
+  e.running.assign(info.max_batch, nullptr);
+  for (int s = 0; s < info.max_batch - e.reserved; ++s) e.free.push_back(s);
+}
+
+}  // namespace
+
+// one nep_lp_submit per (engine, warm, budget, bound_res, check_every) group, warm-start copies first
+int NepBnb::submit(std::vector<std::pair<Engine *, std::pair<int, NodeP>>> &items) {
+  struct Group {
+    Engine *eng;
+    bool warm;
+    int64_t budget;
+    double bres;
+    int ce;
+    std::vector<std::pair<int, NodeP>> its;
+  };
+  std::vector<Group> groups;
+  std::vector<std::pair<int, int>> copies[2];   // per engine (leaf first): (src, dst)
+  const double cutoff = std::min(inc, p.upper_bound);
+  for (auto &it : items) {
+    Engine *eng = it.first;
+    const int slot = it.second.first;
+    const NodeP &node = it.second.second;
+    bool warm = false;
+    int src = -1;
+    if (p.warm && eng->root_ready) {
+      src = eng->root_state ? eng->root_slot : -1;
+      if (node->parent.eng == eng && node->parent.slot >= 0 && eng->gen[node->parent.slot] == node->parent.gen)
+        src = node->parent.slot;
+      if (src >= 0) {
+        if (src != slot) copies[eng == &L ? 0 : 1].push_back({src, slot});
+        warm = true;
+      }
+    }
+    const int64_t budget = (node->kind == RETRY || node->kind == REFROOT || !eng->root_ready)
+                               ? p.root_max_iters
+                               : (node->kind == NODE ? p.node_max_iters : p.max_iters);
+    const double bres = (node->kind == NODE && (eng->root_ready || two)) ? p.node_bound_res : 0.0;
+    const int ce = (node->kind == REFROOT || !eng->root_ready) ? p.root_check_every : p.check_every;
+    Group *g = nullptr;
+    for (auto &gg : groups)
+      if (gg.eng == eng && gg.warm == warm && gg.budget == budget && gg.bres == bres && gg.ce == ce) g = &gg;
+    if (!g) {
+      groups.push_back(Group{eng, warm, budget, bres, ce, {}});
+      g = &groups.back();
+    }
+    g->its.push_back({slot, node});
+  }
+  // copies: a slot that is both a parent state (source) and a new node's slot (destination) is read before
+  // it is overwritten; a cycle falls back to the root's state
+  for (int e = 0; e < 2; ++e) {
+    Engine *eng = e == 0 ? &L : &B;
+    auto &cps = copies[e];
+    while (!cps.empty()) {
+      size_t k = cps.size();
+      for (size_t i = 0; i < cps.size() && k == cps.size(); ++i) {
+        bool is_src = false;
+        for (auto &c : cps) is_src |= c.first == cps[i].second;
+        if (!is_src) k = i;
+      }
+      if (k == cps.size()) {
+        cps[0].first = eng->root_slot;
+        continue;
+      }
+      const auto c = cps[k];
+      cps.erase(cps.begin() + k);
+      int rc = nep_lp_copy_state(eng->lp, c.first, c.second);
+      if (rc) return rc;
+    }
+  }
+  for (auto &g : groups) {
+    const int n = (int)g.its.size(), ni = g.eng->n_int;
+    sl.resize(n);
+    lbv.assign((size_t)n * ni, -INF);
+    ubv.assign((size_t)n * ni, INF);
+    for (int b = 0; b < n; ++b) {
+      sl[b] = g.its[b].first;
+      const Node &nd = *g.its[b].second;
+      for (size_t q = 0; q < nd.idx.size(); ++q) {
+        lbv[(size_t)b * ni + nd.idx[q]] = nd.val[q];
+        ubv[(size_t)b * ni + nd.idx[q]] = nd.val[q];
+      }
+    }
+    nep_lp_opts o{};
+    o.tol = p.tol;
+    o.cutoff = std::isfinite(cutoff) ? cutoff : INF;
+    o.max_iters = g.budget;
+    o.check_every = g.ce;
+    o.warm_start = g.warm ? 1 : 0;
+    o.gap_tol = (two && g.eng == &B) ? p.bound_gap : 0.0;
+    o.bound_res = g.bres;
+    sts.assign(n, 0);
+    int rc = nep_lp_submit(g.eng->lp, n, sl.data(), lbv.data(), ubv.data(), &o, sts.data());
+    if (rc) return rc;
+    for (int b = 0; b < n; ++b) {
+      const int slot = sl[b];
+      const NodeP &node = g.its[b].second;
+      g.eng->gen[slot] += 1;
+      st.lps += 1;
+      if (sts[b] == NEP_LP_INFEASIBLE) {
+        st.lp_status[6] += 1;
+        st.lp_status_kind[node->kind][6] += 1;
+        g.eng->free.push_back(slot);
+        if (node->kind == REFROOT) g.eng->root_ready = true;   // every leaf is a sub-box of it: no root state
+      } else {
+        g.eng->running[slot] = node;
+        g.eng->inflight += 1;
+      }
+    }
+  }
+  return NEP_OK;
+}
+
+int NepBnb::branch_var(const Node &node, const float *flow, const double *z) const {
+  const int F = p.F, N = p.N;
+  std::vector<char> fixed(std::max(p.c1, p.n1) + 1, 0);
+  for (int32_t i : node.idx) fixed[i] = 1;
+  if (p.n0 >= 0) {
+    int best = -1;
+    double bv = -INF;
+    for (int j = 0; j < N; ++j) {
+      double in = 0.0;
+      for (int f = 0; f < F; ++f) in += (double)flow[(size_t)f * N + j];
+      if (!fixed[p.n0 + j] && in > p.flow_tol && in > bv) { bv = in; best = j; }
+    }
+    if (best >= 0) return p.n0 + best;
+  }
+  {
+    int best = -1;
+    double bv = -INF;
+    for (int k = 0; k < F * N; ++k) {
+      const double fl = (double)flow[k];
+      if (!fixed[p.c0 + k] && fl > p.flow_tol && fl > bv) { bv = fl; best = k; }
+    }
+    if (best >= 0) return p.c0 + best;
+  }
+  int best = -1;
+  double bv = -INF;
+  for (int k = p.c0; k < p.c1; ++k)
+    if (!fixed[k] && z[k] > bv) { bv = z[k]; best = k; }
+  if (p.n0 >= 0)
+    for (int k = p.n0; k < p.n1; ++k)
+      if (!fixed[k] && z[k] > bv) { bv = z[k]; best = k; }
+  return best;
+}
+
+void NepBnb::round_all(const Node &node, const float *flow, const double *z, double bound, const Parent &me) {
+  const int F = p.F, N = p.N, FN = F * N;
+  std::vector<double> cfix(FN, -1.0), nfix;
+  if (p.n0 >= 0) nfix.assign(N, -1.0);
+  for (size_t q = 0; q < node.idx.size(); ++q) {
+    const int i = node.idx[q];
+    if (i >= p.c0 && i < p.c1) cfix[i - p.c0] = node.val[q];
+    else if (p.n0 >= 0 && i >= p.n0 && i < p.n1) nfix[i - p.n0] = node.val[q];
+  }
+  const int modes = p.unit_flow_leaves ? 3 : 2;
+  const int32_t by_flow[3] = {0, 1, 1};
+  const double thr[3] = {p.flow_tol, p.flow_tol, 1.0 - 1e-6};
+  std::vector<double> cout((size_t)modes * FN), nout(p.n0 >= 0 ? (size_t)modes * N : 0);
+  int32_t found[3] = {0, 0, 0};
+  if (nep_round_leaves(F, N, cfix.data(), p.n0 >= 0 ? nfix.data() : nullptr, flow, z + p.c0, fn_mem.data(),
+                       node_mem.data(), modes, by_flow, thr, cout.data(), p.n0 >= 0 ? nout.data() : nullptr,
+                       found) < 0)
+    return;
+  for (int q = 0; q < modes; ++q) {
+    if (!found[q]) continue;
+    auto leaf = std::make_shared<Node>();
+    leaf->kind = LEAF;
+    leaf->parent = me;
+    leaf->depth = node.depth + 1;
+    leaf->idx.reserve(nb());
+    for (int k = p.c0; k < p.c1; ++k) leaf->idx.push_back(k);
+    leaf->val.assign(cout.begin() + (size_t)q * FN, cout.begin() + (size_t)(q + 1) * FN);
+    if (p.n0 >= 0) {
+      for (int k = p.n0; k < p.n1; ++k) leaf->idx.push_back(k);
+      leaf->val.insert(leaf->val.end(), nout.begin() + (size_t)q * N, nout.begin() + (size_t)(q + 1) * N);
+    }
+    if (!seen.insert(key_of(leaf->val)).second) continue;
+    leaf->bound = bound;   // (no model-specific integer bound on this path)
+    if (!pruned(leaf->bound)) pending.push_back(leaf);
+  }
+}
+
+int NepBnb::finish_one(Engine &eng, int slot, const NodeP &node, int status, double o, double po, int64_t iters,
+                       const float *flow, const double *z) {
+  eng.inflight -= 1;
+  st.lp_iterations += iters;
+  lp_iters.push_back(iters);
+  const int col = status_col(status);
+  st.lp_status[col] += 1;
+  st.lp_status_kind[node->kind][col] += 1;
+  if (node->kind == REFROOT) {
+    if (p.warm && status != NEP_LP_INFEASIBLE && status != NEP_LP_CUTOFF) {
+      int rc = nep_lp_copy_state(eng.lp, slot, eng.root_slot);
+      if (rc) return rc;
+      eng.root_state = true;
+    }
+    eng.root_ready = true;
+    eng.free.push_back(slot);
+    return NEP_OK;
+  }
+  if (status == NEP_LP_OPTIMAL) st.certified += 1;
+  if (!eng.root_ready && node->depth == 0 && node->kind == NODE) {
+    st.root_seconds = now_s() - t0;
+    if (p.warm && status != NEP_LP_INFEASIBLE && status != NEP_LP_CUTOFF) {
+      int rc = nep_lp_copy_state(eng.lp, slot, eng.root_slot);
+      if (rc) return rc;
+      eng.root_state = true;
+    }
+    eng.root_ready = true;
+    const Parent me0{&eng, slot, eng.gen[slot]};
+    for (auto &s : seeds) {
+      if (!seen.insert(key_of(s->val)).second) continue;
+      s->parent = me0;
+      s->depth = 1;
+      pending.push_back(s);
+    }
+    seeds.clear();
+  }
+  if (status == NEP_LP_INFEASIBLE || status == NEP_LP_CUTOFF) {
+    eng.free.push_back(slot);
+    return NEP_OK;
+  }
+  const double bound = std::max(node->bound, o);
+  if (node->kind != NODE) {
+    st.leaves += 1;
+    bool kept = false;
+    if (status == NEP_LP_OPTIMAL) {
+      if (po < inc - gap_abs(inc)) {
+        inc = po;
+        inc_source = 1;
+        inc_node = node;
+        inc_z.assign(eng.n_int, 0.0);
+        int rc = nep_lp_get_solution(eng.lp, slot, inc_z.data(), nullptr);
+        if (rc) return rc;
+        if (p.warm) {
+          rc = nep_lp_copy_state(eng.lp, slot, eng.inc_slot);
+          if (rc) return rc;
+          inc_slot = eng.inc_slot;
+        } else {
+          if (keep_slot >= 0) eng.free.push_back(keep_slot);
+          keep_slot = slot;
+          inc_slot = slot;
+          kept = true;
+        }
+        st.lp_incumbents += 1;
+        set_cutoffs();
+      }
+    } else if (node->kind == LEAF) {
+      double pres = 0.0;
+      if (std::isfinite(p.retry_res)) {
+        double d[16];
+        int rc = nep_lp_get_diag(eng.lp, slot, d);
+        if (rc) return rc;
+        pres = d[3];
+      }
+      if (pres <= p.retry_res) {
+        auto r = std::make_shared<Node>(*node);
+        r->bound = bound;
+        r->kind = RETRY;
+        r->parent = Parent{&eng, slot, eng.gen[slot]};
+        retry.push_back(r);
+      } else {
+        st.unresolved += 1;
+        unresolved_bounds.push_back(bound);
+      }
+    } else {
+      st.unresolved += 1;
+      unresolved_bounds.push_back(bound);
+    }
+    if (!kept) eng.free.push_back(slot);
+    return NEP_OK;
+  }
+  if (pruned(bound)) {
+    eng.free.push_back(slot);
+    return NEP_OK;
+  }
+  st.nodes += 1;
+  const Parent me{&eng, slot, eng.gen[slot]};
+  round_all(*node, flow, z, bound, me);
+  if (p.primal_at_root && node->depth == 0 && !root_event_done) {
+    // the caller's primal heuristic runs on this node's LP (z, flows) before the search goes on
+    root_event_pending = true;
+    ev_z.assign(z, z + eng.n_int);
+    ev_flow.assign(flow, flow + (size_t)p.F * p.N);
+    ev_node = node;
+    ev_parent = me;
+    ev_bound = bound;
+  }
+  const int var = branch_var(*node, flow, z);
+  if (var >= 0) {
+    for (double v : {1.0, 0.0}) {
+      auto ch = std::make_shared<Node>();
+      ch->idx = node->idx;
+      ch->idx.push_back(var);
+      ch->val = node->val;
+      ch->val.push_back(v);
+      ch->bound = bound;
+      if (pruned(ch->bound)) continue;
+      ch->kind = (int)ch->idx.size() >= nb() ? LEAF : NODE;
+      ch->parent = me;
+      ch->depth = node->depth + 1;
+      push_heap(ch);
+    }
+  }
+  eng.free.push_back(slot);   // most recently finished last: its state survives longest
+  return NEP_OK;
+}
+
+// every finished LP of one advance of `eng`: the flows / integer vectors of the branching nodes that will
+// branch, read in one device call each, then each LP in order
+int NepBnb::finish_block(Engine &eng, int nd) {
+  std::vector<int32_t> want;
+  for (int i = 0; i < nd; ++i) {
+    const NodeP &node = eng.running[done_slots[i]];
+    if (!node || node->kind != NODE || sts[i] == NEP_LP_INFEASIBLE || sts[i] == NEP_LP_CUTOFF) continue;
+    if (pruned(std::max(node->bound, obj[i]))) continue;
+    want.push_back(done_slots[i]);
+  }
+  const size_t FN = (size_t)p.F * p.N;
+  const int ni = eng.n_int;
+  std::vector<float> fl(want.size() * FN);
+  std::vector<double> zs(want.size() * ni);
+  if (!want.empty()) {
+    int rc = nep_lp_get_flows(eng.lp, (int)want.size(), want.data(), fl.data());
+    if (rc) return rc;
+    rc = nep_lp_get_solutions(eng.lp, (int)want.size(), want.data(), zs.data());
+    if (rc) return rc;
+  }
+  // (copies: finish_one may submit nothing, but the outputs are reused by later advances)
+  const std::vector<int32_t> ds(done_slots.begin(), done_slots.begin() + nd);
+  const std::vector<int32_t> ss(sts.begin(), sts.begin() + nd);
+  const std::vector<double> ob(obj.begin(), obj.begin() + nd), po(pobj.begin(), pobj.begin() + nd);
+  const std::vector<int64_t> it(its.begin(), its.begin() + nd);
+  for (int i = 0; i < nd; ++i) {
+    const int slot = ds[i];
+    NodeP node = eng.running[slot];
+    eng.running[slot] = nullptr;
+    if (!node) continue;
+    const float *f = nullptr;
+    const double *z = nullptr;
+    for (size_t w = 0; w < want.size(); ++w)
+      if (want[w] == slot) { f = fl.data() + w * FN; z = zs.data() + w * ni; }
+    std::vector<float> fl1;
+    std::vector<double> z1;
+    if (node->kind == NODE && !f && ss[i] != NEP_LP_INFEASIBLE && ss[i] != NEP_LP_CUTOFF &&
+        !pruned(std::max(node->bound, ob[i]))) {
+      // (the incumbent improved within this block: read it now)
+      fl1.resize(FN);
+      z1.resize(ni);
+      int rc = nep_lp_get_flows(eng.lp, 1, &slot, fl1.data());
+      if (!rc) rc = nep_lp_get_solution(eng.lp, slot, z1.data(), nullptr);
+      if (rc) return rc;
+      f = fl1.data();
+      z = z1.data();
+    }
+    int rc = finish_one(eng, slot, node, ss[i], ob[i], po[i], it[i], f, z);
+    if (rc) return rc;
+  }
+  return NEP_OK;
+}
+
+int NepBnb::drain_and_close() {
+  const double t = now_s();
+  std::vector<double> open;
+  for (int e = 0; e < n_engines(); ++e)
+    for (auto &n : engines[e]->running)
+      if (n && n->kind != REFROOT) open.push_back(n->bound);
+  st.drained = (int64_t)open.size();
+  for (int e = 0; e < n_engines(); ++e)
+    if (nep_lp_active(engines[e]->lp) > 0) nep_lp_set_params(engines[e]->lp, p.tol, -INF);
+  for (int e = 0; e < n_engines(); ++e) {
+    Engine &eng = *engines[e];
+    while (nep_lp_active(eng.lp) > 0) {
+      int32_t nd = 0;
+      int rc = nep_lp_advance(eng.lp, nep_lp_active(eng.lp), &nd, done_slots.data(), obj.data(), pobj.data(),
+                              sts.data(), its.data());
+      if (rc) return rc;
+      for (int i = 0; i < nd; ++i) {
+        NodeP n = eng.running[done_slots[i]];
+        eng.running[done_slots[i]] = nullptr;
+        if (n && n->kind != REFROOT && sts[i] != NEP_LP_INFEASIBLE) open.push_back(std::max(n->bound, obj[i]));
+      }
+    }
+  }
+  st.drain_seconds = now_s() - t;
+  while (!heap.empty()) { open.push_back(heap.top().bound); heap.pop(); }
+  for (auto &n : pending) open.push_back(n->bound);
+  for (auto &n : retry) open.push_back(n->bound);
+  for (double b : unresolved_bounds) open.push_back(b);
+  double bound = inc;
+  for (double b : open) bound = std::min(bound, b);
+  st.bound = bound;
+  st.any_unresolved = unresolved_bounds.empty() ? 0 : 1;
+  st.unresolved_below = 0;
+  for (double b : unresolved_bounds)
+    if (b < inc - gap_abs(inc)) st.unresolved_below = 1;
+  st.limit_hit = limit_hit ? 1 : 0;
+  st.incumbent = inc;
+  st.incumbent_source = inc_source;
+  st.incumbent_slot = inc_source == 1 ? inc_slot : -1;
+  finished = true;
+  return NEP_OK;
+}
+
+extern "C" {
+
+void *nep_bnb_create(void *leaf_model, void *bound_model, const nep_bnb_params *params, const double *fn_mem,
+                     const double *node_mem) {
+  if (!leaf_model || !params || !fn_mem || !node_mem) return nullptr;
+  auto *t = new NepBnb();
+  t->p = *params;
+  t->two = bound_model != nullptr;
+  t->fn_mem.assign(fn_mem, fn_mem + params->F);
+  t->node_mem.assign(node_mem, node_mem + params->N);
+  init_engine(t->L, leaf_model, 2);   // (bnb.py: root and incumbent slots whenever max_batch >= 3)
+  t->engines[0] = &t->L;
+  if (t->two) {
+    init_engine(t->B, bound_model, t->p.warm ? 1 : 0);
+    t->engines[0] = &t->B;   // (bnb.py's engine order: bound model first)
+    t->engines[1] = &t->L;
+  }
+  const int mb = std::max(t->L.max_batch, t->two ? t->B.max_batch : 0);
+  t->done_slots.assign(mb, 0);
+  t->sts.assign(mb, 0);
+  t->obj.assign(mb, 0.0);
+  t->pobj.assign(mb, 0.0);
+  t->its.assign(mb, 0);
+  // the root (the heap) and, with two models and warm starts, the reference root the leaves start from
+  auto root = std::make_shared<Node>();
+  root->bound = -INF;
+  root->kind = NODE;
+  root->depth = 0;
+  t->push_heap(root);
+  if (t->two) {
+    if (t->p.warm) {
+      t->refroot = std::make_shared<Node>();
+      t->refroot->bound = -INF;
+      t->refroot->kind = REFROOT;
+      t->refroot->depth = 0;
+    } else {
+      t->L.root_ready = true;
+    }
+  }
+  return t;
+}
+
+void nep_bnb_destroy(void *tree) { delete static_cast<NepBnb *>(tree); }
+
+int nep_bnb_add_leaf(void *tree, int32_t n, const int32_t *idx, const double *val, double bound, int32_t where) {
+  auto *t = static_cast<NepBnb *>(tree);
+  if (!t || n < 0 || (n > 0 && (!idx || !val))) return NEP_ERR_ARG;
+  auto leaf = std::make_shared<Node>();
+  leaf->idx.assign(idx, idx + n);
+  leaf->val.assign(val, val + n);
+  leaf->kind = LEAF;
+  leaf->bound = bound;
+  if (where == 0) {   // a seed leaf: queued when the root LP finishes
+    leaf->depth = 1;
+    t->seeds.push_back(leaf);
+    return NEP_OK;
+  }
+  // where = 1: a leaf of the root event's node (the primal heuristic), at the front of the leaf queue
+  if (!t->seen.insert(NepBnb::key_of(leaf->val)).second) return NEP_OK;
+  leaf->bound = std::max(t->ev_bound, bound);
+  leaf->parent = t->ev_parent;
+  leaf->depth = t->ev_node ? t->ev_node->depth + 1 : 1;
+  if (!t->pruned(leaf->bound)) t->pending.push_front(leaf);
+  return NEP_OK;
+}
+
+int nep_bnb_set_incumbent(void *tree, double value) {
+  auto *t = static_cast<NepBnb *>(tree);
+  if (!t) return NEP_ERR_ARG;
+  if (!(value < t->inc)) return NEP_OK;
+  t->inc = value;
+  t->inc_source = 2;
+  if (t->keep_slot >= 0) {
+    t->L.free.push_back(t->keep_slot);
+    t->keep_slot = -1;
+  }
+  t->inc_slot = -1;
+  t->inc_node = nullptr;
+  t->st.heuristic_incumbents += 1;
+  t->set_cutoffs();
+  return NEP_OK;
+}
+
+int nep_bnb_event_data(void *tree, double *z, float *flow) {
+  auto *t = static_cast<NepBnb *>(tree);
+  if (!t || t->ev_z.empty()) return NEP_ERR_STATE;
+  if (z) std::memcpy(z, t->ev_z.data(), t->ev_z.size() * sizeof(double));
+  if (flow) std::memcpy(flow, t->ev_flow.data(), t->ev_flow.size() * sizeof(float));
+  return NEP_OK;
+}
+
+int nep_bnb_run(void *tree, int32_t *event) {
+  auto *t = static_cast<NepBnb *>(tree);
+  if (!t || !event) return NEP_ERR_ARG;
+  *event = NEP_BNB_DONE;
+  if (t->finished) return NEP_OK;
+  if (!t->started) {
+    t->started = true;
+    t->t0 = now_s();
+  }
+  NepBnb &T = *t;
+  Engine &L = T.L, &B = T.B;
+  for (;;) {
+    if (T.root_event_pending) {   // the caller's primal heuristic on the root node
+      T.root_event_pending = false;
+      T.root_event_done = true;
+      *event = NEP_BNB_ROOT;
+      return NEP_OK;
+    }
+    const bool stop = T.st.nodes >= T.p.node_limit ||
+                      (T.p.time_limit > 0 && now_s() - T.t0 > T.p.time_limit);
+    int busy = 0;
+    for (int e = 0; e < T.n_engines(); ++e)
+      for (auto &n : T.engines[e]->running)
+        if (n && n->kind != REFROOT) ++busy;
+    const size_t open_n = T.heap.size() + T.pending.size() + T.retry.size() + busy;
+    if (open_n == 0) break;
+    if (stop) {
+      T.limit_hit = true;
+      break;
+    }
+    // fill the free slots: retries, rounding leaves, then best-first open nodes
+    std::vector<std::pair<Engine *, std::pair<int, NodeP>>> items;
+    if (!T.two) {
+      while (!L.free.empty() && (!T.retry.empty() || !T.pending.empty() || !T.heap.empty())) {
+        NodeP node;
+        if (!T.retry.empty()) {
+          node = T.retry.front();
+          T.retry.pop_front();
+        } else if (!T.pending.empty()) {
+          node = T.pending.front();
+          T.pending.pop_front();
+          if (T.pruned(node->bound)) continue;
+        } else {
+          node = T.heap.top().node;
+          T.heap.pop();
+          if (T.pruned(node->bound)) continue;
+        }
+        const int s = L.free.front();
+        L.free.pop_front();
+        items.push_back({&L, {s, node}});
+        if (!L.root_ready) break;   // the root runs alone (its state warm-starts everything after)
+      }
+    } else {
+      if (T.refroot && !L.free.empty()) {
+        const int s = L.free.front();
+        L.free.pop_front();
+        items.push_back({&L, {s, T.refroot}});
+        T.refroot = nullptr;
+      }
+      while (!B.free.empty() && !T.heap.empty() && (!B.root_ready || L.root_ready)) {
+        NodeP node = T.heap.top().node;
+        T.heap.pop();
+        if (T.pruned(node->bound)) continue;
+        if (node->kind != NODE) {   // a leaf from branching: the reference model's
+          T.pending.push_back(node);
+          continue;
+        }
+        const int s = B.free.front();
+        B.free.pop_front();
+        items.push_back({&B, {s, node}});
+        if (!B.root_ready) break;
+      }
+      while (L.root_ready && !L.free.empty() && (!T.retry.empty() || !T.pending.empty())) {
+        NodeP node;
+        if (!T.retry.empty()) {
+          node = T.retry.front();
+          T.retry.pop_front();
+        } else {
+          node = T.pending.front();
+          T.pending.pop_front();
+        }
+        if (node->kind == LEAF && T.pruned(node->bound)) continue;
+        const int s = L.free.front();
+        L.free.pop_front();
+        items.push_back({&L, {s, node}});
+      }
+    }
+    double t1 = now_s();
+    if (!items.empty()) {
+      int rc = T.submit(items);
+      if (rc) return rc;
+    }
+    double t2 = now_s();
+    T.st.submit_seconds += t2 - t1;
+    int inflight = 0;
+    for (int e = 0; e < T.n_engines(); ++e) inflight += T.engines[e]->inflight;
+    if (inflight == 0) continue;
+    T.st.advance_calls += 1;
+    T.st.inflight_sum += busy;
+    for (int e = 0; e < T.n_engines(); ++e) {
+      Engine &eng = *T.engines[e];
+      if (eng.inflight <= 0) continue;
+      const int min_done = T.two ? 0 : (T.p.time_limit > 0 ? 0 : 1);
+      int32_t nd = 0;
+      int rc = nep_lp_advance(eng.lp, min_done, &nd, T.done_slots.data(), T.obj.data(), T.pobj.data(),
+                              T.sts.data(), T.its.data());
+      if (rc) return rc;
+      const double t3 = now_s();
+      T.st.advance_seconds += t3 - t2;
+      rc = T.finish_block(eng, nd);
+      if (rc) return rc;
+      t2 = now_s();
+      T.st.finish_seconds += t2 - t3;
+    }
+  }
+  int rc = T.drain_and_close();
+  if (rc) return rc;
+  *event = NEP_BNB_DONE;
+  return NEP_OK;
+}
+
+int nep_bnb_get_stats(void *tree, nep_bnb_stats *out) {
+  auto *t = static_cast<NepBnb *>(tree);
+  if (!t || !out) return NEP_ERR_ARG;
+  *out = t->st;
+  out->n_lp_iters = (int64_t)t->lp_iters.size();
+  return NEP_OK;
+}
+
+int nep_bnb_get_lp_iters(void *tree, int64_t *out) {
+  auto *t = static_cast<NepBnb *>(tree);
+  if (!t || !out) return NEP_ERR_ARG;
+  if (!t->lp_iters.empty()) std::memcpy(out, t->lp_iters.data(), t->lp_iters.size() * sizeof(int64_t));
+  return NEP_OK;
+}
+
+int nep_bnb_incumbent(void *tree, double *z, int32_t *n_fix, int32_t *idx, double *val) {
+  auto *t = static_cast<NepBnb *>(tree);
+  if (!t) return NEP_ERR_ARG;
+  if (t->inc_source != 1 || !t->inc_node) {
+    if (n_fix) *n_fix = -1;
+    return NEP_OK;
+  }
+  if (z) std::memcpy(z, t->inc_z.data(), t->inc_z.size() * sizeof(double));
+  if (n_fix) *n_fix = (int32_t)t->inc_node->idx.size();
+  if (idx) std::memcpy(idx, t->inc_node->idx.data(), t->inc_node->idx.size() * sizeof(int32_t));
+  if (val) std::memcpy(val, t->inc_node->val.data(), t->inc_node->val.size() * sizeof(double));
+  return NEP_OK;
+}
+
+}  // extern "C"

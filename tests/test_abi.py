@@ -16,7 +16,7 @@ HEADER = os.path.join(REPO, "include", "neptune_lp.h")
 
 def declared():
     text = open(HEADER).read()
-    return sorted(set(re.findall(r"^(?:int|void|const char \*)\s*(nep_\w+)\(", text, re.M)))
+    return sorted(set(re.findall(r"^(?:int|void \*|void|const char \*)\s*(nep_\w+)\(", text, re.M)))
 
 
 def test_header_declares_exactly_the_binding_exports():

@@ -1,0 +1,81 @@
+"""The native tree search (csrc/nep_bnb.cpp, nep_bnb_*) against core/engine/bnb.py's Python
+loop: on the golden step-1 instances both searches end OPTIMAL at the recorded MIP with the same tree (nodes,
+LPs — bnb.py's decision order and tie-breaks, the same engine calls), and on the 64x32 / 256x128 synthetic
+instances the native loop's host share of the wall time (everything outside the device waits of
+nep_lp_advance) is below 25 % (64x32: 0.149 native vs 0.220 Python, profiles/r05/native)."""
+import math
+
+import pytest
+
+from golden_util import golden, payload
+
+pytestmark = pytest.mark.gpu
+G = golden()
+CASES = ["payload", "testpy", "syn_4x3_s0_r0.5_NeptuneMinDelayAndUtilization", "syn_4x3_s0_r0.5_NeptuneMinDelay",
+         "syn_4x3_s0_r0.5_NeptuneMinUtilization", "syn_6x4_s1_r0.3_NeptuneMinDelayAndUtilization",
+         "syn_8x4_s2_r0.1_NeptuneMinDelayAndUtilization", "sim0_NeptuneMinDelay", "sim3_NeptuneMinDelayAndUtilization",
+         "sim2_NeptuneMinUtilization"]
+
+
+def _search(step1, data, native, **kw):
+    from core.solvers.neptune.neptune_step import make_lp
+    model = make_lp(data, step1.VARIANT, step1.step_id(), step1.batch + 2, **step1.model_kwargs())
+    bmodel = None
+    try:
+        bmodel = step1.bound_model(data, step1.batch + 1)
+        return step1.branch_and_bound(model, bmodel, native=native, **kw).solve()
+    finally:
+        model.close()
+        if bmodel is not None:
+            bmodel.close()
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_native_search_matches_python(name):
+    import core.solvers as S
+    from core.utils import data_to_solver_input
+    if name not in G:
+        pytest.skip("no golden")
+    p = payload(name)
+    data = data_to_solver_input(p, workload_coeff=p.get("workload_coeff", 1), with_db=False)
+    solver = S.SOLVERS[p["solver"]["type"]](**p["solver"].get("args", {}))
+    step1 = getattr(solver, "step1", None)
+    if step1 is None or not hasattr(step1, "branch_and_bound") or G[name]["models"][0]["status"] != 0:
+        pytest.skip("no NEPTUNE step 1 / no recorded step-1 optimum")
+    step1.load_data(data)
+    rp = _search(step1, data, False)
+    rn = _search(step1, data, True)
+    print(name, "python", rp.status, rp.objective, rp.nodes, rp.lps, "| native", rn.status, rn.objective, rn.nodes,
+          rn.lps)
+    assert rn.native and not rp.native
+    assert rn.status == rp.status == "OPTIMAL"
+    ref = G[name]["models"][0]["mip_objective"]
+    assert abs(rn.objective - ref) <= 1e-6 * max(1.0, abs(ref))
+    assert abs(rn.objective - rp.objective) <= 1e-9 * max(1.0, abs(rp.objective))
+    assert (rn.nodes, rn.lps, rn.leaves) == (rp.nodes, rp.lps, rp.leaves)
+
+
+@pytest.mark.parametrize("n,f,seconds", [(64, 32, 10.0), (256, 128, 20.0)])
+def test_native_search_host_share(n, f, seconds):
+    from core.solvers.neptune.neptune_step import NeptuneStep1CPUMinDelayAndUtilization
+    from core.utils import data_to_solver_input
+    from core.utils.synthetic import synthetic_payload
+    data = data_to_solver_input(synthetic_payload(n, f, seed=0), with_db=False)
+    out = {}
+    for native in (False, True):
+        st1 = NeptuneStep1CPUMinDelayAndUtilization(alpha=0.5, verbose=False, batch=32, lp_tol=1e-6, lp_max_iters=4096)
+        st1.load_data(data)
+        r = _search(st1, data, native, time_limit=seconds)
+        tm = r.timing
+        wall = r.seconds
+        host = 1.0 - tm["advance"] / wall
+        out[native] = (host, r.nodes, r.lps, r.objective, r.bound)
+        print(f"{n}x{f} {'native' if native else 'python'}: host {host:.3f} of {wall:.1f} s, nodes {r.nodes}, lps {r.lps}, "
+              f"incumbent {r.objective}, bound {r.bound}, timing {dict((k, round(v, 2)) for k, v in tm.items())}")
+        assert r.objective is not None and math.isfinite(r.bound) and r.bound <= r.objective + 1e-9
+    # the VERDICT's bar (host < 25 % of the B&B wall) on the native loop; at 64x32, where the per-LP Python work
+    # was the host share, it is also below the Python loop's (at 256x128 both are the native submit / rounding /
+    # device reads: equal within noise)
+    assert out[True][0] < 0.25
+    if n <= 64:
+        assert out[True][0] < out[False][0]
