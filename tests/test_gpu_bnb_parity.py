@@ -39,7 +39,7 @@ def test_bnb_node_lps_match_highs():
 
     try:
         Recording(m, data.workload_matrix, data.function_memory_matrix, data.node_memory_matrix, batch=32, tol=5e-7,
-                  time_limit=6.0, upper_bound=ub * (1 + 1e-6) + 1e-6, node_max_iters=1024).solve()
+                  time_limit=6.0, upper_bound=ub * (1 + 1e-6) + 1e-6, node_max_iters=1024, native=False).solve()
     finally:
         m.close()
     mdl = build_model(oracle_input(p, with_db=False), "MinDelayAndUtilization", step=1, alpha=0.5)
