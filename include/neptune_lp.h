@@ -278,6 +278,7 @@ typedef struct {
   int32_t c0, c1, n0, n1, n_int;   /* integer layout: c = z_int[c0:c1] (F x N), n = z_int[n0:n1] (n0 < 0: none) */
   int32_t F, N;
   int32_t warm;                    /* warm starts (reserves the leaf model's last two slots: root / incumbent state) */
+  int32_t batch, batch_b;          /* LPs in flight per model (leaf, bound); further free slots keep finished states */
   int32_t check_every, root_check_every;
   int32_t unit_flow_leaves;        /* a third rounding mode: (f, j) carrying a unit of flow */
   int32_t objective_integral;      /* every integral point's objective is integral: prune at incumbent - 1 */

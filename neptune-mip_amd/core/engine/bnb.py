@@ -167,6 +167,8 @@ class BranchAndBound:
         self.node_mem = np.asarray(node_mem, np.float64).reshape(self.N)
         self.reserved = 2 if lp.max_batch >= 3 else 0
         self.batch = max(1, min(int(batch), lp.max_batch - self.reserved))
+        # (the bound model: its slots beyond `batch` + its root's park finished parents' states)
+        self.batch_b = max(1, min(int(batch), bound_lp.max_batch - 1)) if bound_lp is not None else self.batch
         self.warm = bool(warm) and self.reserved == 2 and (bound_lp is None or bound_lp.max_batch >= 2)
         self.bound_lp = bound_lp
         # the bound model's LPs stop once their own gap (repaired point vs best bound) is within bound_gap:
@@ -755,7 +757,8 @@ class BranchAndBound:
         n0, n1 = self.n_range if self.n_range is not None else (-1, -1)
         inf = math.inf
         p = BnbParams(c0=self.c0, c1=self.c1, n0=n0, n1=n1, n_int=lp.n_int, F=self.F, N=self.N,
-                      warm=1 if self.warm else 0, check_every=int(self.check_every),
+                      warm=1 if self.warm else 0, batch=int(self.batch), batch_b=int(self.batch_b),
+                      check_every=int(self.check_every),
                       root_check_every=int(self.root_check_every), unit_flow_leaves=1 if len(self.round_modes) > 2 else 0,
                       objective_integral=1 if self.objective_integral else 0,
                       primal_at_root=1 if self.primal is not None else 0, tol=self.tol, gap=self.gap,
@@ -910,8 +913,12 @@ class BranchAndBound:
                 self._rebalance(inc)
             # fill the free slots: retries, rounding leaves, then best-first open nodes
             items = []
+            # at most `batch` LPs in flight per model; slots beyond that keep finished states (parked
+            # parents, least recently finished reused first)
+            capL = self.batch - L.inflight
+            capB = self.batch_b - B.inflight
             if not self.two:
-                while L.free and (self.retry or self.pending or self.heap):
+                while L.free and capL > 0 and (self.retry or self.pending or self.heap):
                     if self.retry:
                         node = self.retry.popleft()
                     elif self.pending:
@@ -923,15 +930,17 @@ class BranchAndBound:
                         if node.bound >= inc - self._gap_abs(inc):
                             continue
                     items.append((L, L.free.popleft(), node))
+                    capL -= 1
                     if not L.root_ready:
                         break                 # the root runs alone (its state warm-starts everything after)
             else:
-                if self.refroot is not None and L.free:
+                if self.refroot is not None and L.free and capL > 0:
                     items.append((L, L.free.popleft(), self.refroot))
+                    capL -= 1
                     self.refroot = None
                 # (the branching nodes wait for both roots: 32 bound LPs beside the lone reference root would
                 # starve its one-slot blocks — 512x256: not done after 60 s, 1.8 s alone)
-                while B.free and self.heap and (not B.root_ready or L.root_ready):
+                while B.free and capB > 0 and self.heap and (not B.root_ready or L.root_ready):
                     _, _, _, node = heapq.heappop(self.heap)
                     if node.bound >= inc - self._gap_abs(inc):
                         continue
@@ -939,13 +948,15 @@ class BranchAndBound:
                         self.pending.append(node)
                         continue
                     items.append((B, B.free.popleft(), node))
+                    capB -= 1
                     if not B.root_ready:
                         break
-                while L.root_ready and L.free and (self.retry or self.pending):
+                while L.root_ready and L.free and capL > 0 and (self.retry or self.pending):
                     node = self.retry.popleft() if self.retry else self.pending.popleft()
                     if node.kind == LEAF and node.bound >= inc - self._gap_abs(inc):
                         continue
                     items.append((L, L.free.popleft(), node))
+                    capL -= 1
             tm = res.timing
             t1 = time.perf_counter()
             if items:

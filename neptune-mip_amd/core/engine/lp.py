@@ -62,6 +62,7 @@ class Stats(ctypes.Structure):
 class BnbParams(ctypes.Structure):
     _fields_ = [("c0", ctypes.c_int32), ("c1", ctypes.c_int32), ("n0", ctypes.c_int32), ("n1", ctypes.c_int32),
                 ("n_int", ctypes.c_int32), ("F", ctypes.c_int32), ("N", ctypes.c_int32), ("warm", ctypes.c_int32),
+                ("batch", ctypes.c_int32), ("batch_b", ctypes.c_int32),
                 ("check_every", ctypes.c_int32), ("root_check_every", ctypes.c_int32),
                 ("unit_flow_leaves", ctypes.c_int32), ("objective_integral", ctypes.c_int32),
                 ("primal_at_root", ctypes.c_int32), ("tol", ctypes.c_double), ("gap", ctypes.c_double),

@@ -88,11 +88,15 @@ class NeptuneStepBase(Solver):
     # MinDelayAndUtilization); leaves stay on the reference model
     strengthen = True
 
+    # bound-model slots beyond the `batch` in flight and its root's: finished branching nodes' states stay there
+    # (least recently finished reused first) so their children warm-start from them (DESIGN.md §7 "Parked parents")
+    bound_park = 0
+
     def bound_model(self, data, max_batch):
         if not self.strengthen or self.step_id() != _lp.STEP1 or self.VARIANT == "MinDelay":
             return None
-        return make_lp(data, self.VARIANT, self.step_id(), max_batch, relaxation=_lp.RELAX_FACILITY,
-                       **self.model_kwargs())
+        return make_lp(data, self.VARIANT, self.step_id(), max_batch + int(self.bound_park),
+                       relaxation=_lp.RELAX_FACILITY, **self.model_kwargs())
 
     def integer_bound(self, layout=None):
         """bound(idx, val): a lower bound on the objective of every integral completion of a node's

@@ -693,8 +693,10 @@ int nep_bnb_run(void *tree, int32_t *event) {
     }
     // fill the free slots: retries, rounding leaves, then best-first open nodes
     std::vector<std::pair<Engine *, std::pair<int, NodeP>>> items;
+    // at most `batch` LPs in flight per model; further free slots keep finished states (parked parents)
+    int capL = T.p.batch - L.inflight, capB = T.p.batch_b - B.inflight;
     if (!T.two) {
-      while (!L.free.empty() && (!T.retry.empty() || !T.pending.empty() || !T.heap.empty())) {
+      while (!L.free.empty() && capL > 0 && (!T.retry.empty() || !T.pending.empty() || !T.heap.empty())) {
         NodeP node;
         if (!T.retry.empty()) {
           node = T.retry.front();
@@ -711,16 +713,18 @@ int nep_bnb_run(void *tree, int32_t *event) {
         const int s = L.free.front();
         L.free.pop_front();
         items.push_back({&L, {s, node}});
+        --capL;
         if (!L.root_ready) break;   // the root runs alone (its state warm-starts everything after)
       }
     } else {
-      if (T.refroot && !L.free.empty()) {
+      if (T.refroot && !L.free.empty() && capL > 0) {
         const int s = L.free.front();
         L.free.pop_front();
+        --capL;
         items.push_back({&L, {s, T.refroot}});
         T.refroot = nullptr;
       }
-      while (!B.free.empty() && !T.heap.empty() && (!B.root_ready || L.root_ready)) {
+      while (!B.free.empty() && capB > 0 && !T.heap.empty() && (!B.root_ready || L.root_ready)) {
         NodeP node = T.heap.top().node;
         T.heap.pop();
         if (T.pruned(node->bound)) continue;
@@ -731,9 +735,10 @@ int nep_bnb_run(void *tree, int32_t *event) {
         const int s = B.free.front();
         B.free.pop_front();
         items.push_back({&B, {s, node}});
+        --capB;
         if (!B.root_ready) break;
       }
-      while (L.root_ready && !L.free.empty() && (!T.retry.empty() || !T.pending.empty())) {
+      while (L.root_ready && !L.free.empty() && capL > 0 && (!T.retry.empty() || !T.pending.empty())) {
         NodeP node;
         if (!T.retry.empty()) {
           node = T.retry.front();
@@ -745,6 +750,7 @@ int nep_bnb_run(void *tree, int32_t *event) {
         if (node->kind == LEAF && T.pruned(node->bound)) continue;
         const int s = L.free.front();
         L.free.pop_front();
+        --capL;
         items.push_back({&L, {s, node}});
       }
     }

@@ -32,6 +32,7 @@ def main():
         if os.environ.get("BNB_MODE", "single") == "product":
             st1 = NeptuneStep1CPUMinDelayAndUtilization(alpha=0.5, verbose=False, batch=32, lp_tol=1e-6, lp_max_iters=4096)
             st1.load_data(data)
+            st1.bound_park = int(os.environ.get("BNB_PARK", st1.bound_park))
             bm = st1.bound_model(data, 33)
             res = st1.branch_and_bound(m, bm, time_limit=seconds, root_max_iters=400000, warm_weight_ref=wref).solve()
         else:
@@ -47,7 +48,7 @@ def main():
     d["build_seconds"] = build
     d["eta"] = m.info.step_size
     d["env"] = {k: os.environ.get(k) for k in ("NEP_HOST_INPUTS", "NEP_HOST_POWER", "NEPTUNE_LP_LIB", "BNB_WREF",
-                                                "BNB_MODE")}
+                                                "BNB_MODE", "BNB_PARK")}
     with open("/proc/self/maps") as fh:
         d["hip_runtime"] = sorted({ln.split()[-1] for ln in fh if "libamdhip64" in ln})
     print(json.dumps(d, default=float))
