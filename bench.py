@@ -79,6 +79,9 @@ def parse(argv=None):
     ap.add_argument("--omega-ref", type=float, default=8.0,
                     help="warm starts take their primal weight in [floor, cap] x (this x the model's cold-start weight "
                          "omega0) (nep_lp_set_reference_weight; 0: relative to the parent's final weight)")
+    ap.add_argument("--leaf-omega", default="",
+                    help="replay: warm-start weight band of leaf boxes (every c and n fixed) as 'floor:cap' multiples "
+                         "of the reference weight (default: the engine's 2,4 for every box)")
     ap.add_argument("--polish-after", type=float, default=0.0,
                     help="replay: warm-started node LPs start primal-feasibility polishing after this many iterations "
                          "(0: the engine's default, 256; -1: never)")
@@ -252,7 +255,7 @@ def cpu_baseline(N, F, seed, fix, budget, workers):
 
     t_start = time.perf_counter()
     pts = []
-    for n in (16, 24, 32, 48, 64, 96, 128):
+    for n in (16, 24, 32, 48, 64, 96, 128, 192, 256):   # (up to BASELINE config 3's size: a short extrapolation)
         f = max(1, n // 2)
         t0 = time.perf_counter()
         m, bnds = model_and_bounds(n, f, 1, seed)
@@ -464,8 +467,11 @@ class ReplayStream:
                           cutoff=math.inf if e.get("cutoff") is None else e["cutoff"])
             else:
                 kw = dict(max_iters=a.max_iters)
+            wf, wc = a.warm_omega_floor, 0.0
+            if "open" in e and getattr(a, "leaf_omega", ""):
+                wf, wc = (float(t) for t in a.leaf_omega.split(":"))
             st = m.submit([slot], lb[None], ub[None], tol=a.tol, check_every=a.check_every, warm_start=True,
-                          warm_omega_floor=a.warm_omega_floor, polish_after=getattr(a, "polish_after", 0.0), **kw)
+                          warm_omega_floor=wf, warm_omega_cap=wc, polish_after=getattr(a, "polish_after", 0.0), **kw)
             if int(st[0]) == LP_INFEASIBLE:
                 self.done.append((LP_INFEASIBLE, float("inf"), float("nan"), 0))
                 self.kinds.append((name, e["kind"]))

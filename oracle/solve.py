@@ -101,8 +101,14 @@ def run_flow(payload, time_limit=None):
             "score": {"step1": score1, "step2": score2}}
 
 
+_POOL_MODEL = None   # the model the forked pool workers inherit (lp_batch_cpu)
+
+
 def _one_lp(args):
-    m, lb, ub = args
+    idx, lo, hi = args
+    m = _POOL_MODEL
+    lb, ub = m["lb"].copy(), m["ub"].copy()
+    lb[idx], ub[idx] = lo, hi
     t = time.perf_counter()
     st, obj, _ = solve(m, relax=True, lb=lb, ub=ub)
     return st, obj, time.perf_counter() - t
@@ -110,10 +116,21 @@ def _one_lp(args):
 
 def lp_batch_cpu(m, bounds, workers=None):
     """Solve len(bounds) node LPs (lb, ub pairs) of one model, one per worker process.
-    Returns (statuses, objectives, wall seconds, workers used)."""
+    Returns (statuses, objectives, wall seconds, workers used).  The workers are forked with the model (not
+    pickled per task: a 256x128 model is ~0.4 GB); each task carries its bounds' difference from the model's."""
+    import multiprocessing as mp
+    global _POOL_MODEL
     workers = workers or os.cpu_count() or 1
-    t0 = time.perf_counter()
-    with ProcessPoolExecutor(max_workers=workers) as ex:
-        res = list(ex.map(_one_lp, [(m, lb, ub) for lb, ub in bounds]))
-    wall = time.perf_counter() - t0
+    tasks = []
+    for lb, ub in bounds:
+        idx = np.flatnonzero((lb != m["lb"]) | (ub != m["ub"]))
+        tasks.append((idx, lb[idx], ub[idx]))
+    _POOL_MODEL = m
+    try:
+        t0 = time.perf_counter()
+        with ProcessPoolExecutor(max_workers=workers, mp_context=mp.get_context("fork")) as ex:
+            res = list(ex.map(_one_lp, tasks))
+        wall = time.perf_counter() - t0
+    finally:
+        _POOL_MODEL = None
     return [r[0] for r in res], [r[1] for r in res], wall, workers

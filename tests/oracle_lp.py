@@ -77,7 +77,8 @@ class OracleLP:
     # streaming form (nep_lp_submit / nep_lp_advance): HiGHS solves each submitted node at once; advance
     # hands back up to min_done finished nodes per call, in slot order, like the engine's blocks
     def submit(self, slots, lb=None, ub=None, tol=1e-7, cutoff=math.inf, max_iters=0, check_every=64,
-               warm_start=False, warm_omega_floor=0.0, bound_res=0.0, gap_tol=0.0, polish_after=0.0):
+               warm_start=False, warm_omega_floor=0.0, bound_res=0.0, gap_tol=0.0, polish_after=0.0,
+               warm_omega_cap=0.0):
         slots = np.asarray(slots).reshape(-1)
         self._cutoff = cutoff
         r = self.solve(slots, lb, ub, tol=tol, cutoff=math.inf)
@@ -175,7 +176,8 @@ class StreamingOracleLP(OracleLP):
     the pre-polish incumbent: round-2 ADVICE)."""
 
     def submit(self, slots, lb=None, ub=None, tol=1e-7, cutoff=math.inf, max_iters=0, check_every=64,
-               warm_start=False, warm_omega_floor=0.0, bound_res=0.0, gap_tol=0.0, polish_after=0.0):
+               warm_start=False, warm_omega_floor=0.0, bound_res=0.0, gap_tol=0.0, polish_after=0.0,
+               warm_omega_cap=0.0):
         slots = np.asarray(slots).reshape(-1)
         self._cutoff = cutoff
         r = self.solve(slots, lb, ub, tol=tol, cutoff=math.inf)
