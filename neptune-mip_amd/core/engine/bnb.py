@@ -155,7 +155,7 @@ class BranchAndBound:
                  seed_leaves=None, integer_bound=None, improve=None, repair=None, node_bound_res=1e-2,
                  retry_res=math.inf, unit_flow_leaves=True, node_max_iters=None, bound_lp=None, bound_gap=1e-4,
                  trace=None, rebalance_every=8, primal=None, primal_every=0,
-                 leaf_routing_warm=False, root_check_every=64, objective_integral=False, warm_weight_ref=8.0,
+                 leaf_routing_warm=False, root_check_every=64, objective_integral=False, warm_weight_ref=0.0,
                  native=None):
         self.lp = lp
         self.two = bound_lp is not None
@@ -203,10 +203,11 @@ class BranchAndBound:
         # step-1 MinUtilization's node count): a node whose valid bound exceeds incumbent - 1 holds no better
         # point, so it is pruned (SCIP's objective-integrality pruning)
         self.objective_integral = bool(objective_integral)
-        # warm-started node LPs take their PDHG primal weight in [2, 4] x (warm_weight_ref x the model's cold-start
-        # weight omega0) instead of [2, 4] x their parent's final weight, which ratchets up along a lineage
-        # (nep_lp_set_reference_weight; 512x256 replay 7.5 -> 12.2 certified LP/s, independent of the root's
-        # chaotic final weight; DESIGN.md §4 "Warm-start primal weight"); 0: parent-relative
+        # warm_weight_ref > 0: warm-started node LPs take their PDHG primal weight in [2, 4] x (warm_weight_ref x
+        # the model's cold-start weight omega0) instead of [2, 4] x their parent's final weight, which ratchets up
+        # along a lineage (nep_lp_set_reference_weight; step 1 at 512x256: replay 7.5 -> 12.2 certified LP/s,
+        # independent of the root's chaotic final weight; DESIGN.md §4 "Warm-start primal weight").  0 (default):
+        # parent-relative — the step-2 models keep it (a 64x32 delete node LP stalls under the step-1 band)
         self.warm_weight_ref = float(warm_weight_ref or 0.0)
         # native tree search (csrc/nep_bnb.cpp, nep_bnb_*): the single-rank search without per-node Python
         # callbacks runs its whole loop in the engine library (None: whenever eligible; NEP_BNB_PYTHON=1 keeps

@@ -270,7 +270,9 @@ class NeptuneStepBase(Solver):
                   node_bound_res=self.node_bound_res, unit_flow_leaves=self.unit_flow_leaves,
                   node_max_iters=max(1, int(self.lp_max_iters * self.node_iters_fraction)),
                   bound_lp=bmodel, primal=self.primal_heuristic(layout, _row_map(model)),
-                  objective_integral=self.objective_integral())
+                  objective_integral=self.objective_integral(),
+                  # step 1: warm starts banded around 8 x the model's cold-start primal weight
+                  warm_weight_ref=8.0 if self.step_id() == _lp.STEP1 else 0.0)
         kw.update(overrides)
         return BranchAndBound(model, data.workload_matrix, data.function_memory_matrix, data.node_memory_matrix, **kw)
 
