@@ -124,6 +124,9 @@ def parse(argv=None):
     ap.add_argument("--bnb-sizes", default="256x128:20,512x256:60",
                     help="instances of the product B&B section (BASELINE configs 3 and 4), NxF[:seconds] "
                          "comma-separated (seconds: that instance's time limit, default --bnb-seconds)")
+    ap.add_argument("--in-order", action="store_true",
+                    help="replay: submit the recorded boxes strictly in their recorded order (default: a box waits "
+                         "while its parent's LP still iterates, as in the B&B, and later ready boxes go first)")
     ap.add_argument("--dump", default=None, help="write per-node-LP records of the replay (kind, depth, warm source, "
                     "status, iterations, final diagnostics of the uncertified) to this JSON file")
     ap.add_argument("--traffic", default=os.path.join(REPO, "profiles", "traffic.json"))
@@ -393,6 +396,11 @@ class ReplayStream:
         self.warm_parent = 0
         self.records = []       # (--dump) one record per completed node LP
         self.status_of = {}
+        # a node is submitted only once its parent's LP finished — as the B&B does (its children exist only
+        # then): an entry whose parent still iterates waits (at most 64 such), later ready entries go first
+        self.entry_of = {e["id"]: e for e in trace["lps"]}
+        self.deferred = []
+        self.in_order = bool(getattr(a, "in_order", False))
 
     def peek_entry(self):
         """(repetition, entry) this rank replays next: entries rank, rank + world, ... of the trace (repeated)."""
@@ -420,21 +428,50 @@ class ReplayStream:
             lb[idx] = ub[idx] = val
         return lb, ub
 
+    def _candidate(self):
+        """(where, rep, entry): the next entry to submit — the first deferred one, else the upcoming one, whose
+        parent's LP is not iterating (where = index into `deferred`, -1 = the upcoming entry); None when every
+        candidate waits for its parent and the deferral window is full."""
+        if self.in_order:
+            rep, e = self.peek_entry()
+            return -1, rep, e
+        running = {(n, v[0]) for (n, _), v in self.running.items()}
+
+        def ready(rep, e):
+            pe = self.entry_of.get(e["parent"])
+            pm = self._model(pe) if pe is not None else self._model(e)
+            return (pm, (rep, e["parent"])) not in running
+        for i, (rep, e) in enumerate(self.deferred):
+            if ready(rep, e):
+                return i, rep, e
+        while len(self.deferred) < 64:
+            rep, e = self.peek_entry()
+            if ready(rep, e):
+                return -1, rep, e
+            self.deferred.append(self.next_entry())
+        return None
+
     def _refill(self):
         import math
         from core.engine.lp import LP_INFEASIBLE
         a = self.a
         while self.counter < self.limit:
-            rep, e = self.peek_entry()
+            cand = self._candidate()
+            if cand is None:
+                break                            # every candidate waits for its parent's LP
+            where_, rep, e = cand
             name = self._model(e)
             if self.busy[name] >= a.batch:
-                break                            # in order: the next node waits for a slot of its model
+                break                            # the next node waits for a slot of its model
             m, root = self.models[name]
             if self.free[name]:
                 slot = self.free[name].pop(0)
             else:                                # every slot parked: evict the oldest parked state
                 slot, _ = self.parked[name].popitem(last=False)
-            self.next_entry()
+            if where_ < 0:
+                self.next_entry()
+            else:
+                del self.deferred[where_]
             key = (rep, e["id"])
             pkey = (name, (rep, e["parent"]))
             old = self.held.pop((name, slot), None)       # this slot's finished state is overwritten now
