@@ -5,13 +5,15 @@
 Workload (`value`).  The node LPs the product's own branch-and-bound submitted on this instance
 (step-1 NeptuneMinDelayAndUtilization, reference `core/solvers/neptune/neptune_step1.py:67-77`, rows
 `neptune/utils/constraints_step1.py`, objective `neptune/utils/objectives.py:30-52`), recorded by
-tools/record_bnb_trace.py into tests/golden/bnb_trace_512x256_s0.json.gz and REPLAYED in submission
-order: each recorded box (a branching node's fixings; a leaf's open c and n, every other c and n fixed to
+tools/record_bnb_trace.py into tests/golden/bnb_trace_512x256_s0.json.gz (s1: `--seed 1`) and REPLAYED in
+submission order, except that a box waits while its parent's LP still iterates (the B&B creates a node only once
+its parent finished; later ready boxes go first; `--in-order` disables this): each recorded box (a branching node's fixings; a leaf's open c and n, every other c and n fixed to
 0) is solved as an LP relaxation of the REFERENCE model — the LP SCIP solves at that node
 (core/solvers/solver.py:35-40).  `--batch` node LPs are in flight per GPU (nep_lp_submit /
 nep_lp_advance): a slot whose LP finishes takes the next box at once.  A node starts from its parent's
 final PDHG state when a slot still holds it (slots are refilled oldest-finished first; finished parents
-with open children are parked), else from the root's.  One *step* = `--batch` node LPs; the timed region
+with open children are parked, `--park` slots), else from the root's, with the PDHG primal weight banded around
+8 x the model's cold-start weight (`--omega-ref`, nep_lp_set_reference_weight).  One *step* = `--batch` node LPs; the timed region
 streams `--steps` x `--batch` of them through the slots and drains them (every node of the timed region
 finishes inside it).  A node counts only if the engine certifies it: repaired primal objective -
 Lagrangian bound <= tol*max(1,|bound|) and every row residual <= tol; nodes that stop at
