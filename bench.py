@@ -729,8 +729,7 @@ def main():
             t_fr = time.perf_counter()
             fr = bm.solve([root], tol=a.tol, max_iters=a.root_max_iters, check_every=a.root_check_every,
                         bound_res=1e-2, gap_tol=1e-4)
-            if a.omega_ref > 0:      # (as the product B&B sets it on both of its models)
-                bm.set_reference_weight(a.omega_ref * bm.info.primal_weight0)
+            # (the facility model keeps the parent-relative warm-start band, as in the product search)
             fac_root = {"status": int(fr["status"][0]), "obj": float(fr["obj"][0]), "iters": int(fr["iters"][0]),
                         "seconds": time.perf_counter() - t_fr}
             log(f"rank {rank}: facility-relaxation root: {fac_root}")
