@@ -306,13 +306,21 @@ typedef struct {
 #define NEP_BNB_DONE 0   /* the search ended (no open node, or a stop): stats / incumbent are final */
 #define NEP_BNB_ROOT 1   /* the root branching node finished: nep_bnb_event_data, then nep_bnb_add_leaf(where = 1) /
                             nep_bnb_set_incumbent for the caller's primal heuristic, then nep_bnb_run again */
+#define NEP_BNB_INCUMBENT 2   /* (nep_bnb_set_step2 with incumbent_events) a new LP incumbent: nep_bnb_incumbent_event,
+                                 then nep_bnb_add_leaf(where = 2) for each neighbour leaf, then nep_bnb_run again */
 
 void *nep_bnb_create(void *leaf_model, void *bound_model, const nep_bnb_params *params, const double *fn_mem,
                      const double *node_mem);
 void nep_bnb_destroy(void *tree);
 /* a leaf (a full c / n assignment, or any box): where = 0 a seed leaf queued when the root LP finishes;
- * where = 1 a leaf of the NEP_BNB_ROOT event's node, at the front of the leaf queue */
+ * where = 1 a leaf of the NEP_BNB_ROOT event's node, where = 2 a neighbour of the NEP_BNB_INCUMBENT event's
+ * leaf, both at the front of the leaf queue */
 int nep_bnb_add_leaf(void *tree, int32_t n, const int32_t *idx, const double *val, double bound, int32_t where);
+/* step 2 (before the first nep_bnb_run): the closed-form integer bound of NeptuneStep2Base.integer_bound
+ * (core/solvers/neptune/neptune_step.py; create != 0: create mode, node_cap: the most nodes an integral placement
+ * opens, +inf: none; old_alloc [F*N]) on every node / leaf, and (incumbent_events) NEP_BNB_INCUMBENT events */
+int nep_bnb_set_step2(void *tree, int32_t create, double node_cap, const double *old_alloc, int32_t incumbent_events);
+int nep_bnb_incumbent_event(void *tree, int32_t *n_fix, int32_t *idx, double *val, double *value);
 /* an incumbent found outside the tree (a checked heuristic point): its value becomes the cutoff */
 int nep_bnb_set_incumbent(void *tree, double value);
 int nep_bnb_event_data(void *tree, double *z_int, float *flow);

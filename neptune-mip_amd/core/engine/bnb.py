@@ -57,6 +57,8 @@ OPTIMAL, INFEASIBLE, LIMIT = "OPTIMAL", "INFEASIBLE", "LIMIT"
 _STATUS_NAME = {LP_OPTIMAL: "certified", LP_ITERATION_LIMIT: "limit", LP_INFEASIBLE: "infeasible",
                 LP_CUTOFF: "cutoff", LP_BOUND: "bound"}
 NODE, LEAF, RETRY, REFROOT = 0, 1, 2, 3
+# step-2 searches on the native tree (NEP_BNB_STEP2 overrides)
+STEP2_NATIVE_DEFAULT = "0"
 _KIND_NAME = {NODE: "node", LEAF: "leaf", RETRY: "retry", REFROOT: "refroot"}
 
 
@@ -156,7 +158,7 @@ class BranchAndBound:
                  retry_res=math.inf, unit_flow_leaves=True, node_max_iters=None, bound_lp=None, bound_gap=1e-4,
                  trace=None, rebalance_every=8, primal=None, primal_every=0,
                  leaf_routing_warm=False, root_check_every=64, objective_integral=False, warm_weight_ref=0.0,
-                 native=None):
+                 native=None, step2_native=None):
         self.lp = lp
         self.two = bound_lp is not None
         self.N, self.F = lp.N, lp.F
@@ -213,6 +215,9 @@ class BranchAndBound:
         # callbacks runs its whole loop in the engine library (None: whenever eligible; NEP_BNB_PYTHON=1 keeps
         # this module's loop, for A/B)
         self.native = native
+        # (create, node_cap, old allocation [F*N]): integer_bound is step 2's closed form, which the native tree
+        # evaluates itself (NeptuneStep2Base.native_bound); improve then runs on NEP_BNB_INCUMBENT events
+        self.step2_native = step2_native
         # (the leaf / reference model only — the model whose node LPs the replay measured; the facility relaxation
         # keeps the parent-relative band: 256x128 / 20 s gap 0.51 % with it, 0.82 % with the band on both)
         for m_ in (lp,):
@@ -741,12 +746,14 @@ class BranchAndBound:
     def _native_ok(self, comm):
         if self.native is False or os.environ.get("NEP_BNB_PYTHON", "0") not in ("", "0"):
             return False
-        eligible = (comm.world == 1 and self.trace is None and self.improve is None and self.integer_bound is None
+        s2 = self.step2_native is not None and os.environ.get("NEP_BNB_STEP2", STEP2_NATIVE_DEFAULT) not in ("", "0")
+        eligible = (comm.world == 1 and self.trace is None
+                    and (self.integer_bound is None or s2) and (self.improve is None or s2)
                     and not self.leaf_routing_warm and self.primal_every == 0 and hasattr(self.lp, "_h")
                     and (self.bound_lp is None or hasattr(self.bound_lp, "_h")))
         if self.native and not eligible:
-            raise ValueError("native tree search: single rank, no trace / improve / integer_bound / leaf routing warm "
-                             "starts / primal_every")
+            raise ValueError("native tree search: single rank, no trace / leaf routing warm starts / primal_every, "
+                             "integer_bound and improve only with step2_native")
         return eligible
 
     def _solve_native(self):
@@ -775,6 +782,11 @@ class BranchAndBound:
             raise RuntimeError("nep_bnb_create failed")
         bm = self.bound_lp if self.two else lp
         try:
+            if self.step2_native is not None:
+                create, cap, old = self.step2_native
+                old = np.ascontiguousarray(old, np.float64).reshape(-1)
+                _check(lib, lib.nep_bnb_set_step2(tree, 1 if create else 0, float(cap), _ptr(old),
+                                                  1 if self.improve is not None else 0), "nep_bnb_set_step2")
             for idx, val in self.seed_leaves:
                 idx = np.ascontiguousarray(idx, np.int32)
                 val = np.ascontiguousarray(val, np.float64)
@@ -784,6 +796,22 @@ class BranchAndBound:
                 _check(lib, lib.nep_bnb_run(tree, ctypes.byref(ev)), "nep_bnb_run")
                 if ev.value == 0:
                     break
+                if ev.value == 2:
+                    # NEP_BNB_INCUMBENT: the neighbour leaves of a new LP incumbent (step 2's node relocation)
+                    n_fix = ctypes.c_int32()
+                    idx = np.zeros(self._nb + 1, np.int32)
+                    val = np.zeros(self._nb + 1)
+                    value = ctypes.c_double()
+                    _check(lib, lib.nep_bnb_incumbent_event(tree, ctypes.byref(n_fix), _ptr(idx), _ptr(val),
+                                                            ctypes.byref(value)), "nep_bnb_incumbent_event")
+                    k = n_fix.value
+                    self.log(f"incumbent {value.value:.10g}")
+                    for nidx, nval in self.improve(idx[:k].astype(np.int64), val[:k].copy(), value.value):
+                        nidx = np.ascontiguousarray(nidx, np.int32)
+                        nval = np.ascontiguousarray(nval, np.float64)
+                        _check(lib, lib.nep_bnb_add_leaf(tree, len(nidx), _ptr(nidx), _ptr(nval), -inf, 2),
+                               "nep_bnb_add_leaf")
+                    continue
                 # NEP_BNB_ROOT: the primal heuristic on the root branching node's LP
                 t = time.time()
                 z = np.zeros(bm.n_int)

@@ -103,6 +103,10 @@ class NeptuneStepBase(Solver):
         fixings (+inf: none exists), or None."""
         return None
 
+    def native_bound(self):
+        """integer_bound's parameters for the native tree search (nep_bnb_set_step2), or None."""
+        return None
+
     def objective_integral(self):
         """Every integral point of the step model has an integral objective: step-1 MinUtilization (sum n,
         objectives.py:24-27) and every step 2 (minimize_disruption, objectives.py:55-63: integer weights on
@@ -272,7 +276,8 @@ class NeptuneStepBase(Solver):
                   bound_lp=bmodel, primal=self.primal_heuristic(layout, _row_map(model)),
                   objective_integral=self.objective_integral(),
                   # step 1: warm starts banded around 8 x the model's cold-start primal weight
-                  warm_weight_ref=8.0 if self.step_id() == _lp.STEP1 else 0.0)
+                  warm_weight_ref=8.0 if self.step_id() == _lp.STEP1 else 0.0,
+                  step2_native=self.native_bound())
         kw.update(overrides)
         return BranchAndBound(model, data.workload_matrix, data.function_memory_matrix, data.node_memory_matrix, **kw)
 
@@ -500,6 +505,12 @@ class NeptuneStep2Base(NeptuneStepBase):
         if self.VARIANT == "MinUtilization":
             return ms
         return ms * len(d.nodes) / self.alpha if self.alpha > 0 else math.inf
+
+    def native_bound(self):
+        """(create, node cap, old allocation): integer_bound below, evaluated by the native tree
+        (csrc/nep_bnb.cpp NepBnb::ibound, the same closed form)."""
+        return (self.mode == "create", float(self.node_cap()),
+                np.asarray(self.data.old_allocations_matrix, np.float64).reshape(-1))
 
     def integer_bound(self, layout=None):
         """The step-2 objective over integral placements, bounded from the node's c (and n) fixings.

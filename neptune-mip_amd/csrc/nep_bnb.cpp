@@ -117,12 +117,25 @@ struct NepBnb {
   NodeP ev_node;
   Parent ev_parent;
   double ev_bound = -INF;
+  // step 2 (nep_bnb_set_step2): the closed-form integer bound of NeptuneStep2Base.integer_bound and the
+  // incumbent event for its node-relocation neighbours (NeptuneStep2Base.improve, run by the caller)
+  bool s2 = false, s2_create = false, inc_events = false;
+  double s2_cap = INF;
+  std::vector<char> s2_old;   // [F*N] old allocation > 0.5
+  struct IncEvent {
+    NodeP node;
+    Parent at;
+    double value;
+  };
+  std::deque<IncEvent> inc_queue;
+  IncEvent cur_inc;
   // scratch
   std::vector<int32_t> sl, done_slots, sts;
   std::vector<double> obj, pobj, lbv, ubv;
   std::vector<int64_t> its;
 
   int nb() const { return (p.c1 - p.c0) + (p.n0 >= 0 ? p.n1 - p.n0 : 0); }
+  double ibound(const std::vector<int32_t> &idx, const std::vector<double> &val) const;
   double gap_abs(double incv) const {
     if (!std::isfinite(incv)) return 0.0;
     double g = p.gap * std::max(1.0, std::fabs(incv));
@@ -311,6 +324,98 @@ int NepBnb::branch_var(const Node &node, const float *flow, const double *z) con
   return best;
 }
 
+// NeptuneStep2Base.integer_bound (core/solvers/neptune/neptune_step.py): the step-2 objective over integral
+// placements bounded from a node's c (and n) fixings — additions A, removals R, the K-node cap; +inf when the
+// fixings admit no integral completion; -inf without step 2
+double NepBnb::ibound(const std::vector<int32_t> &idx, const std::vector<double> &val) const {
+  if (!s2) return -INF;
+  const int F = p.F, N = p.N, FN = F * N;
+  const double w = (double)FN;
+  std::vector<double> fx(FN, -1.0), nf(N, -1.0);
+  for (size_t q = 0; q < idx.size(); ++q) {
+    if (idx[q] >= p.c0 && idx[q] < p.c0 + FN) fx[idx[q] - p.c0] = val[q];
+    else if (p.n0 >= 0 && idx[q] >= p.n0 && idx[q] < p.n1) nf[idx[q] - p.n0] = val[q];
+  }
+  std::vector<char> one(FN), zero(FN);
+  double O = 0.0, add_fixed = 0.0, rem_fixed = 0.0;
+  for (int k = 0; k < FN; ++k) {
+    one[k] = fx[k] > 0.5;
+    zero[k] = fx[k] >= 0 && fx[k] < 0.5;
+    O += s2_old[k] ? 1.0 : 0.0;
+    if (one[k] && !s2_old[k]) add_fixed += 1.0;
+    if (zero[k] && s2_old[k]) rem_fixed += 1.0;
+  }
+  double uncovered = 0.0;
+  std::vector<char> freef(F, 1);
+  std::vector<double> ones_f(F, 0.0);
+  for (int f = 0; f < F; ++f) {
+    bool cov = false;
+    for (int j = 0; j < N; ++j) {
+      const int k = f * N + j;
+      cov |= one[k] || (s2_old[k] && !zero[k]);
+      if (one[k]) { freef[f] = 0; ones_f[f] += 1.0; }
+    }
+    if (!cov) uncovered += 1.0;
+  }
+  double A = add_fixed + uncovered, R_lb = rem_fixed;
+  if (std::isfinite(s2_cap)) {
+    const int K = (int)std::floor(s2_cap + 1e-9);
+    std::vector<char> opened(N, 0), closed(N, 0);
+    int n_open = 0;
+    for (int j = 0; j < N; ++j) {
+      bool any = false;
+      for (int f = 0; f < F; ++f) any |= one[f * N + j] != 0;
+      opened[j] = nf[j] > 0.5 || any;
+      closed[j] = nf[j] >= 0 && nf[j] < 0.5;
+      if (opened[j] && closed[j]) return INF;
+      n_open += opened[j];
+    }
+    if (n_open > K) return INF;
+    auto top_sum = [&](const std::vector<double> &v) {   // sum over opened + the K - n_open largest free others
+      double s = 0.0;
+      std::vector<double> rest;
+      for (int j = 0; j < N; ++j) {
+        if (opened[j]) s += v[j];
+        else if (!closed[j]) rest.push_back(v[j]);
+      }
+      std::sort(rest.begin(), rest.end(), std::greater<double>());
+      const int take = std::max(0, K - n_open);
+      for (int q = 0; q < take && q < (int)rest.size(); ++q) s += rest[q];
+      return s;
+    };
+    std::vector<double> keep(N, 0.0), cov(N, 0.0);
+    double nfreef = 0.0;
+    for (int f = 0; f < F; ++f) nfreef += freef[f];
+    for (int j = 0; j < N; ++j) {
+      if (closed[j]) continue;
+      for (int f = 0; f < F; ++f) {
+        const int k = f * N + j;
+        if (s2_old[k] && !zero[k]) {
+          keep[j] += 1.0;
+          if (freef[f]) cov[j] += 1.0;
+        }
+      }
+    }
+    R_lb = std::max(R_lb, O - top_sum(keep));
+    A = std::max(A, add_fixed + std::max(0.0, nfreef - top_sum(cov)));
+  }
+  if (s2_create) {
+    double nzero = 0.0;
+    for (int k = 0; k < FN; ++k) nzero += zero[k];
+    if ((double)FN - nzero < O) return INF;
+    return A + (2 * w - 1) * R_lb;
+  }
+  double need = 0.0, nfree = 0.0, kept = 0.0;
+  for (int f = 0; f < F; ++f) {
+    need += std::max(ones_f[f], 1.0);
+    if (ones_f[f] == 0.0) nfree += 1.0;
+  }
+  if (need > O + 1e-9) return INF;
+  for (int k = 0; k < FN; ++k) kept += (one[k] && s2_old[k]) ? 1.0 : 0.0;
+  kept += std::max(0.0, nfree - (A - add_fixed));
+  return (2 * w + 1) * A - (O - kept);
+}
+
 void NepBnb::round_all(const Node &node, const float *flow, const double *z, double bound, const Parent &me) {
   const int F = p.F, N = p.N, FN = F * N;
   std::vector<double> cfix(FN, -1.0), nfix;
@@ -343,7 +448,7 @@ void NepBnb::round_all(const Node &node, const float *flow, const double *z, dou
       leaf->val.insert(leaf->val.end(), nout.begin() + (size_t)q * N, nout.begin() + (size_t)(q + 1) * N);
     }
     if (!seen.insert(key_of(leaf->val)).second) continue;
-    leaf->bound = bound;   // (no model-specific integer bound on this path)
+    leaf->bound = std::max(bound, ibound(leaf->idx, leaf->val));
     if (!pruned(leaf->bound)) pending.push_back(leaf);
   }
 }
@@ -377,6 +482,8 @@ int NepBnb::finish_one(Engine &eng, int slot, const NodeP &node, int status, dou
     eng.root_ready = true;
     const Parent me0{&eng, slot, eng.gen[slot]};
     for (auto &s : seeds) {
+      s->bound = ibound(s->idx, s->val);
+      if (!(s->bound < INF)) continue;
       if (!seen.insert(key_of(s->val)).second) continue;
       s->parent = me0;
       s->depth = 1;
@@ -412,6 +519,7 @@ int NepBnb::finish_one(Engine &eng, int slot, const NodeP &node, int status, dou
         }
         st.lp_incumbents += 1;
         set_cutoffs();
+        if (inc_events) inc_queue.push_back(IncEvent{node, Parent{&eng, slot, eng.gen[slot]}, po});
       }
     } else if (node->kind == LEAF) {
       double pres = 0.0;
@@ -462,7 +570,7 @@ int NepBnb::finish_one(Engine &eng, int slot, const NodeP &node, int status, dou
       ch->idx.push_back(var);
       ch->val = node->val;
       ch->val.push_back(v);
-      ch->bound = bound;
+      ch->bound = std::max(bound, ibound(ch->idx, ch->val));
       if (pruned(ch->bound)) continue;
       ch->kind = (int)ch->idx.size() >= nb() ? LEAF : NODE;
       ch->parent = me;
@@ -627,12 +735,54 @@ int nep_bnb_add_leaf(void *tree, int32_t n, const int32_t *idx, const double *va
     t->seeds.push_back(leaf);
     return NEP_OK;
   }
+  if (where == 2) {   // a neighbour of the NEP_BNB_INCUMBENT event's leaf: its own bound, at the front
+    if (!t->seen.insert(NepBnb::key_of(leaf->val)).second) return NEP_OK;
+    leaf->bound = std::max(bound, t->ibound(leaf->idx, leaf->val));
+    leaf->parent = t->cur_inc.at;
+    leaf->depth = t->cur_inc.node ? t->cur_inc.node->depth : 1;
+    t->pending.push_front(leaf);
+    return NEP_OK;
+  }
   // where = 1: a leaf of the root event's node (the primal heuristic), at the front of the leaf queue
   if (!t->seen.insert(NepBnb::key_of(leaf->val)).second) return NEP_OK;
-  leaf->bound = std::max(t->ev_bound, bound);
+  leaf->bound = std::max(std::max(t->ev_bound, bound), t->ibound(leaf->idx, leaf->val));
   leaf->parent = t->ev_parent;
   leaf->depth = t->ev_node ? t->ev_node->depth + 1 : 1;
   if (!t->pruned(leaf->bound)) t->pending.push_front(leaf);
+  return NEP_OK;
+}
+
+int nep_bnb_set_step2(void *tree, int32_t create, double node_cap, const double *old_alloc, int32_t incumbent_events) {
+  auto *t = static_cast<NepBnb *>(tree);
+  if (!t || !old_alloc || t->started) return NEP_ERR_ARG;
+  const size_t FN = (size_t)t->p.F * t->p.N;
+  t->s2 = true;
+  t->s2_create = create != 0;
+  t->s2_cap = node_cap;
+  t->s2_old.resize(FN);
+  for (size_t k = 0; k < FN; ++k) t->s2_old[k] = old_alloc[k] > 0.5;
+  t->inc_events = incumbent_events != 0;
+  // the root's bound is the integer bound of the empty box (+inf: no integral point at all)
+  const double rb = t->ibound({}, {});
+  while (!t->heap.empty()) t->heap.pop();
+  if (rb < INF) {
+    auto root = std::make_shared<Node>();
+    root->bound = rb;
+    root->kind = NODE;
+    root->depth = 0;
+    t->push_heap(root);
+  }
+  return NEP_OK;
+}
+
+int nep_bnb_incumbent_event(void *tree, int32_t *n_fix, int32_t *idx, double *val, double *value) {
+  auto *t = static_cast<NepBnb *>(tree);
+  if (!t || !t->cur_inc.node) return NEP_ERR_STATE;
+  const Node &nd = *t->cur_inc.node;
+  if (n_fix) *n_fix = (int32_t)nd.idx.size();
+  if (idx) std::memcpy(idx, nd.idx.data(), nd.idx.size() * sizeof(int32_t));
+  if (val) std::memcpy(val, nd.val.data(), nd.val.size() * sizeof(double));
+  if (value) *value = t->cur_inc.value;
   return NEP_OK;
 }
 
@@ -673,6 +823,12 @@ int nep_bnb_run(void *tree, int32_t *event) {
   NepBnb &T = *t;
   Engine &L = T.L, &B = T.B;
   for (;;) {
+    if (!T.inc_queue.empty()) {   // the caller's neighbours of a new LP incumbent (step 2's node relocation)
+      T.cur_inc = T.inc_queue.front();
+      T.inc_queue.pop_front();
+      *event = NEP_BNB_INCUMBENT;
+      return NEP_OK;
+    }
     if (T.root_event_pending) {   // the caller's primal heuristic on the root node
       T.root_event_pending = false;
       T.root_event_done = true;

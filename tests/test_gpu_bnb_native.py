@@ -80,3 +80,38 @@ def test_native_search_host_share(n, f, seconds):
     assert out[True][0] < 0.35
     if n <= 64:
         assert out[True][5] < out[False][5]
+
+
+FLOW_CASES = ["payload", "testpy", "syn_4x3_s0_r0.5_NeptuneMinDelayAndUtilization", "syn_6x4_s1_r0.3_NeptuneMinDelay",
+              "syn_8x4_s2_r0.1_NeptuneMinDelayAndUtilization", "sim3_NeptuneMinDelayAndUtilization"]
+
+
+@pytest.mark.parametrize("name", FLOW_CASES)
+def test_native_step2_matches_python(name, monkeypatch):
+    """Step 2 on the native tree (the integer bound in C++, node relocation on NEP_BNB_INCUMBENT events): the whole
+    NEPTUNE flow gives the same step-1 / step-2 scores as with the Python loop (NEP_BNB_PYTHON=1), both equal to the
+    reference's recorded ones."""
+    import core.solvers as S
+    from core.utils import data_to_solver_input
+    if name not in G:
+        pytest.skip("no golden")
+    p = payload(name)
+    scores, native = {}, {}
+    monkeypatch.setenv("NEP_BNB_STEP2", "1")
+    for py in ("1", "0"):
+        monkeypatch.setenv("NEP_BNB_PYTHON", py)
+        data = data_to_solver_input(p, workload_coeff=p.get("workload_coeff", 1), with_db=False)
+        solver = S.SOLVERS[p["solver"]["type"]](**p["solver"].get("args", {}))
+        if not hasattr(solver, "step2_delete"):
+            pytest.skip("not a NEPTUNE flow")
+        solver.load_data(data)
+        solver.solve()
+        scores[py] = solver.score()
+        steps = [s for s in (solver.step2_delete, solver.step2_create) if getattr(s, "result", None) is not None]
+        native[py] = [bool(getattr(s.result, "native", False)) for s in steps]
+    print(name, scores, native)
+    ref = G[name]["response"]["score"]
+    for py in ("1", "0"):
+        assert abs(scores[py]["step1"] - ref["step1"]) <= 1e-6 * max(1.0, abs(ref["step1"]))
+        assert abs(scores[py]["step2"] - ref["step2"]) <= 1e-6 * max(1.0, abs(ref["step2"]))
+    assert not any(native["1"]) and native["0"] and all(native["0"])
