@@ -321,6 +321,9 @@ int nep_bnb_add_leaf(void *tree, int32_t n, const int32_t *idx, const double *va
  * opens, +inf: none; old_alloc [F*N]) on every node / leaf, and (incumbent_events) NEP_BNB_INCUMBENT events */
 int nep_bnb_set_step2(void *tree, int32_t create, double node_cap, const double *old_alloc, int32_t incumbent_events);
 int nep_bnb_incumbent_event(void *tree, int32_t *n_fix, int32_t *idx, double *val, double *value);
+/* host only: that integer bound of one box (params: the layout fields), for the CPU suite */
+int nep_bnb_debug_ibound(const nep_bnb_params *params, int32_t create, double node_cap, const double *old_alloc,
+                         int32_t n, const int32_t *idx, const double *val, double *out);
 /* an incumbent found outside the tree (a checked heuristic point): its value becomes the cutoff */
 int nep_bnb_set_incumbent(void *tree, double value);
 int nep_bnb_event_data(void *tree, double *z_int, float *flow);

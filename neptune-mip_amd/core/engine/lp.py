@@ -95,7 +95,7 @@ EXPORTS = ("nep_model_create", "nep_model_destroy", "nep_model_get_info", "nep_l
            "nep_lp_get_solutions", "nep_round_leaves", "nep_lp_set_reference_weight",
            "nep_bnb_create", "nep_bnb_destroy", "nep_bnb_add_leaf", "nep_bnb_set_incumbent", "nep_bnb_event_data",
            "nep_bnb_run", "nep_bnb_get_stats", "nep_bnb_get_lp_iters", "nep_bnb_incumbent", "nep_bnb_set_step2",
-           "nep_bnb_incumbent_event")
+           "nep_bnb_incumbent_event", "nep_bnb_debug_ibound")
 SCORE_FIELDS = ("network_delay", "nodes_used", "node_cost", "bad_c_x", "bad_memory", "bad_handle", "bad_cpu",
                 "bad_n_c", "bad_budget", "handle_maxdev", "cpu_maxexcess")
 
@@ -162,6 +162,7 @@ def load_library(path=None):
     lib.nep_bnb_incumbent.argtypes = [vp, _dp, pi32, pi32, _dp]
     lib.nep_bnb_set_step2.argtypes = [vp, i32, ctypes.c_double, _dp, i32]
     lib.nep_bnb_incumbent_event.argtypes = [vp, pi32, pi32, _dp, _dp]
+    lib.nep_bnb_debug_ibound.argtypes = [ctypes.POINTER(BnbParams), i32, ctypes.c_double, _dp, i32, pi32, _dp, _dp]
     lib.nep_lp_get_flows.argtypes = [vp, i32, pi32, ctypes.POINTER(ctypes.c_float)]
     lib.nep_lp_get_flows_split.argtypes = [vp, i32, pi32, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float)]
     lib.nep_lp_routing_entries.argtypes = [vp, i32, ctypes.c_double, i32, i64, pi64, pi32, pi32, _dp]

@@ -327,8 +327,16 @@ int NepBnb::branch_var(const Node &node, const float *flow, const double *z) con
 // NeptuneStep2Base.integer_bound (core/solvers/neptune/neptune_step.py): the step-2 objective over integral
 // placements bounded from a node's c (and n) fixings — additions A, removals R, the K-node cap; +inf when the
 // fixings admit no integral completion; -inf without step 2
+static double step2_ibound(const nep_bnb_params &p, bool s2_create, double s2_cap, const std::vector<char> &s2_old,
+                           const std::vector<int32_t> &idx, const std::vector<double> &val);
+
 double NepBnb::ibound(const std::vector<int32_t> &idx, const std::vector<double> &val) const {
   if (!s2) return -INF;
+  return step2_ibound(p, s2_create, s2_cap, s2_old, idx, val);
+}
+
+static double step2_ibound(const nep_bnb_params &p, bool s2_create, double s2_cap, const std::vector<char> &s2_old,
+                           const std::vector<int32_t> &idx, const std::vector<double> &val) {
   const int F = p.F, N = p.N, FN = F * N;
   const double w = (double)FN;
   std::vector<double> fx(FN, -1.0), nf(N, -1.0);
@@ -772,6 +780,17 @@ int nep_bnb_set_step2(void *tree, int32_t create, double node_cap, const double 
     root->depth = 0;
     t->push_heap(root);
   }
+  return NEP_OK;
+}
+
+int nep_bnb_debug_ibound(const nep_bnb_params *params, int32_t create, double node_cap, const double *old_alloc,
+                         int32_t n, const int32_t *idx, const double *val, double *out) {
+  if (!params || !old_alloc || !out || n < 0 || (n > 0 && (!idx || !val))) return NEP_ERR_ARG;
+  const size_t FN = (size_t)params->F * params->N;
+  std::vector<char> old(FN);
+  for (size_t k = 0; k < FN; ++k) old[k] = old_alloc[k] > 0.5;
+  *out = step2_ibound(*params, create != 0, node_cap, old, std::vector<int32_t>(idx, idx + n),
+                      std::vector<double>(val, val + n));
   return NEP_OK;
 }
 

@@ -166,3 +166,38 @@ def test_step2_integer_bound_with_node_cap(mode, seed):
         b = bound(np.concatenate([ci, n0 + ni]).astype(np.int64), np.concatenate([cv, nv]))
         if comp:
             assert b <= min(comp) + 1e-9, (ci, cv, ni, nv, b, min(comp))
+
+
+@pytest.mark.parametrize("mode", ["delete", "create"])
+@pytest.mark.parametrize("cap", [math.inf, 2.0, 3.0])
+@pytest.mark.parametrize("seed", range(4))
+def test_native_integer_bound_equals_python(mode, cap, seed):
+    """The native tree's copy of integer_bound (csrc/nep_bnb.cpp step2_ibound, nep_bnb_debug_ibound) equals
+    NeptuneStep2Base.integer_bound on random c / n boxes, with and without the node cap."""
+    import ctypes
+    from core.engine.lp import BnbParams, load_library
+    from core.solvers.neptune.neptune_step import NeptuneStep2Base
+    rng = np.random.default_rng(300 + seed)
+    F, N = 4, 5
+    FN = F * N
+    old = (rng.random((F, N)) < 0.35).astype(float)
+    s = NeptuneStep2Base.__new__(NeptuneStep2Base)
+    s.mode = mode
+    s.data = types.SimpleNamespace(functions=list(range(F)), nodes=list(range(N)), old_allocations_matrix=old)
+    s.node_cap = lambda: cap
+    n0 = FN + 3
+    layout = {"c": (0, FN), "n": (n0, n0 + N)}
+    bound = s.integer_bound(layout)
+    lib = load_library()
+    p = BnbParams(c0=0, c1=FN, n0=n0, n1=n0 + N, n_int=n0 + N, F=F, N=N)
+    oldv = np.ascontiguousarray(old.ravel())
+    out = ctypes.c_double()
+    for trial in range(200):
+        k = int(rng.integers(0, FN + N))
+        pool = np.concatenate([np.arange(FN), np.arange(n0, n0 + N)])
+        idx = np.sort(rng.choice(pool, size=k, replace=False)).astype(np.int32)
+        val = rng.integers(0, 2, size=k).astype(np.float64)
+        ref = bound(idx.astype(np.int64), val)
+        assert lib.nep_bnb_debug_ibound(ctypes.byref(p), 1 if mode == "create" else 0, float(cap), oldv.ctypes.data,
+                                        k, idx.ctypes.data, val.ctypes.data, ctypes.byref(out)) == 0
+        assert out.value == ref or abs(out.value - ref) <= 1e-9 * max(1.0, abs(ref)), (idx, val, out.value, ref)
