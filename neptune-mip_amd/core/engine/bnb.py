@@ -58,7 +58,7 @@ _STATUS_NAME = {LP_OPTIMAL: "certified", LP_ITERATION_LIMIT: "limit", LP_INFEASI
                 LP_CUTOFF: "cutoff", LP_BOUND: "bound"}
 NODE, LEAF, RETRY, REFROOT = 0, 1, 2, 3
 # step-2 searches on the native tree (NEP_BNB_STEP2 overrides)
-STEP2_NATIVE_DEFAULT = "0"
+STEP2_NATIVE_DEFAULT = "1"
 _KIND_NAME = {NODE: "node", LEAF: "leaf", RETRY: "retry", REFROOT: "refroot"}
 
 
