@@ -46,7 +46,7 @@ for r in "$@"; do
       python3 tools/traffic.py summarize /tmp/pmc_fetch /tmp/pmc_write > "$O/traffic.json"; cat "$O/traffic.json" ;;
     sq)
       export ROC_AQL_QUEUE_SIZE=65536
-      step pmc_sq 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU -d /tmp/pmc_sq -o run -- python3 tools/traffic.py run
+      step pmc_sq 400 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU -d /tmp/pmc_sq -o run -- python3 tools/traffic.py run
       python3 tools/traffic.py sq /tmp/pmc_sq > "$O/sq.json"; cat "$O/sq.json" ;;
     probe:*) a=${r#probe:}; step probe 600 python -u tools/step2_probe.py ${a//,/ } ;;
     py:*) a=${r#py:}; step "py_${a%%.py*}" 600 python -u tools/${a//,/ } ;;
