@@ -13,22 +13,25 @@ its parent finished; later ready boxes go first; `--in-order` disables this): ea
 nep_lp_advance): a slot whose LP finishes takes the next box at once.  A node starts from its parent's
 final PDHG state when a slot still holds it (slots are refilled oldest-finished first; finished parents
 with open children are parked, `--park` slots), else from the root's, with the PDHG primal weight banded around
-8 x the model's cold-start weight (`--omega-ref`, nep_lp_set_reference_weight).  One *step* = `--batch` node LPs; the timed region
-streams `--steps` x `--batch` of them through the slots and drains them (every node of the timed region
-finishes inside it).  A node counts only if the engine certifies it: repaired primal objective -
-Lagrangian bound <= tol*max(1,|bound|) and every row residual <= tol; nodes that stop at
-`--max-iters` keep a valid bound and are reported, not counted.  The root LP is solved before the timed
-region (its seconds are `lp.root_seconds`); the instance lives on the device before the timer starts;
-node bounds are uploaded inside it, as the B&B host does per node.  Secondary figures in the same JSON:
-`native_replay` (the same boxes on the model the product ran them on), `children_stream` (root children
-with `--fix` random c-fixings, the round-1..3 workload) and `bnb` (the product search itself).
+8 x the model's cold-start weight (`--omega-ref`, nep_lp_set_reference_weight).  The timed region
+streams the WHOLE recorded trace once (1026 node LPs at 512x256, seed 0) and drains it, whatever --steps says:
+one *step* is 1/K of the trace (ms_per_step = wall / K), so `value` does not depend on --steps / --warmup (the
+warmup streams the first W x --batch boxes on a stream of its own, untimed).  A node counts only if the engine
+certifies it: repaired primal objective - Lagrangian bound <= tol*max(1,|bound|) and every row residual <= tol
+(DESIGN.md §4); nodes that stop at `--max-iters` keep a valid bound and are reported, not counted.  The root LP
+is solved before the timed region (its seconds are `lp.root_seconds`); the instance lives on the device before
+the timer starts; node bounds are uploaded inside it, as the B&B host does per node.  Secondary figures in the
+same JSON: `product_node_lp_per_s` (the product search's own node-LP rates), `native_replay` (the trace's first
+boxes on the models the product ran them on), `children_stream` (root children with `--fix` random c-fixings,
+the round-1..3 workload), `bnb` (the product search itself) and `alibaba_flows` (the reference's three Alibaba
+requests end to end beside its published processing_time).
 
 Multi-GPU.  `--gpus N` > 1 without a launcher environment starts N rank processes itself
 (torch.distributed.run, one rank per GPU, 127.0.0.1 rendezvous) before anything touches the GPU; under a
-launcher the world it reports must equal --gpus.  Every rank holds the same instance and takes replay
-entries rank, rank + world, ... (subtree sharding); the only exchange is the B&B bound
-all-reduce(MIN) of 8 bytes per timed stream.  value = certified LPs of all ranks / max-over-ranks wall
-time ("scaling": "weak").
+launcher the world it reports must equal --gpus.  Rank r replays the recorded B&B of instance seed --seed + r
+(one placement request per GPU: weak scaling; `rank_seed`); the only exchange is the B&B bound all-reduce(MIN)
+of 8 bytes per timed stream.  value = certified LPs of all ranks / max-over-ranks wall time.  The sharded search
+of ONE instance (subtrees per rank, one packed all-reduce per loop over RCCL) is the `bnb` section.
 
 Roofline.  The dominant kernel is `x_pass` (csrc/nep_kernels.hip).  Its algorithmic bytes per LP
 iteration are SURVEY.md §8(d)'s B_iter = 4 (2P + 2FN + 2N + 2m) (x, c, n and the duals, each read and
@@ -131,6 +134,10 @@ def parse(argv=None):
                          "while its parent's LP still iterates, as in the B&B, and later ready boxes go first)")
     ap.add_argument("--dump", default=None, help="write per-node-LP records of the replay (kind, depth, warm source, "
                     "status, iterations, final diagnostics of the uncertified) to this JSON file")
+    ap.add_argument("--alibaba-seconds", type=float, default=120.0,
+                    help="alibaba_flows section: the reference's three Alibaba 100x25 requests through core.request "
+                         "(main.py's route body), each B&B step limited to this many seconds (a safety bound: they end "
+                         "OPTIMAL well within it); 0 = skip")
     ap.add_argument("--traffic", default=os.path.join(REPO, "profiles", "traffic.json"))
     return ap.parse_args(argv)
 
@@ -303,6 +310,50 @@ def cpu_baseline(N, F, seed, fix, budget, workers):
             "measured": [{"nodes": a, "functions": b, "seconds": t, "status": s} for a, b, t, s in pts]}
 
 
+# the reference's published end-to-end figures for its Alibaba 100x25 trace case (SCIP via OR-Tools 9.6):
+# testing/alibaba/alibaba_test/output_<solver>_case0.json "score" and "processing_time" (:7787 / :7800)
+ALIBABA_PUBLISHED = {"NeptuneMinDelay": ({"step1": 0.0, "step2": 23.0}, 436.445),
+                     "NeptuneMinDelayAndUtilization": ({"step1": 0.005, "step2": 65010.0}, 1258.109),
+                     "NeptuneMinUtilization": ({"step1": 1.0, "step2": 65010.0}, 1224.564)}
+
+
+def alibaba_flows(a):
+    """The reference's three Alibaba 100x25 requests (tests/golden/inputs/alibaba_<solver>.json, the payloads of
+    testing/alibaba/alibaba_test) through `core.request.solve_request` — the body of main.py's route
+    (main.py:31-62): load_data + solve timed as the reference's `processing_time`, step 1 then step 2 (delete,
+    then create when delete is not OPTIMAL, neptune.py:18-30) on the GPU engine.  Reported beside the reference's
+    recorded score and processing_time; each step's status says whether its B&B proved optimality."""
+    from core.request import solve_request
+    out = []
+    for stype, (ref_score, ref_t) in ALIBABA_PUBLISHED.items():
+        with open(os.path.join(REPO, "tests", "golden", "inputs", f"alibaba_{stype}.json")) as fh:
+            p = json.load(fh)
+        p = json.loads(json.dumps(p))
+        p.setdefault("solver", {}).setdefault("args", {})["time_limit"] = a.alibaba_seconds
+        p["with_db"] = False
+        keep = []
+        t0 = time.perf_counter()
+        body = solve_request(p, solver_out=keep)
+        wall = time.perf_counter() - t0
+        s_ = keep[0]
+        steps = {}
+        for k in ("step1", "step2_delete", "step2_create"):
+            r = getattr(getattr(s_, k, None), "result", None)
+            if r is not None:
+                steps[k] = {"status": r.status, "objective": r.objective, "bound": r.bound, "nodes": r.nodes,
+                            "lps": r.lps, "seconds": r.seconds}
+        score = {k: float(v) for k, v in body["score"].items()}
+        out.append({"solver": stype, "processing_time_s": body["processing_time"], "wall_s": wall,
+                    "score": score, "steps": steps,
+                    "all_steps_optimal": all(v["status"] == "OPTIMAL" for v in steps.values() if v),
+                    "reference_score": ref_score, "reference_processing_time_s": ref_t,
+                    "speedup_vs_reference": ref_t / max(1e-9, body["processing_time"]),
+                    "score_matches_reference": all(abs(score[k] - v) <= 1e-6 * max(1.0, abs(v))
+                                                   for k, v in ref_score.items())})
+        log(f"alibaba {stype}: {body['processing_time']:.2f} s (reference {ref_t:.1f} s), score {score}")
+    return out
+
+
 def bnb_section(a, rank, world, dev, N, F, seconds):
     """The product's own branch-and-bound (core/engine/bnb.py, the search SCIP runs inside
     pywraplp Solve(), solver.py:35-40) on BASELINE config 3's / 4's instance (256x128, 512x256, step-1
@@ -377,7 +428,7 @@ class ReplayStream:
         self.lps = [e for e in trace["lps"] if e["parent"] is not None]
         self.parent_of = {e["id"]: e["parent"] for e in trace["lps"]}
         self.ancestors = getattr(a, "warm_ancestors", False)
-        self.pos, self.stride = rank, world
+        self.pos = 0
         self.counter = 0
         self.done = []          # (status, obj, primal_obj, iters) per completed node
         self.kinds = []         # (model, kind) per completed node
@@ -392,8 +443,7 @@ class ReplayStream:
         self.free = {name: list(range(a.batch + park)) for name in models}
         self.parked = {name: OrderedDict() for name in models}   # slot -> node key, oldest first
         self.busy = {name: 0 for name in models}
-        mine = [self.lps[i] for i in range(rank, len(self.lps), world)]
-        self.kids = Counter(e["parent"] for e in mine)
+        self.kids = Counter(e["parent"] for e in self.lps)
         self.kids_left = {}     # (model, node key) -> children of it not yet started
         self.warm_parent = 0
         self.records = []       # (--dump) one record per completed node LP
@@ -405,13 +455,15 @@ class ReplayStream:
         self.in_order = bool(getattr(a, "in_order", False))
 
     def peek_entry(self):
-        """(repetition, entry) this rank replays next: entries rank, rank + world, ... of the trace (repeated)."""
-        rep, i = divmod(self.pos, len(self.lps))
-        return rep, self.lps[i]
+        """(repetition, entry) this rank replays next: the trace's entries in recorded order, once (None at its
+        end)."""
+        if self.pos >= len(self.lps):
+            return None
+        return 0, self.lps[self.pos]
 
     def next_entry(self):
         out = self.peek_entry()
-        self.pos += self.stride
+        self.pos += 1
         return out
 
     def _model(self, e):
@@ -435,8 +487,8 @@ class ReplayStream:
         parent's LP is not iterating (where = index into `deferred`, -1 = the upcoming entry); None when every
         candidate waits for its parent and the deferral window is full."""
         if self.in_order:
-            rep, e = self.peek_entry()
-            return -1, rep, e
+            nxt = self.peek_entry()
+            return None if nxt is None else (-1,) + nxt
         running = {(n, v[0]) for (n, _), v in self.running.items()}
 
         def ready(rep, e):
@@ -447,7 +499,10 @@ class ReplayStream:
             if ready(rep, e):
                 return i, rep, e
         while len(self.deferred) < 64:
-            rep, e = self.peek_entry()
+            nxt = self.peek_entry()
+            if nxt is None:
+                return None
+            rep, e = nxt
             if ready(rep, e):
                 return -1, rep, e
             self.deferred.append(self.next_entry())
@@ -554,8 +609,25 @@ class ReplayStream:
             self._refill()
 
 
-def trace_path(a):
-    return os.path.join(REPO, "tests", "golden", f"bnb_trace_{a.nodes}x{a.functions}_s{a.seed}.json.gz")
+def trace_path(a, seed=None):
+    seed = a.seed if seed is None else seed
+    return os.path.join(REPO, "tests", "golden", f"bnb_trace_{a.nodes}x{a.functions}_s{seed}.json.gz")
+
+
+def rank_seed(a, rank, world):
+    """The instance (generator seed) rank `rank` replays.  One rank: --seed.  N ranks: one recorded B&B per GPU —
+    rank r takes seed --seed + r (independent placement requests, weak scaling); without a recorded trace for
+    that seed it takes the recorded seeds in turn (tests/golden/bnb_trace_<N>x<F>_s<seed>.json.gz).  The recorded
+    512x256 search is one narrow dive (p50 ~25 LPs per depth level, 44 levels): dealing ITS subtrees over 8 ranks
+    leaves 56 % of the LPs on one rank (96 % at 2 ranks), so the sharded search itself is measured by the `bnb`
+    section (core/engine/bnb.py over RCCL), not by splitting a single-GPU trace."""
+    if world <= 1:
+        return a.seed
+    want = a.seed + rank
+    if os.path.exists(trace_path(a, want)):
+        return want
+    have = [s_ for s_ in range(a.seed, a.seed + 64) if os.path.exists(trace_path(a, s_))]
+    return have[rank % len(have)] if have else want
 
 
 class NodeStream:
@@ -642,12 +714,13 @@ def _probe_ranks(a, rank, world):
     import gzip
     import torch.distributed as td
     td.init_process_group("gloo")
-    with gzip.open(trace_path(a), "rt") as fh:
+    seed = rank_seed(a, rank, world)
+    with gzip.open(trace_path(a, seed), "rt") as fh:
         trace = json.load(fh)
     rs = ReplayStream({}, a, rank, world, trace)
     ids = [rs.next_entry()[1]["id"] for _ in range(int(os.environ["NEP_BENCH_PROBE_RANKS"]))]
     got = [None] * world
-    td.all_gather_object(got, {"rank": rank, "world": world, "ids": ids})
+    td.all_gather_object(got, {"rank": rank, "world": world, "seed": seed, "ids": ids, "entries": len(rs.lps)})
     if rank == 0:
         print(json.dumps({"probe": "ranks", "ranks": got, "n_gpus": world}), flush=True)
     td.destroy_process_group()
@@ -677,7 +750,8 @@ def main():
     from core.utils.synthetic import synthetic_payload
 
     N, F, B = a.nodes, a.functions, a.batch
-    payload = synthetic_payload(N, F, seed=a.seed)
+    seed = rank_seed(a, rank, world)
+    payload = synthetic_payload(N, F, seed=seed)
     data = data_to_solver_input(payload, with_db=False)
     alpha = payload["solver"]["args"]["alpha"]
     park = max(0, a.park)
@@ -713,11 +787,11 @@ def main():
 
     kind = a.stream
     if kind == "auto":
-        kind = "replay" if os.path.exists(trace_path(a)) else "children"
+        kind = "replay" if os.path.exists(trace_path(a, seed)) else "children"
     bm = fac_root = None
     if kind == "replay":
         import gzip
-        with gzip.open(trace_path(a), "rt") as fh:
+        with gzip.open(trace_path(a, seed), "rt") as fh:
             trace = json.load(fh)
         stream = ReplayStream({"leaf": (m, root)}, a, rank, world, trace)
         if a.native_steps > 0:
@@ -736,8 +810,8 @@ def main():
     else:
         stream = NodeStream(m, root, a, rank)
 
-    def timed(stream, steps, tag):
-        """steps * B nodes of `stream`, drained, timed between barriers (max over ranks)."""
+    def timed(stream, steps, tag, count=None):
+        """steps * B nodes of `stream` (or `count` of them), drained, timed between barriers (max over ranks)."""
         m.reset_stats()
         if bm is not None:
             bm.reset_stats()
@@ -746,9 +820,10 @@ def main():
             td.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        # the timed K steps: K*B nodes streamed through the B slots and drained (every node finished,
-        # hard ones included — no node is left iterating outside the timed region)
-        stream.drain(steps * B)
+        # the timed K steps: K*B nodes (the replay: the whole recorded trace, K steps of 1/K of it each) streamed
+        # through the B slots and drained (every node finished, hard ones included — no node is left iterating
+        # outside the timed region)
+        stream.drain(steps * B if count is None else count)
         ok = [o for st_, o, _, _ in stream.done[i0:] if st_ == LP_OPTIMAL]
         best = torch.tensor([min(ok) if ok else float("inf")], dtype=torch.float64, device=dev)
         if dist:
@@ -796,9 +871,12 @@ def main():
                 "util": util, "stats": st, "warm_split_rank0": split}
 
     if a.warmup > 0:
-        stream.drain(a.warmup * B)
-        log(f"rank {rank}: warmup: {len(stream.done)} node LPs completed")
-    prim = timed(stream, a.steps, kind)
+        # untimed: the first W x B boxes (replay: on a stream of their own — the timed region then replays the
+        # whole trace from its start, so `value` does not depend on --steps / --warmup)
+        ws = ReplayStream({"leaf": (m, root)}, a, rank, world, trace) if kind == "replay" else stream
+        ws.drain(a.warmup * B)
+        log(f"rank {rank}: warmup: {len(ws.done)} node LPs completed")
+    prim = timed(stream, a.steps, kind, count=len(stream.lps) if kind == "replay" else None)
     if a.dump and rank == 0 and getattr(stream, "records", None) is not None:
         with open(a.dump, "w") as fh:
             json.dump(stream.records, fh)
@@ -866,6 +944,7 @@ def main():
             per_lp_iter = t["bytes_per_launch"] / max(1, t.get("lps_per_launch", 1))
             traffic = per_lp_iter * lps_per_launch
             traffic_ratio = per_lp_iter / per_lp
+    flows = alibaba_flows(a) if (world == 1 and a.alibaba_seconds > 0) else None
     cpu = None
     if world == 1 and a.cpu_budget > 0:
         cpu = cpu_baseline(N, F, a.seed, a.fix, a.cpu_budget, a.cpu_workers)
@@ -884,7 +963,28 @@ def main():
         "data": "synthetic (SURVEY.md §8(d) generator, seed %d)" % a.seed,
         "config": {"workload": workload, "nodes": N, "functions": F, "lp_in_flight_per_gpu": B,
                    "fixings_per_lp": a.fix if kind == "children" else "recorded B&B boxes", "tol": a.tol, "max_iters_per_lp": a.max_iters,
-                   "routing_entries_P": P, "parallelism": f"bnb-subtrees x{world}"},
+                   "routing_entries_P": P,
+                   "parallelism": (f"bnb-subtrees x{world}" if kind != "replay" else
+                                   ("one recorded B&B" if world == 1 else f"one recorded B&B per GPU x{world}")),
+                   "timed_lps_per_rank": (len(stream.lps) if kind == "replay" else a.steps * B),
+                   "instance_seed_rank0": seed,
+                   "workload_note": ("value = certified LP relaxations of the REFERENCE model (the LP SCIP solves at "
+                                     "each node) at the boxes the product's own 512x256 B&B submitted in 60 s "
+                                     "(tests/golden/bnb_trace_512x256_s<seed>.json.gz), the whole trace once per "
+                                     "rank in recorded order (a box waits for its parent's LP; finished parents "
+                                     "park their state, --park slots); one step = 1/K of the trace.  The product "
+                                     "search's own node-LP rate (branching nodes on the facility relaxation, "
+                                     "budgets, stops) is `product_node_lp_per_s`"
+                                     if kind == "replay" else "root children with random c-fixings")},
+        "product_node_lp_per_s": {
+            "native_replay_resolved": native["resolved_lp_per_s"] if native else None,
+            "native_replay_certified": native["certified_lp_per_s"] if native else None,
+            "bnb_resolved": ({b_["workload"]: b_["resolved_lp_per_s"] for b_ in bnb} if bnb else None),
+            "bnb_certified": ({b_["workload"]: b_["certified_lp_per_s"] for b_ in bnb} if bnb else None),
+            "note": "the product B&B's node LPs per second: resolved = certified + bound-converged + proven "
+                    "infeasible + cut off (every such LP ends its node); native_replay = the trace's first "
+                    "boxes on the models the product ran them on; bnb = the product search itself"},
+        "alibaba_flows": flows,
         "objective_gap": {"certified_max": gmax, "tol": a.tol,
                           "note": "(primal obj - Lagrangian bound)/max(1,|bound|) per certified LP; "
                                   "HiGHS parity on the reference's own models: tests/test_gpu_lp.py"},

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define NEP_API_VERSION 11
+#define NEP_API_VERSION 12
 
 /* variants: neptune.py:41-66 (NeptuneMinDelay / MinUtilization / MinDelayAndUtilization) */
 enum { NEP_MIN_DELAY = 0, NEP_MIN_UTILIZATION = 1, NEP_MIN_DELAY_AND_UTILIZATION = 2 };
@@ -289,6 +289,7 @@ typedef struct {
   double upper_bound;              /* a-priori cutoff (+inf: none) */
   int64_t node_limit;
   double time_limit;               /* seconds (<= 0: none) */
+  int32_t world, rank;             /* API 12: the sharded search (world > 1: NEP_BNB_SYNC once per loop) */
 } nep_bnb_params;
 
 typedef struct {
@@ -301,6 +302,12 @@ typedef struct {
   int32_t incumbent_source;        /* 0 none, 1 a certified leaf LP, 2 nep_bnb_set_incumbent */
   int32_t incumbent_slot;          /* leaf-model slot holding the incumbent LP's state (source 1) */
   int32_t limit_hit, any_unresolved, unresolved_below;
+  int32_t stalled;                 /* API 12: ended because open nodes could never get a slot (reported as a limit) */
+  uint32_t split_hash;             /* sharded: crc32 of the frontier every rank dealt (bnb.py _frontier_hash) */
+  int32_t reserved_;
+  int64_t presplit_nodes, presplit_lps, presplit_certified;   /* sharded: counts when the frontier was dealt */
+  int64_t rebalanced, sync_calls;  /* sharded: open nodes imported from other ranks; collectives answered */
+  double agreed_incumbent;         /* min(this rank's incumbent, the ranks' agreed one) */
 } nep_bnb_stats;
 
 #define NEP_BNB_DONE 0   /* the search ended (no open node, or a stop): stats / incumbent are final */
@@ -308,9 +315,34 @@ typedef struct {
                             nep_bnb_set_incumbent for the caller's primal heuristic, then nep_bnb_run again */
 #define NEP_BNB_INCUMBENT 2   /* (nep_bnb_set_step2 with incumbent_events) a new LP incumbent: nep_bnb_incumbent_event,
                                  then nep_bnb_add_leaf(where = 2) for each neighbour leaf, then nep_bnb_run again */
+#define NEP_BNB_SYNC 3   /* (world > 1) the loop's collective is due: nep_bnb_sync_get, the caller's all-reduce over the
+                            ranks (incumbent MIN, stop OR, open SUM; core/engine/comm.py agree), nep_bnb_sync_set,
+                            optionally a rebalance (nep_bnb_export_nodes / nep_bnb_import_nodes), then nep_bnb_run */
 
+/* API 12: the calls the tree makes on one model, with the model's integer vector length and slot count.
+ * nep_bnb_create fills one from an engine handle (the nep_lp_* functions, ctx = the handle); a caller may pass its
+ * own (the CPU suite: HiGHS node LPs behind ctypes callbacks).  Same contracts as the nep_lp_* functions. */
+typedef struct {
+  void *ctx;
+  int32_t n_int, max_batch;
+  int (*submit)(void *ctx, int32_t n, const int32_t *slots, const double *lb_int, const double *ub_int,
+                const nep_lp_opts *opts, int32_t *status);
+  int (*advance)(void *ctx, int32_t min_done, int32_t *n_done, int32_t *done_slots, double *obj, double *primal_obj,
+                 int32_t *status, int64_t *iters);
+  int (*active)(void *ctx);
+  int (*copy_state)(void *ctx, int32_t src_slot, int32_t dst_slot);
+  int (*set_params)(void *ctx, double tol, double cutoff);
+  int (*get_flows)(void *ctx, int32_t n, const int32_t *slots, float *flows);
+  int (*get_solutions)(void *ctx, int32_t n, const int32_t *slots, double *z_out);
+  int (*get_diag)(void *ctx, int32_t slot, double *out16);
+} nep_bnb_engine;
+
+/* NULL on a bad argument (nep_last_error says which): batch < 1, a layout outside n_int, no working slot left
+ * after the reserved ones, world / rank out of range. */
 void *nep_bnb_create(void *leaf_model, void *bound_model, const nep_bnb_params *params, const double *fn_mem,
                      const double *node_mem);
+void *nep_bnb_create_engines(const nep_bnb_engine *leaf, const nep_bnb_engine *bound, const nep_bnb_params *params,
+                             const double *fn_mem, const double *node_mem);
 void nep_bnb_destroy(void *tree);
 /* a leaf (a full c / n assignment, or any box): where = 0 a seed leaf queued when the root LP finishes;
  * where = 1 a leaf of the NEP_BNB_ROOT event's node, where = 2 a neighbour of the NEP_BNB_INCUMBENT event's
@@ -328,9 +360,20 @@ int nep_bnb_debug_ibound(const nep_bnb_params *params, int32_t create, double no
 int nep_bnb_set_incumbent(void *tree, double value);
 int nep_bnb_event_data(void *tree, double *z_int, float *flow);
 int nep_bnb_run(void *tree, int32_t *event);
+/* NEP_BNB_SYNC: out6 = {incumbent, stop, open + in-flight nodes, heap size, frontier dealt, collectives so far};
+ * the caller answers with the agreed values (a lower incumbent becomes every model's cutoff at once) */
+int nep_bnb_sync_get(void *tree, double *out6);
+int nep_bnb_sync_set(void *tree, double incumbent, int32_t stop, int64_t open_total);
+/* rebalance (bnb.py _rebalance): the k best-bound open nodes leave this rank's heap (lens[k]; meta[k][3] = bound,
+ * depth, kind; idx / val concatenated, at most cap entries) / enter it (pruned against the incumbent; they start
+ * from the model's root state) */
+int nep_bnb_export_nodes(void *tree, int32_t k, int32_t cap, int32_t *lens, double *meta, int32_t *idx, double *val);
+int nep_bnb_import_nodes(void *tree, int32_t k, const int32_t *lens, const double *meta, const int32_t *idx,
+                         const double *val);
 int nep_bnb_get_stats(void *tree, nep_bnb_stats *out);
 int nep_bnb_get_lp_iters(void *tree, int64_t *out);
-/* the LP incumbent's integer vector and its leaf box (*n_fix = -1: no LP incumbent) */
+/* the LP incumbent's integer vector (n_int) and its leaf box (at most c1 - c0 + n1 - n0 entries: a leaf fixes every
+ * c and n; *n_fix = -1: no LP incumbent) */
 int nep_bnb_incumbent(void *tree, double *z_int, int32_t *n_fix, int32_t *idx, double *val);
 
 const char *nep_last_error(void);

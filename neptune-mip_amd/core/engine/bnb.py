@@ -702,7 +702,7 @@ class BranchAndBound:
             res.polished = True
         # (uncertified: the slot's state moved on; res.x / res.z stay the certified leaf's, fetched before)
 
-    def _finish_sharded(self, res, inc, limit_hit, unresolved_below):
+    def _finish_sharded(self, res, inc, limit_hit, unresolved_below, any_unresolved=None):
         """End of a sharded search: one all-gather of every rank's summary; the owner of the best
         certified incumbent (lowest rank on ties, chosen on the certified objectives BEFORE any polish)
         polishes it and broadcasts objective, integer vector and compacted routing entries."""
@@ -710,7 +710,7 @@ class BranchAndBound:
         mine = res.objective is not None and res.objective <= inc
         g = comm.gather([res.bound, 1.0 if limit_hit else 0.0, 1.0 if unresolved_below else 0.0, 1.0 if mine else 0.0,
                          res.nodes - self.presplit[0], res.lps - self.presplit[1], res.certified - self.presplit[2],
-                         1.0 if self.unresolved_bounds else 0.0])
+                         1.0 if (any_unresolved if any_unresolved is not None else self.unresolved_bounds) else 0.0])
         res.bound = float(g[:, 0].min())
         self._limit_hit = bool(g[:, 1].max() > 0)
         self._unresolved_below = bool(g[:, 2].max() > 0)
@@ -744,26 +744,74 @@ class BranchAndBound:
 
     # ---------------------------------------------------------------------------------------
     def _native_ok(self, comm):
+        """The native tree runs every search without per-node Python callbacks — single rank or sharded (API 12) —
+        on the engine's models by default, and on any Python model with the streaming interface (the CPU suite's
+        HiGHS node LPs, through lp.PyBnbEngine) when native=True."""
         if self.native is False or os.environ.get("NEP_BNB_PYTHON", "0") not in ("", "0"):
             return False
         s2 = self.step2_native is not None and os.environ.get("NEP_BNB_STEP2", STEP2_NATIVE_DEFAULT) not in ("", "0")
-        eligible = (comm.world == 1 and self.trace is None
-                    and (self.integer_bound is None or s2) and (self.improve is None or s2)
-                    and not self.leaf_routing_warm and self.primal_every == 0 and hasattr(self.lp, "_h")
-                    and (self.bound_lp is None or hasattr(self.bound_lp, "_h")))
+        engine = hasattr(self.lp, "_h") and (self.bound_lp is None or hasattr(self.bound_lp, "_h"))
+        eligible = (self.trace is None and (self.integer_bound is None or s2) and (self.improve is None or s2)
+                    and not self.leaf_routing_warm and self.primal_every == 0 and (engine or self.native is True))
+        if comm.world > 1 and os.environ.get("NEP_BNB_SHARDED_NATIVE", "1") in ("", "0"):
+            eligible = False
         if self.native and not eligible:
-            raise ValueError("native tree search: single rank, no trace / leaf routing warm starts / primal_every, "
+            raise ValueError("native tree search: no trace / leaf routing warm starts / primal_every, "
                              "integer_bound and improve only with step2_native")
         return eligible
+
+    def _rebalance_native(self, lib, tree, heap_n):
+        """_rebalance on the native tree: the same pairing from one all-gather of the heap sizes, the donor's k
+        best-bound open nodes exported (nep_bnb_export_nodes) and broadcast, imported by the idle rank (pruned
+        against the agreed incumbent; they start from that rank's root state)."""
+        from .lp import _check, _ptr
+        comm = self.comm
+        cnt = comm.gather([float(heap_n)])[:, 0].astype(np.int64)
+        idle = [r for r in range(comm.world) if cnt[r] == 0]
+        nb = self._nb + 1
+        for r in idle:
+            d = int(np.argmax(cnt))
+            k = int(min(cnt[d] // 2, self.batch))
+            if k <= 0:
+                break
+            cnt[d] -= k
+            cnt[r] += k
+            if comm.rank == d:
+                lens = np.zeros(k, np.int32)
+                meta = np.zeros(3 * k)
+                idx = np.zeros(k * nb, np.int32)
+                val = np.zeros(k * nb)
+                _check(lib, lib.nep_bnb_export_nodes(tree, k, k * nb, _ptr(lens), _ptr(meta), _ptr(idx), _ptr(val)),
+                       "nep_bnb_export_nodes")
+                tot = int(lens.sum())
+                head = np.concatenate([[k], lens.astype(np.float64)])
+            else:
+                head = np.zeros(k + 1)
+            head = comm.bcast(head, d)
+            lens = head[1:].astype(np.int32)
+            tot = int(lens.sum())
+            if comm.rank == d:
+                body = np.concatenate([meta, idx[:tot].astype(np.float64), val[:tot]])
+            else:
+                body = np.zeros(3 * k + 2 * tot)
+            body = comm.bcast(body, d)
+            if comm.rank == r:
+                meta = np.ascontiguousarray(body[:3 * k])
+                idx = np.ascontiguousarray(body[3 * k:3 * k + tot].astype(np.int32))
+                val = np.ascontiguousarray(body[3 * k + tot:])
+                _check(lib, lib.nep_bnb_import_nodes(tree, k, _ptr(lens), _ptr(meta), _ptr(idx), _ptr(val)),
+                       "nep_bnb_import_nodes")
 
     def _solve_native(self):
         """solve() on the native tree (nep_bnb_*, csrc/nep_bnb.cpp): the same search, its loop in the library;
         this method handles the root's primal heuristic (NEP_BNB_ROOT) and the end (routing, polish, repair)."""
         import ctypes
-        from .lp import BnbParams, BnbStats, _check, _ptr
+        from .lp import BnbParams, BnbStats, PyBnbEngine, _check, _ptr, load_library
         t0 = self.t0 = time.time()
         self.res = res = BnBResult()
-        lp, lib = self.lp, self.lp._lib
+        comm = self.comm
+        lp = self.lp
+        lib = getattr(lp, "_lib", None) or load_library()
         n0, n1 = self.n_range if self.n_range is not None else (-1, -1)
         inf = math.inf
         p = BnbParams(c0=self.c0, c1=self.c1, n0=n0, n1=n1, n_int=lp.n_int, F=self.F, N=self.N,
@@ -775,12 +823,31 @@ class BranchAndBound:
                       bound_gap=self.bound_gap, max_iters=int(self.max_iters), node_max_iters=int(self.node_max_iters),
                       root_max_iters=int(self.root_max_iters), node_bound_res=float(self.node_bound_res or 0.0),
                       retry_res=float(self.retry_res), flow_tol=float(self.flow_tol), upper_bound=float(self.ub0),
-                      node_limit=int(self.node_limit), time_limit=float(self.time_limit or 0.0))
-        tree = lib.nep_bnb_create(lp._h, self.bound_lp._h if self.two else None, ctypes.byref(p), _ptr(self.fn_mem),
-                                  _ptr(self.node_mem))
+                      # (round-5 ADVICE: a non-finite node limit is no limit)
+                      node_limit=int(min(float(self.node_limit), 2.0 ** 62)), time_limit=float(self.time_limit or 0.0),
+                      world=int(comm.world), rank=int(comm.rank))
+        py_engines = []
+        if hasattr(lp, "_h"):
+            tree = lib.nep_bnb_create(lp._h, self.bound_lp._h if self.two else None, ctypes.byref(p),
+                                      _ptr(self.fn_mem), _ptr(self.node_mem))
+        else:
+            py_engines = [PyBnbEngine(lp, self.F, self.N)] + ([PyBnbEngine(self.bound_lp, self.F, self.N)]
+                                                              if self.two else [])
+            tree = lib.nep_bnb_create_engines(ctypes.byref(py_engines[0].table),
+                                              ctypes.byref(py_engines[1].table) if self.two else None,
+                                              ctypes.byref(p), _ptr(self.fn_mem), _ptr(self.node_mem))
         if not tree:
-            raise RuntimeError("nep_bnb_create failed")
+            raise RuntimeError(f"nep_bnb_create failed: {lib.nep_last_error().decode()}")
+
+        def run_checked(what, rc):
+            for e in py_engines:
+                if e.error is not None:
+                    raise e.error
+            _check(lib, rc, what)
+
         bm = self.bound_lp if self.two else lp
+        loops = 0
+        split_seen = False
         try:
             if self.step2_native is not None:
                 create, cap, old = self.step2_native
@@ -792,10 +859,25 @@ class BranchAndBound:
                 val = np.ascontiguousarray(val, np.float64)
                 _check(lib, lib.nep_bnb_add_leaf(tree, len(idx), _ptr(idx), _ptr(val), -inf, 0), "nep_bnb_add_leaf")
             ev = ctypes.c_int32()
+            sync = np.zeros(6)
             while True:
-                _check(lib, lib.nep_bnb_run(tree, ctypes.byref(ev)), "nep_bnb_run")
+                run_checked("nep_bnb_run", lib.nep_bnb_run(tree, ctypes.byref(ev)))
                 if ev.value == 0:
                     break
+                if ev.value == 3:
+                    # NEP_BNB_SYNC (sharded): the loop's one collective — incumbent MIN, stop OR, open SUM — then,
+                    # every rebalance_every loops after the split, the open-node rebalance
+                    _check(lib, lib.nep_bnb_sync_get(tree, _ptr(sync)), "nep_bnb_sync_get")
+                    inc_l, stop_l, open_l, heap_n, split = float(sync[0]), bool(sync[1]), int(sync[2]), int(sync[3]), \
+                        bool(sync[4])
+                    inc_g, stop_g, total = comm.agree(inc_l, stop_l, open_l)
+                    _check(lib, lib.nep_bnb_sync_set(tree, inc_g, 1 if stop_g else 0, int(total)), "nep_bnb_sync_set")
+                    split_seen = split_seen or split
+                    if not stop_g and (total if split else open_l) > 0:
+                        loops += 1
+                        if split and self.rebalance_every and loops % self.rebalance_every == 0:
+                            self._rebalance_native(lib, tree, heap_n)
+                    continue
                 if ev.value == 2:
                     # NEP_BNB_INCUMBENT: the neighbour leaves of a new LP incumbent (step 2's node relocation)
                     n_fix = ctypes.c_int32()
@@ -861,21 +943,34 @@ class BranchAndBound:
         tm["advance"], tm["finish"], tm["submit"] = st.advance_seconds, st.finish_seconds, st.submit_seconds
         tm["drain"], tm["root"] = st.drain_seconds, st.root_seconds
         res.native = True
+        res.rebalanced = int(st.rebalanced)
+        res.split_hash = int(st.split_hash) if split_seen else None
         t_end = time.perf_counter()
         res.bound = float(st.bound)
-        if res.objective is not None and res.incumbent_slot is not None:
-            res.x = lp.routing(res.incumbent_slot)
-            if self.polish_tol:
-                self._polish(res)
+        limit_hit, unresolved_below = bool(st.limit_hit), bool(st.unresolved_below)
+        if comm.world == 1:
+            if res.objective is not None and res.incumbent_slot is not None:
+                res.x = lp.routing(res.incumbent_slot)
+                if self.polish_tol:
+                    self._polish(res)
+        else:
+            self.presplit = (int(st.presplit_nodes), int(st.presplit_lps), int(st.presplit_certified)) \
+                if split_seen else (res.nodes, res.lps, res.certified)
+            self._finish_sharded(res, float(st.agreed_incumbent), limit_hit, unresolved_below,
+                                 any_unresolved=bool(st.any_unresolved))
+            limit_hit, unresolved_below = self._limit_hit, self._unresolved_below
         if res.objective is not None and self.repair is not None:
             res.x, dobj, res.repaired = self.repair(res.x, res.z)
             res.objective += dobj
             if not res.repaired:
                 self.log("incumbent routing: CPU repair incomplete")
+        any_unresolved = bool(st.any_unresolved) if comm.world == 1 else self._any_unresolved
         if res.objective is None:
-            res.status = LIMIT if (st.limit_hit or st.any_unresolved) else INFEASIBLE
+            res.status = LIMIT if (limit_hit or any_unresolved) else INFEASIBLE
         else:
-            res.status = LIMIT if (st.limit_hit or st.unresolved_below) else OPTIMAL
+            res.status = LIMIT if (limit_hit or unresolved_below) else OPTIMAL
+        if st.stalled:
+            self.log("search stalled: open nodes could not get an LP slot (reported as a limit)")
         res.timing["end"] = time.perf_counter() - t_end
         res.seconds = time.time() - t0
         return res

@@ -18,7 +18,7 @@ STEP1, STEP2_DELETE, STEP2_CREATE = 1, 2, 3
 LP_OPTIMAL, LP_ITERATION_LIMIT, LP_INFEASIBLE, LP_CUTOFF, LP_NUMERICAL, LP_BOUND = 0, 1, 2, 3, 4, 5
 VARIANTS = {"MinDelay": MIN_DELAY, "MinUtilization": MIN_UTILIZATION,
             "MinDelayAndUtilization": MIN_DELAY_AND_UTILIZATION}
-API_VERSION = 11
+API_VERSION = 12
 RELAX_REFERENCE, RELAX_FACILITY = 0, 1
 
 _dp = ctypes.POINTER(ctypes.c_double)
@@ -69,7 +69,8 @@ class BnbParams(ctypes.Structure):
                 ("bound_gap", ctypes.c_double), ("max_iters", ctypes.c_int64), ("node_max_iters", ctypes.c_int64),
                 ("root_max_iters", ctypes.c_int64), ("node_bound_res", ctypes.c_double),
                 ("retry_res", ctypes.c_double), ("flow_tol", ctypes.c_double), ("upper_bound", ctypes.c_double),
-                ("node_limit", ctypes.c_int64), ("time_limit", ctypes.c_double)]
+                ("node_limit", ctypes.c_int64), ("time_limit", ctypes.c_double),
+                ("world", ctypes.c_int32), ("rank", ctypes.c_int32)]
 
 
 class BnbStats(ctypes.Structure):
@@ -81,7 +82,105 @@ class BnbStats(ctypes.Structure):
                [(k, ctypes.c_double) for k in ("advance_seconds", "finish_seconds", "submit_seconds", "drain_seconds",
                                                "root_seconds", "bound", "incumbent")] + \
                [(k, ctypes.c_int32) for k in ("incumbent_source", "incumbent_slot", "limit_hit", "any_unresolved",
-                                              "unresolved_below")]
+                                              "unresolved_below", "stalled")] + \
+               [("split_hash", ctypes.c_uint32), ("reserved_", ctypes.c_int32)] + \
+               [(k, ctypes.c_int64) for k in ("presplit_nodes", "presplit_lps", "presplit_certified", "rebalanced",
+                                              "sync_calls")] + \
+               [("agreed_incumbent", ctypes.c_double)]
+
+
+# nep_bnb_engine (API 12): the calls the native tree makes on one model
+_i32p, _i64p, _dblp = ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_double)
+_fltp = ctypes.POINTER(ctypes.c_float)
+BNB_SUBMIT = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int32, _i32p, _dblp, _dblp,
+                              ctypes.POINTER(LpOpts), _i32p)
+BNB_ADVANCE = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int32, _i32p, _i32p, _dblp, _dblp, _i32p,
+                               _i64p)
+BNB_ACTIVE = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p)
+BNB_COPY = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32)
+BNB_PARAMS = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_double, ctypes.c_double)
+BNB_FLOWS = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int32, _i32p, _fltp)
+BNB_SOLS = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int32, _i32p, _dblp)
+BNB_DIAG = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int32, _dblp)
+
+
+class BnbEngine(ctypes.Structure):
+    _fields_ = [("ctx", ctypes.c_void_p), ("n_int", ctypes.c_int32), ("max_batch", ctypes.c_int32),
+                ("submit", BNB_SUBMIT), ("advance", BNB_ADVANCE), ("active", BNB_ACTIVE), ("copy_state", BNB_COPY),
+                ("set_params", BNB_PARAMS), ("get_flows", BNB_FLOWS), ("get_solutions", BNB_SOLS),
+                ("get_diag", BNB_DIAG)]
+
+
+class PyBnbEngine:
+    """A nep_bnb_engine call table over a Python model with LPModel's streaming interface (submit / advance /
+    active / copy_state / set_params / flows / solutions / diag, n_int, max_batch): lets the native tree search
+    (csrc/nep_bnb.cpp, nep_bnb_create_engines) drive node LPs that are not the engine's — the CPU suite runs it
+    over HiGHS (tests/oracle_lp.py).  A Python exception inside a call ends the search with NEP_ERR_STATE and is
+    kept in `error` (BranchAndBound re-raises it)."""
+
+    def __init__(self, model, F, N):
+        self.model, self.F, self.N = model, int(F), int(N)
+        self.n_int, self.max_batch = int(model.n_int), int(model.max_batch)
+        self.error = None
+        ni, mb = self.n_int, self.max_batch
+        A = np.ctypeslib.as_array
+
+        def guard(fn):
+            def call(*args):
+                try:
+                    fn(*args)
+                    return 0
+                except BaseException as e:      # (never unwind through the C frames)
+                    self.error = e
+                    return -4
+            return call
+
+        def submit(_, n, slots, lb, ub, opts, status):
+            o = opts.contents
+            st = model.submit(A(slots, (n,)).copy(), A(lb, (n, ni)).copy(), A(ub, (n, ni)).copy(), tol=o.tol,
+                              cutoff=o.cutoff, max_iters=int(o.max_iters), check_every=int(o.check_every),
+                              warm_start=bool(o.warm_start), bound_res=o.bound_res, gap_tol=o.gap_tol)
+            A(status, (n,))[:] = np.asarray(st, np.int32)
+
+        def advance(_, min_done, n_done, slots, obj, pobj, status, iters):
+            r = model.advance(int(min_done))
+            k = len(r["slots"])
+            n_done[0] = k
+            if k:
+                A(slots, (mb,))[:k] = r["slots"]
+                A(obj, (mb,))[:k] = r["obj"]
+                A(pobj, (mb,))[:k] = r["primal_obj"]
+                A(status, (mb,))[:k] = r["status"]
+                A(iters, (mb,))[:k] = r["iters"]
+
+        def copy_state(_, src, dst):
+            model.copy_state(int(src), int(dst))
+
+        def set_params(_, tol, cutoff):
+            model.set_params(tol, cutoff)
+
+        def flows(_, n, slots, out):
+            A(out, (n * self.F * self.N,))[:] = np.asarray(model.flows(A(slots, (n,)).copy()), np.float32).ravel()
+
+        def sols(_, n, slots, out):
+            A(out, (n * ni,))[:] = np.asarray(model.solutions(A(slots, (n,)).copy()), np.float64).ravel()
+
+        def diag(_, slot, out):
+            d = model.diag(int(slot))
+            o = A(out, (16,))
+            o[:] = 0.0
+            o[3] = float(d.get("pres", 0.0))
+
+        def active(_):
+            try:
+                return int(model.active())
+            except BaseException as e:
+                self.error = e
+                return 0
+
+        self.table = BnbEngine(None, ni, mb, BNB_SUBMIT(guard(submit)), BNB_ADVANCE(guard(advance)),
+                               BNB_ACTIVE(active), BNB_COPY(guard(copy_state)), BNB_PARAMS(guard(set_params)),
+                               BNB_FLOWS(guard(flows)), BNB_SOLS(guard(sols)), BNB_DIAG(guard(diag)))
 
 
 # every entry point declared in include/neptune_lp.h
@@ -95,7 +194,8 @@ EXPORTS = ("nep_model_create", "nep_model_destroy", "nep_model_get_info", "nep_l
            "nep_lp_get_solutions", "nep_round_leaves", "nep_lp_set_reference_weight",
            "nep_bnb_create", "nep_bnb_destroy", "nep_bnb_add_leaf", "nep_bnb_set_incumbent", "nep_bnb_event_data",
            "nep_bnb_run", "nep_bnb_get_stats", "nep_bnb_get_lp_iters", "nep_bnb_incumbent", "nep_bnb_set_step2",
-           "nep_bnb_incumbent_event", "nep_bnb_debug_ibound")
+           "nep_bnb_incumbent_event", "nep_bnb_debug_ibound", "nep_bnb_create_engines", "nep_bnb_sync_get",
+           "nep_bnb_sync_set", "nep_bnb_export_nodes", "nep_bnb_import_nodes")
 SCORE_FIELDS = ("network_delay", "nodes_used", "node_cost", "bad_c_x", "bad_memory", "bad_handle", "bad_cpu",
                 "bad_n_c", "bad_budget", "handle_maxdev", "cpu_maxexcess")
 
@@ -163,6 +263,13 @@ def load_library(path=None):
     lib.nep_bnb_set_step2.argtypes = [vp, i32, ctypes.c_double, _dp, i32]
     lib.nep_bnb_incumbent_event.argtypes = [vp, pi32, pi32, _dp, _dp]
     lib.nep_bnb_debug_ibound.argtypes = [ctypes.POINTER(BnbParams), i32, ctypes.c_double, _dp, i32, pi32, _dp, _dp]
+    lib.nep_bnb_create_engines.argtypes = [ctypes.POINTER(BnbEngine), ctypes.POINTER(BnbEngine),
+                                           ctypes.POINTER(BnbParams), _dp, _dp]
+    lib.nep_bnb_create_engines.restype = vp
+    lib.nep_bnb_sync_get.argtypes = [vp, _dp]
+    lib.nep_bnb_sync_set.argtypes = [vp, ctypes.c_double, i32, i64]
+    lib.nep_bnb_export_nodes.argtypes = [vp, i32, i32, pi32, _dp, pi32, _dp]
+    lib.nep_bnb_import_nodes.argtypes = [vp, i32, pi32, _dp, pi32, _dp]
     lib.nep_lp_get_flows.argtypes = [vp, i32, pi32, ctypes.POINTER(ctypes.c_float)]
     lib.nep_lp_get_flows_split.argtypes = [vp, i32, pi32, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float)]
     lib.nep_lp_routing_entries.argtypes = [vp, i32, ctypes.c_double, i32, i64, pi64, pi32, pi32, _dp]

@@ -17,15 +17,18 @@ from .solvers import SOLVERS
 from .utils import check_input, data_to_solver_input
 
 
-def solve_request(payload):
+def solve_request(payload, solver_out=None):
     """Response body of the reference's `serve()` for one payload (dict).  A malformed payload fails
-    the reference's input assertions (`check_input`, main.py:35) before any engine call."""
+    the reference's input assertions (`check_input`, main.py:35) before any engine call.  solver_out: a list
+    that receives the solver object (bench.py reads each step's B&B status from it)."""
     check_input(payload)
     solver = payload.get("solver", {"type": "NeptuneMinDelayAndUtilization"})
     solver_type = solver.get("type")
     solver_args = solver.get("args", {})
     with_db = payload.get("with_db", True)
     s = SOLVERS[solver_type](**solver_args)
+    if solver_out is not None:
+        solver_out.append(s)
     start = time.time()
     s.load_data(data_to_solver_input(payload, with_db=with_db, workload_coeff=payload.get("workload_coeff", 1)))
     s.solve()

@@ -9,6 +9,13 @@
 // (the host share of the 64x32 search, DESIGN.md §7 "Native tree search").  Decision order and tie-breaks are
 // bnb.py's, so the two searches visit the same tree (tests/test_gpu_bnb_native.py compares them).
 //
+// API 12: the models are reached through a call table (nep_bnb_engine: nep_lp_* on an engine handle, or a
+// caller's own — the CPU suite drives the tree over HiGHS node LPs, tests/test_bnb_native_cpu.py), and the
+// sharded search runs here too: with world > 1 the tree stops once per loop with NEP_BNB_SYNC for the caller's
+// one collective (incumbent MIN, stop OR, open count SUM; core/engine/comm.py agree), deals the frontier at
+// world x batch open nodes (the same canonical order and crc32 as bnb.py) and exports / imports open nodes for
+// the caller's rebalance.
+//
 // Reference: SCIP's tree search inside pywraplp Solver.Solve() (core/solvers/solver.py:35-40).
 #include <algorithm>
 #include <chrono>
@@ -25,7 +32,13 @@
 
 #include "../../include/neptune_lp.h"
 
+namespace nep {
+int set_error(int code, const char *msg);   // nep_host.cpp: nep_last_error's thread-local message
+}
+
 namespace {
+
+int bad(int code, const char *msg) { return nep::set_error(code, msg); }
 
 constexpr double INF = std::numeric_limits<double>::infinity();
 enum Kind { NODE = 0, LEAF = 1, RETRY = 2, REFROOT = 3 };
@@ -59,7 +72,7 @@ struct Node {
 using NodeP = std::shared_ptr<Node>;
 
 struct Engine {
-  void *lp = nullptr;
+  nep_bnb_engine ops{};         // the model's calls (ops.ctx: the engine handle for nep_lp_*)
   int n_int = 0;                // this model's integer vector length (its boxes, solutions)
   int max_batch = 0, reserved = 0, root_slot = -1, inc_slot = -1;
   std::vector<int64_t> gen;
@@ -86,6 +99,56 @@ double now_s() {
   return duration<double>(steady_clock::now().time_since_epoch()).count();
 }
 
+// zlib's crc32 (poly 0xEDB88320), chained like zlib.crc32(data, crc): the frontier hash of bnb.py
+uint32_t crc32_update(uint32_t crc, const void *data, size_t n) {
+  static uint32_t table[256];
+  static bool init = false;
+  if (!init) {
+    for (uint32_t i = 0; i < 256; ++i) {
+      uint32_t c = i;
+      for (int k = 0; k < 8; ++k) c = (c & 1) ? 0xEDB88320u ^ (c >> 1) : c >> 1;
+      table[i] = c;
+    }
+    init = true;
+  }
+  const unsigned char *p = static_cast<const unsigned char *>(data);
+  crc = ~crc;
+  for (size_t i = 0; i < n; ++i) crc = table[(crc ^ p[i]) & 0xFFu] ^ (crc >> 8);
+  return ~crc;
+}
+
+// the nep_lp_* calls of an engine model as a call table (ctx = the model handle)
+int op_submit(void *c, int32_t n, const int32_t *sl, const double *lb, const double *ub, const nep_lp_opts *o,
+              int32_t *st) { return nep_lp_submit(c, n, sl, lb, ub, o, st); }
+int op_advance(void *c, int32_t md, int32_t *nd, int32_t *sl, double *ob, double *po, int32_t *st, int64_t *it) {
+  return nep_lp_advance(c, md, nd, sl, ob, po, st, it);
+}
+int op_active(void *c) { return nep_lp_active(c); }
+int op_copy(void *c, int32_t a, int32_t b) { return nep_lp_copy_state(c, a, b); }
+int op_params(void *c, double tol, double cut) { return nep_lp_set_params(c, tol, cut); }
+int op_flows(void *c, int32_t n, const int32_t *sl, float *f) { return nep_lp_get_flows(c, n, sl, f); }
+int op_sols(void *c, int32_t n, const int32_t *sl, double *z) { return nep_lp_get_solutions(c, n, sl, z); }
+int op_diag(void *c, int32_t s, double *o) { return nep_lp_get_diag(c, s, o); }
+
+int model_ops(void *lp, nep_bnb_engine *out) {
+  nep_model_info info{};
+  const int rc = nep_model_get_info(lp, &info);
+  if (rc) return rc;
+  *out = nep_bnb_engine{};
+  out->ctx = lp;
+  out->n_int = info.n_int;
+  out->max_batch = info.max_batch;
+  out->submit = op_submit;
+  out->advance = op_advance;
+  out->active = op_active;
+  out->copy_state = op_copy;
+  out->set_params = op_params;
+  out->get_flows = op_flows;
+  out->get_solutions = op_sols;
+  out->get_diag = op_diag;
+  return NEP_OK;
+}
+
 }  // namespace
 
 struct NepBnb {
@@ -101,7 +164,8 @@ struct NepBnb {
   std::vector<double> unresolved_bounds;
   std::vector<int64_t> lp_iters;
   int64_t seq = 0;
-  double inc = INF;
+  double inc = INF;          // this rank's incumbent (its own LP leaves / heuristic points)
+  double cut = INF;          // sharded search: the incumbent the ranks agreed on (prunes like inc)
   int inc_source = 0;        // 0 none, 1 an LP leaf (inc_slot / kept slot), 2 external (nep_bnb_set_incumbent)
   int inc_slot = -1;         // slot of the leaf engine holding the incumbent's state
   int keep_slot = -1;        // (warm = 0) a working slot kept for the incumbent
@@ -129,6 +193,14 @@ struct NepBnb {
   };
   std::deque<IncEvent> inc_queue;
   IncEvent cur_inc;
+  // sharded search (p.world > 1): one NEP_BNB_SYNC per loop for the caller's collective
+  bool split = false;        // the frontier has been dealt (before: every rank runs the same search)
+  bool sync_answered = false;
+  double sync_out[6] = {0, 0, 0, 0, 0, 0};   // incumbent, stop, open, heap size, split, loops
+  double agreed_inc = INF;
+  bool agreed_stop = false;
+  int64_t agreed_open = 0;
+  bool stalled = false;      // nothing could be submitted and nothing was in flight (ends the search)
   // scratch
   std::vector<int32_t> sl, done_slots, sts;
   std::vector<double> obj, pobj, lbv, ubv;
@@ -142,7 +214,8 @@ struct NepBnb {
     if (p.objective_integral) g = std::max(g, 1.0 - std::min(0.5, 1e-6 + 1e-9 * std::fabs(incv)));
     return g;
   }
-  bool pruned(double bound) const { return bound >= inc - gap_abs(inc); }
+  double incv() const { return std::min(inc, cut); }   // the pruning incumbent (the agreed one when sharded)
+  bool pruned(double bound) const { return bound >= incv() - gap_abs(incv()); }
   static std::string key_of(const std::vector<double> &val) {
     std::string k((val.size() + 7) / 8, '\0');
     for (size_t i = 0; i < val.size(); ++i)
@@ -153,9 +226,16 @@ struct NepBnb {
   Engine *engines[2] = {nullptr, nullptr};
   int n_engines() const { return two ? 2 : 1; }
 
-  void set_cutoffs() {
-    for (int e = 0; e < n_engines(); ++e) nep_lp_set_params(engines[e]->lp, p.tol, std::min(inc, p.upper_bound));
+  int set_cutoffs() {
+    for (int e = 0; e < n_engines(); ++e) {
+      const nep_bnb_engine &o = engines[e]->ops;
+      const int rc = o.set_params(o.ctx, p.tol, std::min(incv(), p.upper_bound));
+      if (rc) return rc;
+    }
+    return NEP_OK;
   }
+  void deal_frontier();
+  int export_nodes(int k, int32_t cap, int32_t *lens, double *meta, int32_t *idx, double *val);
 
   int submit(std::vector<std::pair<Engine *, std::pair<int, NodeP>>> &items);
   int finish_block(Engine &eng, int nd);
@@ -168,18 +248,21 @@ struct NepBnb {
 
 namespace {
 
-void init_engine(Engine &e, void *lp, int reserved) {
-  nep_model_info info{};
-  nep_model_get_info(lp, &info);
-  e.lp = lp;
-  e.n_int = info.n_int;
-  e.max_batch = info.max_batch;
-  e.reserved = info.max_batch > reserved ? reserved : 0;
-  e.root_slot = info.max_batch - 1;
-  e.inc_slot = info.max_batch - 2;
-  e.gen.assign(info.max_batch, 0);
-  e.running.assign(info.max_batch, nullptr);
-  for (int s = 0; s < info.max_batch - e.reserved; ++s) e.free.push_back(s);
+void init_engine(Engine &e, const nep_bnb_engine &ops, int reserved) {
+  e.ops = ops;
+  e.n_int = ops.n_int;
+  e.max_batch = ops.max_batch;
+  e.reserved = ops.max_batch > reserved ? reserved : 0;
+  e.root_slot = ops.max_batch - 1;
+  e.inc_slot = ops.max_batch - 2;
+  e.gen.assign(ops.max_batch, 0);
+  e.running.assign(ops.max_batch, nullptr);
+  for (int s = 0; s < ops.max_batch - e.reserved; ++s) e.free.push_back(s);
+}
+
+bool ops_complete(const nep_bnb_engine &o) {
+  return o.submit && o.advance && o.active && o.copy_state && o.set_params && o.get_flows && o.get_solutions &&
+         o.get_diag && o.n_int > 0 && o.max_batch > 0;
 }
 
 }  // namespace
@@ -196,7 +279,7 @@ int NepBnb::submit(std::vector<std::pair<Engine *, std::pair<int, NodeP>>> &item
   };
   std::vector<Group> groups;
   std::vector<std::pair<int, int>> copies[2];   // per engine (leaf first): (src, dst)
-  const double cutoff = std::min(inc, p.upper_bound);
+  const double cutoff = std::min(incv(), p.upper_bound);
   for (auto &it : items) {
     Engine *eng = it.first;
     const int slot = it.second.first;
@@ -244,7 +327,7 @@ int NepBnb::submit(std::vector<std::pair<Engine *, std::pair<int, NodeP>>> &item
       }
       const auto c = cps[k];
       cps.erase(cps.begin() + k);
-      int rc = nep_lp_copy_state(eng->lp, c.first, c.second);
+      int rc = eng->ops.copy_state(eng->ops.ctx, c.first, c.second);
       if (rc) return rc;
     }
   }
@@ -270,7 +353,7 @@ int NepBnb::submit(std::vector<std::pair<Engine *, std::pair<int, NodeP>>> &item
     o.gap_tol = (two && g.eng == &B) ? p.bound_gap : 0.0;
     o.bound_res = g.bres;
     sts.assign(n, 0);
-    int rc = nep_lp_submit(g.eng->lp, n, sl.data(), lbv.data(), ubv.data(), &o, sts.data());
+    int rc = g.eng->ops.submit(g.eng->ops.ctx, n, sl.data(), lbv.data(), ubv.data(), &o, sts.data());
     if (rc) return rc;
     for (int b = 0; b < n; ++b) {
       const int slot = sl[b];
@@ -471,7 +554,7 @@ int NepBnb::finish_one(Engine &eng, int slot, const NodeP &node, int status, dou
   st.lp_status_kind[node->kind][col] += 1;
   if (node->kind == REFROOT) {
     if (p.warm && status != NEP_LP_INFEASIBLE && status != NEP_LP_CUTOFF) {
-      int rc = nep_lp_copy_state(eng.lp, slot, eng.root_slot);
+      int rc = eng.ops.copy_state(eng.ops.ctx, slot, eng.root_slot);
       if (rc) return rc;
       eng.root_state = true;
     }
@@ -483,7 +566,7 @@ int NepBnb::finish_one(Engine &eng, int slot, const NodeP &node, int status, dou
   if (!eng.root_ready && node->depth == 0 && node->kind == NODE) {
     st.root_seconds = now_s() - t0;
     if (p.warm && status != NEP_LP_INFEASIBLE && status != NEP_LP_CUTOFF) {
-      int rc = nep_lp_copy_state(eng.lp, slot, eng.root_slot);
+      int rc = eng.ops.copy_state(eng.ops.ctx, slot, eng.root_slot);
       if (rc) return rc;
       eng.root_state = true;
     }
@@ -508,15 +591,15 @@ int NepBnb::finish_one(Engine &eng, int slot, const NodeP &node, int status, dou
     st.leaves += 1;
     bool kept = false;
     if (status == NEP_LP_OPTIMAL) {
-      if (po < inc - gap_abs(inc)) {
+      if (po < incv() - gap_abs(incv())) {
         inc = po;
         inc_source = 1;
         inc_node = node;
         inc_z.assign(eng.n_int, 0.0);
-        int rc = nep_lp_get_solution(eng.lp, slot, inc_z.data(), nullptr);
+        int rc = eng.ops.get_solutions(eng.ops.ctx, 1, &slot, inc_z.data());
         if (rc) return rc;
         if (p.warm) {
-          rc = nep_lp_copy_state(eng.lp, slot, eng.inc_slot);
+          rc = eng.ops.copy_state(eng.ops.ctx, slot, eng.inc_slot);
           if (rc) return rc;
           inc_slot = eng.inc_slot;
         } else {
@@ -526,14 +609,15 @@ int NepBnb::finish_one(Engine &eng, int slot, const NodeP &node, int status, dou
           kept = true;
         }
         st.lp_incumbents += 1;
-        set_cutoffs();
+        rc = set_cutoffs();
+        if (rc) return rc;
         if (inc_events) inc_queue.push_back(IncEvent{node, Parent{&eng, slot, eng.gen[slot]}, po});
       }
     } else if (node->kind == LEAF) {
       double pres = 0.0;
       if (std::isfinite(p.retry_res)) {
         double d[16];
-        int rc = nep_lp_get_diag(eng.lp, slot, d);
+        int rc = eng.ops.get_diag(eng.ops.ctx, slot, d);
         if (rc) return rc;
         pres = d[3];
       }
@@ -605,9 +689,9 @@ int NepBnb::finish_block(Engine &eng, int nd) {
   std::vector<float> fl(want.size() * FN);
   std::vector<double> zs(want.size() * ni);
   if (!want.empty()) {
-    int rc = nep_lp_get_flows(eng.lp, (int)want.size(), want.data(), fl.data());
+    int rc = eng.ops.get_flows(eng.ops.ctx, (int)want.size(), want.data(), fl.data());
     if (rc) return rc;
-    rc = nep_lp_get_solutions(eng.lp, (int)want.size(), want.data(), zs.data());
+    rc = eng.ops.get_solutions(eng.ops.ctx, (int)want.size(), want.data(), zs.data());
     if (rc) return rc;
   }
   // (copies: finish_one may submit nothing, but the outputs are reused by later advances)
@@ -631,8 +715,8 @@ int NepBnb::finish_block(Engine &eng, int nd) {
       // (the incumbent improved within this block: read it now)
       fl1.resize(FN);
       z1.resize(ni);
-      int rc = nep_lp_get_flows(eng.lp, 1, &slot, fl1.data());
-      if (!rc) rc = nep_lp_get_solution(eng.lp, slot, z1.data(), nullptr);
+      int rc = eng.ops.get_flows(eng.ops.ctx, 1, &slot, fl1.data());
+      if (!rc) rc = eng.ops.get_solutions(eng.ops.ctx, 1, &slot, z1.data());
       if (rc) return rc;
       f = fl1.data();
       z = z1.data();
@@ -650,14 +734,20 @@ int NepBnb::drain_and_close() {
     for (auto &n : engines[e]->running)
       if (n && n->kind != REFROOT) open.push_back(n->bound);
   st.drained = (int64_t)open.size();
-  for (int e = 0; e < n_engines(); ++e)
-    if (nep_lp_active(engines[e]->lp) > 0) nep_lp_set_params(engines[e]->lp, p.tol, -INF);
+  for (int e = 0; e < n_engines(); ++e) {
+    const nep_bnb_engine &o = engines[e]->ops;
+    if (o.active(o.ctx) > 0) {
+      const int rc = o.set_params(o.ctx, p.tol, -INF);
+      if (rc) return rc;
+    }
+  }
   for (int e = 0; e < n_engines(); ++e) {
     Engine &eng = *engines[e];
-    while (nep_lp_active(eng.lp) > 0) {
+    const nep_bnb_engine &o = eng.ops;
+    while (o.active(o.ctx) > 0) {
       int32_t nd = 0;
-      int rc = nep_lp_advance(eng.lp, nep_lp_active(eng.lp), &nd, done_slots.data(), obj.data(), pobj.data(),
-                              sts.data(), its.data());
+      int rc = o.advance(o.ctx, o.active(o.ctx), &nd, done_slots.data(), obj.data(), pobj.data(), sts.data(),
+                         its.data());
       if (rc) return rc;
       for (int i = 0; i < nd; ++i) {
         NodeP n = eng.running[done_slots[i]];
@@ -671,37 +761,115 @@ int NepBnb::drain_and_close() {
   for (auto &n : pending) open.push_back(n->bound);
   for (auto &n : retry) open.push_back(n->bound);
   for (double b : unresolved_bounds) open.push_back(b);
-  double bound = inc;
+  double bound = incv();
   for (double b : open) bound = std::min(bound, b);
   st.bound = bound;
   st.any_unresolved = unresolved_bounds.empty() ? 0 : 1;
   st.unresolved_below = 0;
   for (double b : unresolved_bounds)
-    if (b < inc - gap_abs(inc)) st.unresolved_below = 1;
+    if (b < incv() - gap_abs(incv())) st.unresolved_below = 1;
   st.limit_hit = limit_hit ? 1 : 0;
+  st.stalled = stalled ? 1 : 0;
   st.incumbent = inc;
+  st.agreed_incumbent = incv();
   st.incumbent_source = inc_source;
   st.incumbent_slot = inc_source == 1 ? inc_slot : -1;
   finished = true;
   return NEP_OK;
 }
 
+// the sharded search's split (bnb.py solve): the frontier — identical on every rank — in canonical order
+// (bound, -depth, seq), its crc32, then every rank keeps the open nodes whose position is its rank mod world
+void NepBnb::deal_frontier() {
+  std::vector<HeapItem> items;
+  while (!heap.empty()) {
+    items.push_back(heap.top());
+    heap.pop();
+  }
+  std::sort(items.begin(), items.end(), [](const HeapItem &a, const HeapItem &b) { return b > a; });
+  uint32_t h = 0;
+  for (const auto &it : items) {
+    const double bd[2] = {it.bound, (double)it.negdepth};
+    h = crc32_update(h, bd, sizeof bd);
+    std::vector<int64_t> ix(it.node->idx.begin(), it.node->idx.end());
+    h = crc32_update(h, ix.data(), ix.size() * sizeof(int64_t));
+    h = crc32_update(h, it.node->val.data(), it.node->val.size() * sizeof(double));
+  }
+  st.split_hash = h;
+  for (size_t i = 0; i < items.size(); ++i)
+    if ((int)(i % (size_t)p.world) == p.rank) heap.push(items[i]);
+  auto keep = [&](std::deque<NodeP> &q) {
+    std::deque<NodeP> out;
+    for (size_t i = 0; i < q.size(); ++i)
+      if ((int)(i % (size_t)p.world) == p.rank) out.push_back(q[i]);
+    q.swap(out);
+  };
+  keep(pending);
+  keep(retry);
+  st.presplit_nodes = st.nodes;
+  st.presplit_lps = st.lps;
+  st.presplit_certified = st.certified;
+  split = true;
+}
+
+// the k best-bound open nodes, taken off this rank's heap for another rank (bnb.py _rebalance's donor side)
+int NepBnb::export_nodes(int k, int32_t cap, int32_t *lens, double *meta, int32_t *idx, double *val) {
+  int32_t used = 0;
+  for (int q = 0; q < k; ++q) {
+    if (heap.empty()) return bad(NEP_ERR_ARG, "nep_bnb_export_nodes: fewer open nodes than asked for");
+    const NodeP n = heap.top().node;
+    const int32_t len = (int32_t)n->idx.size();
+    if (used + len > cap) return bad(NEP_ERR_ARG, "nep_bnb_export_nodes: idx / val capacity too small");
+    heap.pop();
+    lens[q] = len;
+    meta[3 * q] = n->bound;
+    meta[3 * q + 1] = n->depth;
+    meta[3 * q + 2] = n->kind;
+    std::copy(n->idx.begin(), n->idx.end(), idx + used);
+    std::copy(n->val.begin(), n->val.end(), val + used);
+    used += len;
+  }
+  return NEP_OK;
+}
+
 extern "C" {
 
-void *nep_bnb_create(void *leaf_model, void *bound_model, const nep_bnb_params *params, const double *fn_mem,
-                     const double *node_mem) {
-  if (!leaf_model || !params || !fn_mem || !node_mem) return nullptr;
+void *nep_bnb_create_engines(const nep_bnb_engine *leaf, const nep_bnb_engine *bound, const nep_bnb_params *params,
+                             const double *fn_mem, const double *node_mem) {
+  if (!leaf || !params || !fn_mem || !node_mem) {
+    bad(NEP_ERR_ARG, "nep_bnb_create: null argument");
+    return nullptr;
+  }
+  if (!ops_complete(*leaf) || (bound && !ops_complete(*bound))) {
+    bad(NEP_ERR_ARG, "nep_bnb_create: incomplete engine call table");
+    return nullptr;
+  }
+  const nep_bnb_params &q = *params;
+  if (q.batch < 1 || (bound && q.batch_b < 1) || q.F < 1 || q.N < 1 || q.c0 < 0 || q.c1 > leaf->n_int ||
+      (q.n0 >= 0 && q.n1 > leaf->n_int)) {
+    bad(NEP_ERR_ARG, "nep_bnb_create: bad batch / layout parameters");
+    return nullptr;
+  }
+  if (q.world < 1 || q.rank < 0 || q.rank >= q.world) {
+    bad(NEP_ERR_ARG, "nep_bnb_create: bad world / rank");
+    return nullptr;
+  }
   auto *t = new NepBnb();
   t->p = *params;
-  t->two = bound_model != nullptr;
+  t->two = bound != nullptr;
   t->fn_mem.assign(fn_mem, fn_mem + params->F);
   t->node_mem.assign(node_mem, node_mem + params->N);
-  init_engine(t->L, leaf_model, 2);   // (bnb.py: root and incumbent slots whenever max_batch >= 3)
+  init_engine(t->L, *leaf, 2);   // (bnb.py: root and incumbent slots whenever max_batch >= 3)
   t->engines[0] = &t->L;
   if (t->two) {
-    init_engine(t->B, bound_model, t->p.warm ? 1 : 0);
+    init_engine(t->B, *bound, t->p.warm ? 1 : 0);
     t->engines[0] = &t->B;   // (bnb.py's engine order: bound model first)
     t->engines[1] = &t->L;
+  }
+  if (t->L.free.empty() || (t->two && t->B.free.empty())) {
+    delete t;
+    bad(NEP_ERR_ARG, "nep_bnb_create: no working slot left after the reserved ones (max_batch too small)");
+    return nullptr;
   }
   const int mb = std::max(t->L.max_batch, t->two ? t->B.max_batch : 0);
   t->done_slots.assign(mb, 0);
@@ -728,11 +896,25 @@ void *nep_bnb_create(void *leaf_model, void *bound_model, const nep_bnb_params *
   return t;
 }
 
+void *nep_bnb_create(void *leaf_model, void *bound_model, const nep_bnb_params *params, const double *fn_mem,
+                     const double *node_mem) {
+  if (!leaf_model) {
+    bad(NEP_ERR_ARG, "nep_bnb_create: null leaf model");
+    return nullptr;
+  }
+  nep_bnb_engine le{}, be{};
+  if (model_ops(leaf_model, &le)) return nullptr;   // (nep_model_get_info set the message)
+  if (bound_model && model_ops(bound_model, &be)) return nullptr;
+  return nep_bnb_create_engines(&le, bound_model ? &be : nullptr, params, fn_mem, node_mem);
+}
+
 void nep_bnb_destroy(void *tree) { delete static_cast<NepBnb *>(tree); }
 
 int nep_bnb_add_leaf(void *tree, int32_t n, const int32_t *idx, const double *val, double bound, int32_t where) {
   auto *t = static_cast<NepBnb *>(tree);
-  if (!t || n < 0 || (n > 0 && (!idx || !val))) return NEP_ERR_ARG;
+  if (!t || n < 0 || (n > 0 && (!idx || !val))) return bad(NEP_ERR_ARG, "nep_bnb_add_leaf: bad argument");
+  for (int32_t q = 0; q < n; ++q)
+    if (idx[q] < 0 || idx[q] >= t->L.n_int) return bad(NEP_ERR_ARG, "nep_bnb_add_leaf: index out of range");
   auto leaf = std::make_shared<Node>();
   leaf->idx.assign(idx, idx + n);
   leaf->val.assign(val, val + n);
@@ -762,7 +944,7 @@ int nep_bnb_add_leaf(void *tree, int32_t n, const int32_t *idx, const double *va
 
 int nep_bnb_set_step2(void *tree, int32_t create, double node_cap, const double *old_alloc, int32_t incumbent_events) {
   auto *t = static_cast<NepBnb *>(tree);
-  if (!t || !old_alloc || t->started) return NEP_ERR_ARG;
+  if (!t || !old_alloc || t->started) return bad(NEP_ERR_ARG, "nep_bnb_set_step2: bad argument or search started");
   const size_t FN = (size_t)t->p.F * t->p.N;
   t->s2 = true;
   t->s2_create = create != 0;
@@ -785,7 +967,8 @@ int nep_bnb_set_step2(void *tree, int32_t create, double node_cap, const double 
 
 int nep_bnb_debug_ibound(const nep_bnb_params *params, int32_t create, double node_cap, const double *old_alloc,
                          int32_t n, const int32_t *idx, const double *val, double *out) {
-  if (!params || !old_alloc || !out || n < 0 || (n > 0 && (!idx || !val))) return NEP_ERR_ARG;
+  if (!params || !old_alloc || !out || n < 0 || (n > 0 && (!idx || !val)))
+    return bad(NEP_ERR_ARG, "nep_bnb_debug_ibound: bad argument");
   const size_t FN = (size_t)params->F * params->N;
   std::vector<char> old(FN);
   for (size_t k = 0; k < FN; ++k) old[k] = old_alloc[k] > 0.5;
@@ -796,7 +979,7 @@ int nep_bnb_debug_ibound(const nep_bnb_params *params, int32_t create, double no
 
 int nep_bnb_incumbent_event(void *tree, int32_t *n_fix, int32_t *idx, double *val, double *value) {
   auto *t = static_cast<NepBnb *>(tree);
-  if (!t || !t->cur_inc.node) return NEP_ERR_STATE;
+  if (!t || !t->cur_inc.node) return bad(NEP_ERR_STATE, "nep_bnb_incumbent_event: no incumbent event");
   const Node &nd = *t->cur_inc.node;
   if (n_fix) *n_fix = (int32_t)nd.idx.size();
   if (idx) std::memcpy(idx, nd.idx.data(), nd.idx.size() * sizeof(int32_t));
@@ -807,7 +990,7 @@ int nep_bnb_incumbent_event(void *tree, int32_t *n_fix, int32_t *idx, double *va
 
 int nep_bnb_set_incumbent(void *tree, double value) {
   auto *t = static_cast<NepBnb *>(tree);
-  if (!t) return NEP_ERR_ARG;
+  if (!t) return bad(NEP_ERR_ARG, "nep_bnb_set_incumbent: null tree");
   if (!(value < t->inc)) return NEP_OK;
   t->inc = value;
   t->inc_source = 2;
@@ -818,13 +1001,12 @@ int nep_bnb_set_incumbent(void *tree, double value) {
   t->inc_slot = -1;
   t->inc_node = nullptr;
   t->st.heuristic_incumbents += 1;
-  t->set_cutoffs();
-  return NEP_OK;
+  return t->set_cutoffs();
 }
 
 int nep_bnb_event_data(void *tree, double *z, float *flow) {
   auto *t = static_cast<NepBnb *>(tree);
-  if (!t || t->ev_z.empty()) return NEP_ERR_STATE;
+  if (!t || t->ev_z.empty()) return bad(NEP_ERR_STATE, "nep_bnb_event_data: no root event");
   if (z) std::memcpy(z, t->ev_z.data(), t->ev_z.size() * sizeof(double));
   if (flow) std::memcpy(flow, t->ev_flow.data(), t->ev_flow.size() * sizeof(float));
   return NEP_OK;
@@ -832,7 +1014,7 @@ int nep_bnb_event_data(void *tree, double *z, float *flow) {
 
 int nep_bnb_run(void *tree, int32_t *event) {
   auto *t = static_cast<NepBnb *>(tree);
-  if (!t || !event) return NEP_ERR_ARG;
+  if (!t || !event) return bad(NEP_ERR_ARG, "nep_bnb_run: null argument");
   *event = NEP_BNB_DONE;
   if (t->finished) return NEP_OK;
   if (!t->started) {
@@ -854,13 +1036,30 @@ int nep_bnb_run(void *tree, int32_t *event) {
       *event = NEP_BNB_ROOT;
       return NEP_OK;
     }
-    const bool stop = T.st.nodes >= T.p.node_limit ||
-                      (T.p.time_limit > 0 && now_s() - T.t0 > T.p.time_limit);
+    const bool sharded = T.p.world > 1;
+    if (sharded && !T.split && T.heap.size() >= (size_t)T.p.world * (size_t)T.p.batch && L.inflight == 0 &&
+        (!T.two || B.inflight == 0))
+      T.deal_frontier();   // the frontier every rank holds identically, dealt once
+    bool stop = T.stalled || T.st.nodes >= T.p.node_limit ||
+                (T.p.time_limit > 0 && now_s() - T.t0 > T.p.time_limit);
     int busy = 0;
     for (int e = 0; e < T.n_engines(); ++e)
       for (auto &n : T.engines[e]->running)
         if (n && n->kind != REFROOT) ++busy;
-    const size_t open_n = T.heap.size() + T.pending.size() + T.retry.size() + busy;
+    int64_t open_n = (int64_t)(T.heap.size() + T.pending.size() + T.retry.size()) + busy;
+    if (sharded) {
+      // one collective per loop, run by the caller: incumbent MIN, stop OR, open + in-flight SUM
+      if (!T.sync_answered) {
+        const double out[6] = {T.incv(), stop ? 1.0 : 0.0, (double)open_n, (double)T.heap.size(),
+                               T.split ? 1.0 : 0.0, (double)T.st.sync_calls};
+        std::copy(out, out + 6, T.sync_out);
+        *event = NEP_BNB_SYNC;
+        return NEP_OK;
+      }
+      T.sync_answered = false;
+      stop = T.agreed_stop;
+      if (T.split) open_n = T.agreed_open;   // (before the split every rank holds the same open nodes)
+    }
     if (open_n == 0) break;
     if (stop) {
       T.limit_hit = true;
@@ -938,16 +1137,23 @@ int nep_bnb_run(void *tree, int32_t *event) {
     T.st.submit_seconds += t2 - t1;
     int inflight = 0;
     for (int e = 0; e < T.n_engines(); ++e) inflight += T.engines[e]->inflight;
-    if (inflight == 0) continue;
+    if (inflight == 0) {
+      // nothing iterates: either this rank's part of a sharded frontier is empty (the others still work), or
+      // open nodes wait for a slot that never frees (round-5 ADVICE: e.g. warm starts off with one working slot
+      // kept for the incumbent) — end the search as a limit instead of looping forever
+      if (items.empty() && T.heap.size() + T.pending.size() + T.retry.size() > 0) T.stalled = true;
+      continue;
+    }
     T.st.advance_calls += 1;
     T.st.inflight_sum += busy;
     for (int e = 0; e < T.n_engines(); ++e) {
       Engine &eng = *T.engines[e];
       if (eng.inflight <= 0) continue;
-      const int min_done = T.two ? 0 : (T.p.time_limit > 0 ? 0 : 1);
+      // before the split every rank must stay identical: drain each batch whole
+      const int min_done = (sharded && !T.split) ? eng.inflight : (T.two ? 0 : (T.p.time_limit > 0 ? 0 : 1));
       int32_t nd = 0;
-      int rc = nep_lp_advance(eng.lp, min_done, &nd, T.done_slots.data(), T.obj.data(), T.pobj.data(),
-                              T.sts.data(), T.its.data());
+      int rc = eng.ops.advance(eng.ops.ctx, min_done, &nd, T.done_slots.data(), T.obj.data(), T.pobj.data(),
+                               T.sts.data(), T.its.data());
       if (rc) return rc;
       const double t3 = now_s();
       T.st.advance_seconds += t3 - t2;
@@ -963,9 +1169,63 @@ int nep_bnb_run(void *tree, int32_t *event) {
   return NEP_OK;
 }
 
+int nep_bnb_sync_get(void *tree, double *out6) {
+  auto *t = static_cast<NepBnb *>(tree);
+  if (!t || !out6) return bad(NEP_ERR_ARG, "nep_bnb_sync_get: null argument");
+  std::copy(t->sync_out, t->sync_out + 6, out6);
+  return NEP_OK;
+}
+
+int nep_bnb_sync_set(void *tree, double incumbent, int32_t stop, int64_t open_total) {
+  auto *t = static_cast<NepBnb *>(tree);
+  if (!t) return bad(NEP_ERR_ARG, "nep_bnb_sync_set: null tree");
+  t->sync_answered = true;
+  t->agreed_stop = stop != 0;
+  t->agreed_open = open_total;
+  t->st.sync_calls += 1;
+  if (incumbent < t->cut) {
+    const double before = t->incv();
+    t->cut = incumbent;
+    if (t->incv() < before) return t->set_cutoffs();
+  }
+  return NEP_OK;
+}
+
+int nep_bnb_export_nodes(void *tree, int32_t k, int32_t cap, int32_t *lens, double *meta, int32_t *idx, double *val) {
+  auto *t = static_cast<NepBnb *>(tree);
+  if (!t || k < 0 || (k > 0 && (!lens || !meta || (cap > 0 && (!idx || !val)))))
+    return bad(NEP_ERR_ARG, "nep_bnb_export_nodes: bad argument");
+  return t->export_nodes(k, cap, lens, meta, idx, val);
+}
+
+int nep_bnb_import_nodes(void *tree, int32_t k, const int32_t *lens, const double *meta, const int32_t *idx,
+                         const double *val) {
+  auto *t = static_cast<NepBnb *>(tree);
+  if (!t || k < 0 || (k > 0 && (!lens || !meta))) return bad(NEP_ERR_ARG, "nep_bnb_import_nodes: bad argument");
+  int64_t o = 0;
+  for (int q = 0; q < k; ++q) {
+    if (lens[q] < 0 || (lens[q] > 0 && (!idx || !val))) return bad(NEP_ERR_ARG, "nep_bnb_import_nodes: bad node");
+    auto n = std::make_shared<Node>();
+    n->idx.assign(idx + o, idx + o + lens[q]);
+    n->val.assign(val + o, val + o + lens[q]);
+    o += lens[q];
+    for (int32_t i : n->idx)
+      if (i < 0 || i >= t->L.n_int) return bad(NEP_ERR_ARG, "nep_bnb_import_nodes: index out of range");
+    n->bound = meta[3 * q];
+    n->depth = (int)meta[3 * q + 1];
+    n->kind = (int)meta[3 * q + 2];
+    // (no parent state on this rank: the node starts from its model's root state)
+    if (!t->pruned(n->bound)) {
+      t->push_heap(n);
+      t->st.rebalanced += 1;
+    }
+  }
+  return NEP_OK;
+}
+
 int nep_bnb_get_stats(void *tree, nep_bnb_stats *out) {
   auto *t = static_cast<NepBnb *>(tree);
-  if (!t || !out) return NEP_ERR_ARG;
+  if (!t || !out) return bad(NEP_ERR_ARG, "nep_bnb_get_stats: null argument");
   *out = t->st;
   out->n_lp_iters = (int64_t)t->lp_iters.size();
   return NEP_OK;
@@ -973,14 +1233,14 @@ int nep_bnb_get_stats(void *tree, nep_bnb_stats *out) {
 
 int nep_bnb_get_lp_iters(void *tree, int64_t *out) {
   auto *t = static_cast<NepBnb *>(tree);
-  if (!t || !out) return NEP_ERR_ARG;
+  if (!t || !out) return bad(NEP_ERR_ARG, "nep_bnb_get_lp_iters: null argument");
   if (!t->lp_iters.empty()) std::memcpy(out, t->lp_iters.data(), t->lp_iters.size() * sizeof(int64_t));
   return NEP_OK;
 }
 
 int nep_bnb_incumbent(void *tree, double *z, int32_t *n_fix, int32_t *idx, double *val) {
   auto *t = static_cast<NepBnb *>(tree);
-  if (!t) return NEP_ERR_ARG;
+  if (!t) return bad(NEP_ERR_ARG, "nep_bnb_incumbent: null tree");
   if (t->inc_source != 1 || !t->inc_node) {
     if (n_fix) *n_fix = -1;
     return NEP_OK;

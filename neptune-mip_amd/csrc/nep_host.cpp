@@ -23,11 +23,6 @@
 #include "../../include/neptune_lp.h"
 #include "nep_internal.h"
 
-#include <csignal>
-#include <dlfcn.h>
-#include <execinfo.h>
-#include <unistd.h>
-
 namespace nep {
 hipError_t launch_x_pass(const DeviceView &v, const int32_t *slots, int nslots, bool check, bool init, bool first,
                          bool plain, int it, hipStream_t s);
@@ -63,6 +58,9 @@ static thread_local std::string g_err;
 static int fail(int code, const std::string &msg) {
   g_err = msg;
   return code;
+}
+namespace nep {
+int set_error(int code, const char *msg) { return fail(code, msg ? msg : ""); }   // (nep_bnb.cpp's messages)
 }
 #define HIPCHK(expr)                                                                         \
   do {                                                                                       \
@@ -1858,53 +1856,6 @@ extern "C" {
 int nep_api_version(void) { return NEP_API_VERSION; }
 const char *nep_last_error(void) { return g_err.c_str(); }
 
-// NEP_SEGV_TRACE=1 (debug aid, DESIGN.md §6 "PMC pass crash"): a SIGSEGV handler that prints every frame's
-// library and nearest exported symbol (dladdr) and the memory mappings around the faulting address, then
-// re-raises with the previous disposition.  Installed at the first model creation.
-static struct sigaction g_prev_segv;
-static void segv_trace(int sig, siginfo_t *si, void *ctx) {
-  void *fr[64];
-  const int n = backtrace(fr, 64);
-  char line[512];
-  int len = snprintf(line, sizeof line, "[nep] SIGSEGV at %p, %d frames\n", si ? si->si_addr : nullptr, n);
-  (void)!write(2, line, len);
-  for (int k = 0; k < n; ++k) {
-    Dl_info di{};
-    if (dladdr(fr[k], &di) && di.dli_fname) {
-      len = snprintf(line, sizeof line, "[nep]  #%d %p %s+0x%lx (%s+0x%lx)\n", k, fr[k], di.dli_fname,
-                     (unsigned long)((char *)fr[k] - (char *)di.dli_fbase), di.dli_sname ? di.dli_sname : "?",
-                     di.dli_saddr ? (unsigned long)((char *)fr[k] - (char *)di.dli_saddr) : 0ul);
-    } else {
-      len = snprintf(line, sizeof line, "[nep]  #%d %p ?\n", k, fr[k]);
-    }
-    (void)!write(2, line, len);
-  }
-  if (FILE *f = std::fopen("/proc/self/maps", "r")) {
-    const unsigned long a = (unsigned long)(si ? si->si_addr : nullptr);
-    char ml[512];
-    while (std::fgets(ml, sizeof ml, f)) {
-      unsigned long lo = 0, hi = 0;
-      if (std::sscanf(ml, "%lx-%lx", &lo, &hi) == 2 && hi + (1ul << 22) > a && lo < a + (1ul << 22))
-        (void)!write(2, ml, std::strlen(ml));
-    }
-    std::fclose(f);
-  }
-  sigaction(SIGSEGV, &g_prev_segv, nullptr);
-  raise(sig);
-  (void)ctx;
-}
-static void maybe_install_segv_trace() {
-  static bool done = false;
-  const char *e = std::getenv("NEP_SEGV_TRACE");
-  if (done || !e || std::atoi(e) == 0) return;
-  done = true;
-  struct sigaction sa{};
-  sa.sa_sigaction = segv_trace;
-  sa.sa_flags = SA_SIGINFO;
-  sigemptyset(&sa.sa_mask);
-  sigaction(SIGSEGV, &sa, &g_prev_segv);
-}
-
 // API 9: a descriptor whose arrays are device memory (nep_model_desc.device_inputs), staged to the host: the
 // build's aggregation, coefficients, presolve base box and scaling read the O(F N + N^2) instance there
 struct HostDesc {
@@ -1938,7 +1889,6 @@ static int stage_device_desc(const nep_model_desc &in, HostDesc &h) {
 
 int nep_model_create(const nep_model_desc *desc_in, int32_t max_batch, void *hip_stream, void **out_model) {
   if (!desc_in || !out_model) return fail(NEP_ERR_ARG, "null argument");
-  maybe_install_segv_trace();
   HostDesc staged;
   const nep_model_desc *desc = desc_in;
   if (desc_in->device_inputs) {

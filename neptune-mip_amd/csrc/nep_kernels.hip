@@ -442,18 +442,32 @@ void x_pass(DeviceView v, const int32_t *__restrict__ slots, int plain, int it, 
       // stored row — the certificate's point — sums to 1 within the fp32 rounding of its entries (C4,
       // constraints_step1.py:27-34).  An fp32 threshold over ~N active entries leaves |sum - 1| ~ N ulps: 1.2e-5
       // on the pooled rows of the Alibaba-shape 1024x512 models (W == 0: one row of 1024 entries per function)
-      double s64 = 0.0;
-      int c64 = 0;
+      // Michelot passes in fp64 from the fp32 support until the support {v > th} is stable (round-5 ADVICE:
+      // applying th64 to every masked entry moved entries across the fp32 support's edge); the final threshold
+      // is always the one computed from the final support, whose entries outside stay 0
+      double th64 = (double)theta;
+      uint32_t sup = 0xffffffffu;
+#pragma unroll 1
+      for (int it = 0; it < 4; ++it) {
+        double s64 = 0.0;
+        int c64 = 0;
+        uint32_t ns = 0;
 #pragma unroll
-      for (int e = 0; e < E; ++e) {
-        const bool in = ((mbits >> e) & 1u) && vv[e] > theta;
-        if (in) s64 += (double)vv[e];
-        c64 += __popcll(__ballot(in));
+        for (int e = 0; e < E; ++e) {
+          const bool in = ((mbits >> e) & 1u) && (double)vv[e] > th64;
+          if (in) {
+            s64 += (double)vv[e];
+            ns |= 1u << e;
+          }
+          c64 += __popcll(__ballot(in));
+        }
+        if (__ballot(ns != sup) == 0) break;
+        sup = ns;
+        s64 = wave_sum_d(s64);
+        if (c64 > 0) th64 = (s64 - 1.0) / (double)c64;
       }
-      s64 = wave_sum_d(s64);
-      const double th64 = c64 > 0 ? (s64 - 1.0) / (double)c64 : (double)theta;
 #pragma unroll
-      for (int e = 0; e < E; ++e) xn[e] = ((mbits >> e) & 1u) ? fmaxf((float)((double)vv[e] - th64), 0.f) : 0.f;
+      for (int e = 0; e < E; ++e) xn[e] = ((sup >> e) & 1u) ? fmaxf((float)((double)vv[e] - th64), 0.f) : 0.f;
     } else {
 #pragma unroll
       for (int e = 0; e < E; ++e) xn[e] = ((mbits >> e) & 1u) ? fmaxf(vv[e] - theta, 0.f) : 0.f;

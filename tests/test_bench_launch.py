@@ -18,7 +18,7 @@ def _run(args, env_extra, timeout=240):
                           capture_output=True, text=True, timeout=timeout)
 
 
-def test_gpus_2_launches_two_ranks_with_the_replay_split():
+def test_gpus_2_launches_two_ranks_one_instance_each():
     r = _run(["--gpus", "2"], {"NEP_BENCH_PROBE_RANKS": "6"})
     assert r.returncode == 0, r.stderr[-2000:]
     line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1]
@@ -26,11 +26,12 @@ def test_gpus_2_launches_two_ranks_with_the_replay_split():
     assert out["n_gpus"] == 2
     ranks = sorted(out["ranks"], key=lambda d: d["rank"])
     assert [d["rank"] for d in ranks] == [0, 1] and all(d["world"] == 2 for d in ranks)
-    with gzip.open(os.path.join(REPO, "tests", "golden", "bnb_trace_512x256_s0.json.gz"), "rt") as fh:
-        lps = [e for e in json.load(fh)["lps"] if e["parent"] is not None]
-    for d in ranks:        # rank r replays entries r, r + world, r + 2 world, ...
-        assert d["ids"] == [lps[d["rank"] + 2 * q]["id"] for q in range(6)]
-    assert not set(ranks[0]["ids"]) & set(ranks[1]["ids"])
+    for d in ranks:        # rank r replays the whole recorded trace of instance seed r (one B&B per GPU)
+        assert d["seed"] == d["rank"]
+        with gzip.open(os.path.join(REPO, "tests", "golden", f"bnb_trace_512x256_s{d['seed']}.json.gz"), "rt") as fh:
+            lps = [e for e in json.load(fh)["lps"] if e["parent"] is not None]
+        assert d["entries"] == len(lps)
+        assert d["ids"] == [lps[q]["id"] for q in range(6)]
 
 
 def test_launcher_world_must_match_gpus():

@@ -68,6 +68,11 @@ def test_product_bnb_time_limited(n, f, seconds):
     assert res.status != INFEASIBLE and res.objective is not None, res.as_dict()
     assert res.certified > 0 and res.nodes > 0
     assert res.bound <= res.objective + 1e-9
+    if n >= 512:
+        # config 4's product search (facility-relaxation bounds): a proven gap, not only an incumbent (round-5
+        # VERDICT; the bench's 60 s figure is 2.5 %)
+        rel = (res.objective - res.bound) / max(1.0, abs(res.objective))
+        assert rel <= 0.05, (rel, res.as_dict())
     x, z = np.asarray(res.x, np.float64), np.asarray(res.z, np.float64)
     c = z[:f * n].reshape(f, n)
     assert np.all((np.abs(c) < 1e-9) | (np.abs(c - 1) < 1e-9)), "incumbent c not integral"

@@ -1,6 +1,7 @@
 """The sharded branch-and-bound on the MI355X engine: world size 2 over gloo,
 both ranks on cuda:0 with the real LPModels (the reference model for leaves, the facility relaxation for the
-branching nodes).  Before the split every rank runs the same search, so the frontier each deals must be
+branching nodes).  The search runs on the native tree (csrc/nep_bnb.cpp, NEP_BNB_SYNC
+events for the per-loop collective).  Before the split every rank runs the same search, so the frontier each deals must be
 bitwise identical (crc32 of its bounds and fixings); after it the ranks search their subtrees, exchange the
 incumbent every loop, rebalance open nodes and end with the owner's objective, placement and routing.
 Multi-GPU throughput stays unmeasured on hardware until the driver's SCALE run."""
@@ -54,7 +55,7 @@ def _worker(rank, world, port, case, out):
                              rebalance_every=4).solve()
         x = None if res.x is None else np.asarray(res.x).round(12).tolist()
         out[rank] = (res.status, res.objective, None if res.z is None else np.asarray(res.z).tolist(), x,
-                     res.split_hash, res.rebalanced, res.nodes)
+                     res.split_hash, res.rebalanced, res.nodes, res.native)
     finally:
         m.close()
         bm.close()
@@ -73,7 +74,8 @@ def _run(case):
 def test_gpu_sharded_bnb_reaches_recorded_mip(name):
     rec = G[name]["models"][0]
     res = _run(("golden", name, None))
-    st0, obj0, z0, x0, h0, _, _ = res[0]
+    st0, obj0, z0, x0, h0, _, _, native = res[0]
+    assert native, "the sharded search ran the Python loop, not the native tree (API 12)"
     for r in range(2):
         assert res[r][:3] == (st0, obj0, z0) and res[r][3] == x0, (r, res[r][:2], (st0, obj0))
         assert res[r][4] == h0, "the ranks dealt different frontiers"
@@ -84,8 +86,9 @@ def test_gpu_sharded_bnb_reaches_recorded_mip(name):
 def test_gpu_sharded_bnb_64x32_time_limited():
     """BASELINE config 2's instance, 10 s: identical frontiers at the split, the same result on both ranks."""
     res = _run(("synthetic", (64, 32), 10.0))
-    st0, obj0, z0, x0, h0, _, _ = res[0]
+    st0, obj0, z0, x0, h0, _, _, native = res[0]
     print({r: (res[r][0], res[r][1], res[r][4], res[r][5], res[r][6]) for r in range(2)})
+    assert native
     assert h0 is not None
     for r in range(2):
         assert res[r][:3] == (st0, obj0, z0) and res[r][3] == x0

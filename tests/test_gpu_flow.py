@@ -97,9 +97,12 @@ def test_neptune_mdu_flow_synthetic_generator(n, f, seconds):
     from core.utils.synthetic import synthetic_payload
     data, alpha, solver, solved, alloc, score = _flow(synthetic_payload(n, f, seed=0), seconds)
     _check_step1(data, alpha, solver, score)
-    for r in (solver.step2_delete.result, solver.step2_create.result):
-        if r is not None and r.objective is not None:
-            pytest.skip("step 2 found a placement on this instance")    # (then the end-to-end test applies)
+    # both step-2 modes PROVEN infeasible (round-5 VERDICT: a time-limited LIMIT passed the same as a proof): the
+    # reference falls back from delete to create and then returns step 1's placement (neptune.py:24-39)
+    st = {m_: getattr(r, "status", None) for m_, r in (("delete", solver.step2_delete.result),
+                                                        ("create", solver.step2_create.result))}
+    print(f"{n}x{f} step 2:", st)
+    assert st == {"delete": "INFEASIBLE", "create": "INFEASIBLE"}, st
     assert not solved and score["step2"] == 0.0
     got = {(fn, nd) for fn, d in alloc.items() for nd in d}
     assert got == _alloc_set(data, solver.step1.result.z, f, n)
