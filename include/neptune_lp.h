@@ -290,6 +290,8 @@ typedef struct {
   int64_t node_limit;
   double time_limit;               /* seconds (<= 0: none) */
   int32_t world, rank;             /* API 12: the sharded search (world > 1: NEP_BNB_SYNC once per loop) */
+  int32_t branching;               /* API 12: 0 n by inflow, then c by flow; 1 pseudo-cost (product score) */
+  int32_t reserved_p;
 } nep_bnb_params;
 
 typedef struct {

@@ -158,7 +158,7 @@ class BranchAndBound:
                  retry_res=math.inf, unit_flow_leaves=True, node_max_iters=None, bound_lp=None, bound_gap=1e-4,
                  trace=None, rebalance_every=8, primal=None, primal_every=0,
                  leaf_routing_warm=False, root_check_every=64, objective_integral=False, warm_weight_ref=0.0,
-                 native=None, step2_native=None):
+                 native=None, step2_native=None, branching=0):
         self.lp = lp
         self.two = bound_lp is not None
         self.N, self.F = lp.N, lp.F
@@ -218,6 +218,9 @@ class BranchAndBound:
         # (create, node_cap, old allocation [F*N]): integer_bound is step 2's closed form, which the native tree
         # evaluates itself (NeptuneStep2Base.native_bound); improve then runs on NEP_BNB_INCUMBENT events
         self.step2_native = step2_native
+        # branching rule of the native tree: 0 = n by largest inflow, then c by largest flow (this module's loop);
+        # 1 = pseudo-cost branching (product score over fractional n / c, csrc/nep_bnb.cpp branch_var_pc)
+        self.branching = int(branching)
         # (the leaf / reference model only — the model whose node LPs the replay measured; the facility relaxation
         # keeps the parent-relative band: 256x128 / 20 s gap 0.51 % with it, 0.82 % with the band on both)
         for m_ in (lp,):
@@ -752,6 +755,7 @@ class BranchAndBound:
         s2 = self.step2_native is not None and os.environ.get("NEP_BNB_STEP2", STEP2_NATIVE_DEFAULT) not in ("", "0")
         engine = hasattr(self.lp, "_h") and (self.bound_lp is None or hasattr(self.bound_lp, "_h"))
         eligible = (self.trace is None and (self.integer_bound is None or s2) and (self.improve is None or s2)
+                    and (self.branching == 0 or self.native is not False)
                     and not self.leaf_routing_warm and self.primal_every == 0 and (engine or self.native is True))
         if comm.world > 1 and os.environ.get("NEP_BNB_SHARDED_NATIVE", "1") in ("", "0"):
             eligible = False
@@ -825,7 +829,7 @@ class BranchAndBound:
                       retry_res=float(self.retry_res), flow_tol=float(self.flow_tol), upper_bound=float(self.ub0),
                       # (round-5 ADVICE: a non-finite node limit is no limit)
                       node_limit=int(min(float(self.node_limit), 2.0 ** 62)), time_limit=float(self.time_limit or 0.0),
-                      world=int(comm.world), rank=int(comm.rank))
+                      world=int(comm.world), rank=int(comm.rank), branching=self.branching)
         py_engines = []
         if hasattr(lp, "_h"):
             tree = lib.nep_bnb_create(lp._h, self.bound_lp._h if self.two else None, ctypes.byref(p),

@@ -70,7 +70,8 @@ class BnbParams(ctypes.Structure):
                 ("root_max_iters", ctypes.c_int64), ("node_bound_res", ctypes.c_double),
                 ("retry_res", ctypes.c_double), ("flow_tol", ctypes.c_double), ("upper_bound", ctypes.c_double),
                 ("node_limit", ctypes.c_int64), ("time_limit", ctypes.c_double),
-                ("world", ctypes.c_int32), ("rank", ctypes.c_int32)]
+                ("world", ctypes.c_int32), ("rank", ctypes.c_int32), ("branching", ctypes.c_int32),
+                ("reserved_p", ctypes.c_int32)]
 
 
 class BnbStats(ctypes.Structure):
@@ -280,7 +281,7 @@ def load_library(path=None):
     lib.nep_last_error.restype = ctypes.c_char_p
     lib.nep_api_version.restype = ctypes.c_int
     # array arguments travel as plain addresses (_ptr: the array's data pointer as an int): ctypes' typed
-    # pointer casts cost ~2 us each, ~10 % of the B&B's host time at 64x32 (tools/bnb_profile.py)
+    # pointer casts cost ~2 us each, ~10 % of the B&B's host time at 64x32 (tools/probes/bnb_profile.py)
     scalar_ptrs = tuple(ctypes.POINTER(t) for t in (ctypes.c_double, ctypes.c_float, ctypes.c_int32, ctypes.c_int64))
     for name in EXPORTS:
         fn = getattr(lib, name)

@@ -504,7 +504,41 @@ class NeptuneStep2Base(NeptuneStepBase):
         ms = float(getattr(d, "max_score", 0.0) or 0.0) * self.soften_step1_sol
         if self.VARIANT == "MinUtilization":
             return ms
+        if self.score_row_lower_bound() > ms * (1 + 1e-9) + 1e-9:
+            return -1.0          # no integral placement meets the score row: every box's integer bound is +inf
         return ms * len(d.nodes) / self.alpha if self.alpha > 0 else math.inf
+
+    def score_row_lower_bound(self):
+        """A lower bound on the MinDelayAndUtilization score row (constraints_step2.py:76-88)
+        alpha / N sum n + sum (1 - alpha) W[f,i] D[i,j] / MD[i,f] x[i,f,j] over every INTEGRAL placement of this
+        step (MD[i,f] = max(maxdelay[f], max_k D[k,i]), :77-81).  A loaded source i of f routes at no delay only to
+        j = i (D[i,i] = 0), which needs c[f,i] = 1 (C1); any other destination costs at least g[f,i] = (1 - alpha)
+        W[f,i] dmin[i] / MD[i,f], dmin[i] = min_{j != i} D[i,j].  With k open nodes at most the pairs of k nodes are
+        local, and in delete mode (D4, sum c <= sum old) at most sum old pairs: so
+          score >= min_k  alpha k / N + sum g - min(top_k(node sums of g), top_{sum old}(g))   (k >= 1).
+        +0 when it proves nothing.  On the SURVEY §8(d) generator the bound exceeds 1.3 x the step-1 score at every
+        size (64x32: 0.477 create / 7.55 delete against 0.177), so both step-2 modes are proven infeasible before any
+        LP — the reference's SCIP returns INFEASIBLE for the same models (neptune.py:24-39 then keeps step 1)."""
+        if self.VARIANT != "MinDelayAndUtilization":
+            return 0.0
+        d = self.data
+        W = np.asarray(d.workload_matrix, np.float64)
+        if not W.any():
+            return 0.0
+        D = np.asarray(d.node_delay_matrix, np.float64)
+        F, N = W.shape
+        md = np.maximum(np.asarray(d.max_delay_matrix, np.float64)[None, :], D.max(axis=0)[:, None])   # [i, f]
+        off = D + np.diag(np.full(N, np.inf))
+        dmin = off.min(axis=1) if N > 1 else np.zeros(N)
+        g = (1 - self.alpha) * W * dmin[None, :] / md.T                                                  # [f, i]
+        tot = float(g.sum())
+        cum = np.concatenate([[0.0], np.cumsum(np.sort(g.sum(axis=0))[::-1])])
+        k = np.arange(1, N + 1)
+        local = cum[k]
+        if self.mode == "delete":
+            O = int(round(float((np.asarray(d.old_allocations_matrix, np.float64) > 0.5).sum())))
+            local = np.minimum(local, float(np.sort(g.ravel())[::-1][:O].sum()))
+        return max(0.0, float(np.min(self.alpha / N * k + tot - local)))
 
     def native_bound(self):
         """(create, node cap, old allocation): integer_bound below, evaluated by the native tree

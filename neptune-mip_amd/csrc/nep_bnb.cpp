@@ -68,6 +68,10 @@ struct Node {
   int kind;
   Parent parent;
   int depth;
+  // the branching that made this node (pseudo-costs): variable, direction (1 = up), the parent LP's distance to
+  // the fixed value, the parent's bound
+  int bvar = -1, bdir = 0;
+  double bfrac = 0.0, pbound = -std::numeric_limits<double>::infinity();
 };
 using NodeP = std::shared_ptr<Node>;
 
@@ -243,6 +247,14 @@ struct NepBnb {
                  const float *flow, const double *z);
   void round_all(const Node &node, const float *flow, const double *z, double bound, const Parent &me);
   int branch_var(const Node &node, const float *flow, const double *z) const;
+  int branch_var_pc(const Node &node, const float *flow, const double *z) const;
+  // pseudo-costs (p.branching == 1): per integer variable and direction, the sum / count of the bound gain per unit
+  // of fractionality its branchings produced, and the running totals per variable kind (c / n) for the unknown ones
+  std::vector<double> pc_sum[2];
+  std::vector<int32_t> pc_cnt[2];
+  double pck_sum[2][2] = {{0, 0}, {0, 0}};   // [kind: 0 c, 1 n][direction]
+  int64_t pck_cnt[2][2] = {{0, 0}, {0, 0}};
+  void pc_update(const Node &node, double gain_bound);
   int drain_and_close();
 };
 
@@ -361,6 +373,7 @@ int NepBnb::submit(std::vector<std::pair<Engine *, std::pair<int, NodeP>>> &item
       g.eng->gen[slot] += 1;
       st.lps += 1;
       if (sts[b] == NEP_LP_INFEASIBLE) {
+        if (p.branching == 1 && node->kind == NODE) pc_update(*node, incv());
         st.lp_status[6] += 1;
         st.lp_status_kind[node->kind][6] += 1;
         g.eng->free.push_back(slot);
@@ -372,6 +385,60 @@ int NepBnb::submit(std::vector<std::pair<Engine *, std::pair<int, NodeP>>> &item
     }
   }
   return NEP_OK;
+}
+
+// one finished child LP: its bound gain over the parent's, per unit of the parent LP's fractionality
+void NepBnb::pc_update(const Node &node, double child_bound) {
+  if (node.bvar < 0 || !(node.pbound > -INF) || !std::isfinite(child_bound)) return;
+  if (pc_sum[0].empty()) {
+    for (int d = 0; d < 2; ++d) {
+      pc_sum[d].assign(L.n_int, 0.0);
+      pc_cnt[d].assign(L.n_int, 0);
+    }
+  }
+  if (node.bvar >= (int)pc_sum[0].size()) return;
+  const double g = std::max(0.0, child_bound - node.pbound) / std::max(node.bfrac, 1e-6);
+  const int d = node.bdir, k = (p.n0 >= 0 && node.bvar >= p.n0 && node.bvar < p.n1) ? 1 : 0;
+  pc_sum[d][node.bvar] += g;
+  pc_cnt[d][node.bvar] += 1;
+  pck_sum[k][d] += g;
+  pck_cnt[k][d] += 1;
+}
+
+// pseudo-cost branching (SCIP's default family, here without strong-branching initialisation): among the free c /
+// n whose LP value is fractional (and, for c, that carry flow), the largest product score
+// max(psi_down z, eps) * max(psi_up (1 - z), eps); a variable never branched takes its kind's average pseudo-cost
+// (1 before any).  No fractional candidate: the flow rule below.
+int NepBnb::branch_var_pc(const Node &node, const float *flow, const double *z) const {
+  const int FN = p.F * p.N;
+  std::vector<char> fixed(std::max(p.c1, p.n1) + 1, 0);
+  for (int32_t i : node.idx) fixed[i] = 1;
+  double avg[2][2];
+  for (int k = 0; k < 2; ++k)
+    for (int d = 0; d < 2; ++d)
+      avg[k][d] = pck_cnt[k][d] > 0 ? pck_sum[k][d] / (double)pck_cnt[k][d]
+                                    : (pck_cnt[k][1 - d] > 0 ? pck_sum[k][1 - d] / (double)pck_cnt[k][1 - d] : 1.0);
+  const bool have = !pc_sum[0].empty();
+  auto psi = [&](int v, int d, int k) {
+    return (have && pc_cnt[d][v] > 0) ? pc_sum[d][v] / (double)pc_cnt[d][v] : avg[k][d];
+  };
+  const double eps = 1e-6, ftol = 1e-4;
+  int best = -1;
+  double bs = -1.0;
+  auto consider = [&](int v, int k) {
+    const double zf = z[v];
+    if (!(zf > ftol && zf < 1.0 - ftol)) return;
+    const double sc = std::max(psi(v, 0, k) * zf, eps) * std::max(psi(v, 1, k) * (1.0 - zf), eps);
+    if (sc > bs) { bs = sc; best = v; }
+  };
+  if (p.n0 >= 0)
+    for (int v = p.n0; v < p.n1; ++v)
+      if (!fixed[v]) consider(v, 1);
+  for (int q = 0; q < FN; ++q) {
+    const int v = p.c0 + q;
+    if (!fixed[v] && (double)flow[q] > p.flow_tol) consider(v, 0);
+  }
+  return best >= 0 ? best : branch_var(node, flow, z);
 }
 
 int NepBnb::branch_var(const Node &node, const float *flow, const double *z) const {
@@ -563,6 +630,8 @@ int NepBnb::finish_one(Engine &eng, int slot, const NodeP &node, int status, dou
     return NEP_OK;
   }
   if (status == NEP_LP_OPTIMAL) st.certified += 1;
+  if (p.branching == 1 && node->kind == NODE)   // (an infeasible / cut-off child gained up to the incumbent)
+    pc_update(*node, (status == NEP_LP_INFEASIBLE || status == NEP_LP_CUTOFF) ? incv() : o);
   if (!eng.root_ready && node->depth == 0 && node->kind == NODE) {
     st.root_seconds = now_s() - t0;
     if (p.warm && status != NEP_LP_INFEASIBLE && status != NEP_LP_CUTOFF) {
@@ -654,7 +723,7 @@ int NepBnb::finish_one(Engine &eng, int slot, const NodeP &node, int status, dou
     ev_parent = me;
     ev_bound = bound;
   }
-  const int var = branch_var(*node, flow, z);
+  const int var = p.branching == 1 ? branch_var_pc(*node, flow, z) : branch_var(*node, flow, z);
   if (var >= 0) {
     for (double v : {1.0, 0.0}) {
       auto ch = std::make_shared<Node>();
@@ -663,6 +732,10 @@ int NepBnb::finish_one(Engine &eng, int slot, const NodeP &node, int status, dou
       ch->val = node->val;
       ch->val.push_back(v);
       ch->bound = std::max(bound, ibound(ch->idx, ch->val));
+      ch->bvar = var;
+      ch->bdir = v > 0.5 ? 1 : 0;
+      ch->bfrac = std::max(1e-6, v > 0.5 ? 1.0 - z[var] : z[var]);
+      ch->pbound = bound;
       if (pruned(ch->bound)) continue;
       ch->kind = (int)ch->idx.size() >= nb() ? LEAF : NODE;
       ch->parent = me;

@@ -86,7 +86,7 @@ struct SmallAcc {
 // Step-2 disruption block kept exact in the bound (DESIGN.md §4 "Disruption block").  The rows
 // D1/D2 (moved_from/to vs c and old), D3a/D3b/D4 (allocated / deallocated vs sum c) carry duals
 // against costs F*N, F*N +- 1: fp32-level relative noise on them moves the plain Lagrangian by ~1e-5
-// (tools/dblock_probe.py), more than the 1e-6 certificate allows.  Instead of dualising them, the
+// (tools/probes/dblock_probe.py), more than the 1e-6 certificate allows.  Instead of dualising them, the
 // bound minimises the block exactly: sum c is relaxed to a free T priced by lambda, each (f, j) takes
 // min over (c, mf, mt) of (r' - lambda) c + cmf mf + cmt mt on its box and D1/D2 (a piecewise-linear
 // function of c: its minimum is at an end or a kink), and G(lambda) = min over (a, d, T) of
@@ -125,7 +125,7 @@ __device__ __forceinline__ double dblock_item(double r, double lam, double old, 
 // c (e.g. c = S / M) has reduced cost exactly 0, so a dual error d in s moves the Lagrangian by M*d
 // (the box of c has width 1); and a column price the PDHG has not resolved at the 1e-6 level (the
 // 1/M price of routing flow to a destination that is not the old placement) drops that whole part
-// of the objective from the bound (tools/dual_repair_probe.py).  The repair re-prices
+// of the objective from the bound (tools/probes/dual_repair_probe.py).  The repair re-prices
 // each pair from the iterate's own c (complementary slackness, as a crossover would):
 //   * c inside a linear piece of its (disruption-)cost: the price that makes that piece's slope 0;
 //   * c at 0 = its lower end: the lowest price keeping c = 0 a minimiser (lowering s never lowers the

@@ -1795,7 +1795,7 @@ int flows(Model &m, int n, const int32_t *slots, float *out, float *wout = nullp
   const size_t plane = (size_t)m.max_batch * m.F * m.N;
   if (!m.d_flows && (rc = dalloc(m, &m.d_flows, 2 * plane))) return rc;
   // pinned staging both ways: pageable copies cost ~0.3 ms per call while a block iterates (round-4 B&B
-  // profile, tools/bnb_profile.py: 2.5 of 10 s at 64x32)
+  // profile, tools/probes/bnb_profile.py: 2.5 of 10 s at 64x32)
   if (!m.h_flows) {
     void *h = nullptr;
     if (hipHostMalloc(&h, sizeof(float) * 2 * plane + sizeof(int32_t) * m.max_batch) != hipSuccess)
@@ -1909,7 +1909,7 @@ int nep_model_create(const nep_model_desc *desc_in, int32_t max_batch, void *hip
   rc = setup_dense(*m, *desc);
   if (rc) return rc;
   if (!host_power && (rc = power_device(*m))) return rc;
-  if (const char *e = std::getenv("NEP_ETA_SCALE")) m->eta *= std::atof(e);   // (probe: tools/root_chaos_probe.py)
+  if (const char *e = std::getenv("NEP_ETA_SCALE")) m->eta *= std::atof(e);   // (probe: tools/probes/root_chaos_probe.py)
   *out_model = m.release();
   return NEP_OK;
 }

@@ -1372,7 +1372,7 @@ __global__ __launch_bounds__(256) void scalar_pass(DeviceView v, const int32_t *
   // primal feasibility polishing (step 1 and step 2; the step-2 duals D1/D2 are kept by x_pass, D3a/D3b/
   // D4/score by this pass): the best bound already meets the gap test against the
   // repaired point's objective and only its primal residual is left — the tail of the node LPs,
-  // whose CPU rows (C5) close last (tools/tail_probe.py).  From here the LP iterates on its
+  // whose CPU rows (C5) close last (tools/probes/tail_probe.py).  From here the LP iterates on its
   // feasibility problem (objective off, duals restarted from 0) from the current point; it is
   // certified once the repaired point is feasible within tol and its objective still within the
   // gap tolerance of the bound kept.
@@ -1476,7 +1476,7 @@ __global__ void init_slot(DeviceView v, const int32_t *__restrict__ slots, const
     // the PDLP update right after a warm start sees the large primal move of re-routing the fixed
     // placements and would shrink omega by orders of magnitude, which stalls the dual (measured on
     // the 512x256 bench children: 81/96 certified within 20k iterations without a floor, 95/96 with
-    // floor 2, 62k iterations in all instead of 304k; tools/floor_probe.py).
+    // floor 2, 62k iterations in all instead of 304k; tools/probes/floor_probe.py).
     if (warm && v.warm_omega_floor > 0) ctrl->omega_lo = fmin(ctrl->omega * v.warm_omega_floor, ctrl->omega_hi);
     // ... and, once that weight has been adapted over kOmegaTrained iterations of its lineage, at most
     // warm_omega_cap times it: without a cap the first restart after a warm start can raise it 50x on

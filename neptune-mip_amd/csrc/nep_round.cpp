@@ -2,7 +2,7 @@
 // nep_round_leaf).  One branching node's LP (its flows F x N and its c) -> a leaf fixing every c and n,
 // the memory-aware greedy of core/engine/bnb.py (DESIGN.md §7 "Primal heuristic"), run per finished node
 // (three modes each): in Python it was ~0.1 ms a call and ~30 % of the 64x32 search's wall time
-// (tools/bnb_profile.py).  Decision order and tie-breaks are the Python restatement's
+// (tools/probes/bnb_profile.py).  Decision order and tie-breaks are the Python restatement's
 // (tests/test_round_native.py compares the two leaf for leaf).
 #include <algorithm>
 #include <cmath>

@@ -190,7 +190,7 @@ def test_facility_relaxation_build():
 def test_presolve_cpu_cover_proves_overloaded_leaf_infeasible():
     """The node presolve's CPU cover test (nep_host.cpp cpu_cover_ok): testpy's step-1 rounding leaf that opens
     node 0 only (c[0,0] = c[1,0] = n[0] = 1, everything else 0) overloads node 0's CPU — HiGHS finds the box
-    infeasible (tools/leaf_limit_probe.py) and PDHG could only stall on it (round-4 GPU suite: testpy's step 1
+    infeasible (tools/probes/leaf_limit_probe.py) and PDHG could only stall on it (round-4 GPU suite: testpy's step 1
     ended LIMIT).  Both the from-scratch and the sparse-change presolve must reject it, and the leaf that
     also opens node 1 must pass."""
     import numpy as np

@@ -5,7 +5,7 @@ place of the big-M pairs (constraints_step1.py:5-15, :69-78) — certified by th
 facility_relaxation).  Root LPs and B&B-style children (n and c fixings), warm-started from the root as the
 search does; every LP must certify — within 25k iterations, or after at most 7 continuations of 25k from its
 own final state (the B&B's RETRY re-solve, core/engine/bnb.py): a long run can stall on a stale primal weight
-that a warm restart re-estimates (tools/fac_conv_probe.py: 32x16 MinUtilization's root, LIMIT at 400k in one
+that a warm restart re-estimates (tools/probes/fac_conv_probe.py: 32x16 MinUtilization's root, LIMIT at 400k in one
 run and in 100k chunks, certifies 8k iterations into the continuation of a 20k chunk)."""
 import numpy as np
 import pytest

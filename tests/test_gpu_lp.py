@@ -37,7 +37,7 @@ def test_root_and_node_lps(name, k):
     ub = np.full((B, m.n_int), np.inf)
     for b, (l, u, _) in enumerate(nodes):
         lb[b + 1], ub[b + 1] = l, u
-    # (step 2: syn_6x4 MDU model 1 LP 3 certifies at 360k iterations, tools/step2_cert_probe.py)
+    # (step 2: syn_6x4 MDU model 1 LP 3 certifies at 360k iterations, tools/probes/step2_cert_probe.py)
     res = m.solve(np.arange(B), lb, ub, tol=SOLVE_TOL, max_iters=400000 if step >= 2 else 100000)
     refs = [rec["lp_objective"]] + [r for _, _, r in nodes]
     for b, ref in enumerate(refs):

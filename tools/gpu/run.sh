@@ -12,8 +12,9 @@
 #   profile        rocprofv3 --kernel-trace --stats over an 8-step bench -> kernel_stats_by_slots.csv
 #   traffic        separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over tools/traffic.py -> traffic.json
 #   sq             SQ wave / wait / VALU counters of the steady x_pass -> sq.json
-#   probe:<args>   tools/step2_probe.py <args, comma-separated>
-#   py:<script>    python tools/<script> (a dev probe)
+#   probe:<args>   tools/probes/step2_probe.py <args, comma-separated>
+#   py:<name>,<args>  a dev probe: python tools/probe.py <name> <args> (tools/probes/<name>.py), or a tools/*.py
+#                  script (py:record_bnb_trace.py,...)
 set -u
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
@@ -46,10 +47,14 @@ for r in "$@"; do
       python3 tools/traffic.py summarize /tmp/pmc_fetch /tmp/pmc_write > "$O/traffic.json"; cat "$O/traffic.json" ;;
     sq)
       export ROC_AQL_QUEUE_SIZE=65536
-      step pmc_sq 400 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU -d /tmp/pmc_sq -o run -- python3 tools/traffic.py run
+      # (x_pass dispatches only, cold nodes — no 114k-iteration root solve: round 5's two passes outlived their limit
+      # while rocprofv3 wrote a dispatch database of ~178k kernels)
+      step pmc_sq 240 rocprofv3 --kernel-include-regex x_pass --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU -d /tmp/pmc_sq -o run -- python3 tools/traffic.py run cold
       python3 tools/traffic.py sq /tmp/pmc_sq > "$O/sq.json"; cat "$O/sq.json" ;;
-    probe:*) a=${r#probe:}; step probe 600 python -u tools/step2_probe.py ${a//,/ } ;;
-    py:*) a=${r#py:}; step "py_${a%%.py*}" 600 python -u tools/${a//,/ } ;;
+    probe:*) a=${r#probe:}; step probe 600 python -u tools/probe.py step2_probe ${a//,/ } ;;
+    py:*) a=${r#py:}; n=${a%%,*}; n=${n%.py}
+      if [ -f "tools/probes/$n.py" ]; then step "py_$n" 600 python -u tools/probe.py ${a//,/ }
+      else step "py_$n" 600 python -u tools/${a//,/ }; fi ;;
     *) echo "unknown recipe $r"; exit 2 ;;
   esac
 done
