@@ -290,8 +290,13 @@ typedef struct {
   int64_t node_limit;
   double time_limit;               /* seconds (<= 0: none) */
   int32_t world, rank;             /* API 12: the sharded search (world > 1: NEP_BNB_SYNC once per loop) */
-  int32_t branching;               /* API 12: 0 n by inflow, then c by flow; 1 pseudo-cost (product score) */
+  int32_t branching;               /* API 12: 0 n by inflow, then c by flow; 1 pseudo-cost (product score);
+                                      2 reliability branching: pseudo-costs, strong-branching probes while unreliable */
+  int32_t strong_cands, strong_rel;  /* branching 2: candidates scored, observations per direction to be reliable */
   int32_t reserved_p;
+  int64_t strong_iters;            /* branching 2: iteration budget of a probe LP */
+  double objective_unit;           /* with objective_integral: the objective's integral unit (<= 0: 1) — e.g. alpha / N
+                                      for MinDelayAndUtilization without workload, whose objective is alpha / N sum n */
 } nep_bnb_params;
 
 typedef struct {
@@ -310,6 +315,7 @@ typedef struct {
   int64_t presplit_nodes, presplit_lps, presplit_certified;   /* sharded: counts when the frontier was dealt */
   int64_t rebalanced, sync_calls;  /* sharded: open nodes imported from other ranks; collectives answered */
   double agreed_incumbent;         /* min(this rank's incumbent, the ranks' agreed one) */
+  int64_t strong_nodes, strong_lps, strong_iterations, strong_decided;   /* branching 2: nodes that probed, probes */
 } nep_bnb_stats;
 
 #define NEP_BNB_DONE 0   /* the search ended (no open node, or a stop): stats / incumbent are final */

@@ -99,12 +99,13 @@ class BnBResult:
         self.advance_calls = 0
         self.inflight_sum = 0           # LPs in flight summed over the advance calls (mean: / advance_calls)
         self.native = False             # the search ran on the native tree (csrc/nep_bnb.cpp)
+        self.strong = None              # (native, branching 2) strong-branching probe counts
 
     def as_dict(self):
         d = {k: getattr(self, k) for k in ("status", "objective", "bound", "nodes", "leaves", "lps", "certified",
                                            "lp_iterations", "unresolved", "seconds", "polished", "repaired",
                                            "lp_status", "lp_status_kind", "drained", "timing",
-                                           "heuristic_incumbents", "routing_warm", "native")}
+                                           "heuristic_incumbents", "routing_warm", "native", "strong")}
         d["inflight_mean"] = self.inflight_sum / max(1, self.advance_calls)
         d["resolved"] = sum(v for k, v in self.lp_status.items() if k not in ("limit", "numerical"))
         it = np.asarray(self.lp_iters, np.float64)
@@ -158,7 +159,7 @@ class BranchAndBound:
                  retry_res=math.inf, unit_flow_leaves=True, node_max_iters=None, bound_lp=None, bound_gap=1e-4,
                  trace=None, rebalance_every=8, primal=None, primal_every=0,
                  leaf_routing_warm=False, root_check_every=64, objective_integral=False, warm_weight_ref=0.0,
-                 native=None, step2_native=None, branching=0):
+                 native=None, step2_native=None, branching=0, strong_cands=8, strong_rel=2, strong_iters=256):
         self.lp = lp
         self.two = bound_lp is not None
         self.N, self.F = lp.N, lp.F
@@ -204,7 +205,10 @@ class BranchAndBound:
         # every integral point has an integral objective (step 2's disruption objective, objectives.py:55-63;
         # step-1 MinUtilization's node count): a node whose valid bound exceeds incumbent - 1 holds no better
         # point, so it is pruned (SCIP's objective-integrality pruning)
+        # (a number: the objective's integral unit, e.g. alpha / N for MinDelayAndUtilization without workload)
         self.objective_integral = bool(objective_integral)
+        self.objective_unit = (1.0 if objective_integral is True or not isinstance(objective_integral, (int, float))
+                               else float(objective_integral)) if objective_integral else 0.0
         # warm_weight_ref > 0: warm-started node LPs take their PDHG primal weight in [2, 4] x (warm_weight_ref x
         # the model's cold-start weight omega0) instead of [2, 4] x their parent's final weight, which ratchets up
         # along a lineage (nep_lp_set_reference_weight; step 1 at 512x256: replay 7.5 -> 12.2 certified LP/s,
@@ -219,8 +223,11 @@ class BranchAndBound:
         # evaluates itself (NeptuneStep2Base.native_bound); improve then runs on NEP_BNB_INCUMBENT events
         self.step2_native = step2_native
         # branching rule of the native tree: 0 = n by largest inflow, then c by largest flow (this module's loop);
-        # 1 = pseudo-cost branching (product score over fractional n / c, csrc/nep_bnb.cpp branch_var_pc)
+        # 1 = pseudo-cost branching (product score over fractional n / c, csrc/nep_bnb.cpp branch_var_pc); 2 = reliability
+        # branching: pseudo-costs, with strong-branching probe LPs (strong_iters iterations, both children of the
+        # strong_cands best candidates) while a candidate's pseudo-costs rest on fewer than strong_rel observations
         self.branching = int(branching)
+        self.strong_cands, self.strong_rel, self.strong_iters = int(strong_cands), int(strong_rel), int(strong_iters)
         # (the leaf / reference model only — the model whose node LPs the replay measured; the facility relaxation
         # keeps the parent-relative band: 256x128 / 20 s gap 0.51 % with it, 0.82 % with the band on both)
         for m_ in (lp,):
@@ -269,8 +276,9 @@ class BranchAndBound:
             return 0.0
         g = self.gap * max(1.0, abs(inc))
         if self.objective_integral:
-            # bound >= inc - 1 + delta prunes; delta covers the fp64 error of a Lagrangian bound of this size
-            g = max(g, 1.0 - min(0.5, 1e-6 + 1e-9 * abs(inc)))
+            # bound >= inc - unit + delta prunes; delta covers the fp64 error of a Lagrangian bound of this size
+            u = self.objective_unit if self.objective_unit > 0 else 1.0
+            g = max(g, u * (1.0 - min(0.5, 1e-6 + 1e-9 * abs(inc) / u)))
         return g
 
     def _ibound(self, idx, val):
@@ -829,7 +837,9 @@ class BranchAndBound:
                       retry_res=float(self.retry_res), flow_tol=float(self.flow_tol), upper_bound=float(self.ub0),
                       # (round-5 ADVICE: a non-finite node limit is no limit)
                       node_limit=int(min(float(self.node_limit), 2.0 ** 62)), time_limit=float(self.time_limit or 0.0),
-                      world=int(comm.world), rank=int(comm.rank), branching=self.branching)
+                      world=int(comm.world), rank=int(comm.rank), branching=self.branching,
+                      strong_cands=self.strong_cands, strong_rel=self.strong_rel, strong_iters=self.strong_iters,
+                      objective_unit=float(self.objective_unit))
         py_engines = []
         if hasattr(lp, "_h"):
             tree = lib.nep_bnb_create(lp._h, self.bound_lp._h if self.two else None, ctypes.byref(p),
@@ -948,6 +958,8 @@ class BranchAndBound:
         tm["drain"], tm["root"] = st.drain_seconds, st.root_seconds
         res.native = True
         res.rebalanced = int(st.rebalanced)
+        res.strong = {k: int(getattr(st, k)) for k in ("strong_nodes", "strong_lps", "strong_iterations",
+                                                       "strong_decided")}
         res.split_hash = int(st.split_hash) if split_seen else None
         t_end = time.perf_counter()
         res.bound = float(st.bound)

@@ -71,7 +71,8 @@ class BnbParams(ctypes.Structure):
                 ("retry_res", ctypes.c_double), ("flow_tol", ctypes.c_double), ("upper_bound", ctypes.c_double),
                 ("node_limit", ctypes.c_int64), ("time_limit", ctypes.c_double),
                 ("world", ctypes.c_int32), ("rank", ctypes.c_int32), ("branching", ctypes.c_int32),
-                ("reserved_p", ctypes.c_int32)]
+                ("strong_cands", ctypes.c_int32), ("strong_rel", ctypes.c_int32), ("reserved_p", ctypes.c_int32),
+                ("strong_iters", ctypes.c_int64), ("objective_unit", ctypes.c_double)]
 
 
 class BnbStats(ctypes.Structure):
@@ -87,7 +88,8 @@ class BnbStats(ctypes.Structure):
                [("split_hash", ctypes.c_uint32), ("reserved_", ctypes.c_int32)] + \
                [(k, ctypes.c_int64) for k in ("presplit_nodes", "presplit_lps", "presplit_certified", "rebalanced",
                                               "sync_calls")] + \
-               [("agreed_incumbent", ctypes.c_double)]
+               [("agreed_incumbent", ctypes.c_double)] + \
+               [(k, ctypes.c_int64) for k in ("strong_nodes", "strong_lps", "strong_iterations", "strong_decided")]
 
 
 # nep_bnb_engine (API 12): the calls the native tree makes on one model

@@ -110,8 +110,13 @@ class NeptuneStepBase(Solver):
     def objective_integral(self):
         """Every integral point of the step model has an integral objective: step-1 MinUtilization (sum n,
         objectives.py:24-27) and every step 2 (minimize_disruption, objectives.py:55-63: integer weights on
-        binaries and integers)."""
-        return self.step_id() != _lp.STEP1 or self.VARIANT == "MinUtilization"
+        binaries and integers) — True; step-1 MinDelayAndUtilization without workload (objectives.py:34-35 sets no
+        x terms when sum W = 0: alpha / N sum n) — its unit alpha / N; else False."""
+        if self.step_id() != _lp.STEP1 or self.VARIANT == "MinUtilization":
+            return True
+        if self.VARIANT == "MinDelayAndUtilization" and not np.asarray(self.data.workload_matrix).any():
+            return float(self.alpha) / len(self.data.nodes)
+        return False
 
     def objective_weights(self):
         """(cost per open node, coefficient of sum W D of the routing) of the step-1 objective, or None."""

@@ -41,7 +41,7 @@ namespace {
 int bad(int code, const char *msg) { return nep::set_error(code, msg); }
 
 constexpr double INF = std::numeric_limits<double>::infinity();
-enum Kind { NODE = 0, LEAF = 1, RETRY = 2, REFROOT = 3 };
+enum Kind { NODE = 0, LEAF = 1, RETRY = 2, REFROOT = 3, STRONG = 4 };   // STRONG: a strong-branching probe LP
 // lp status columns of nep_bnb_stats.lp_status: certified, bound, limit, infeasible, cutoff, numerical, presolve
 int status_col(int st) {
   switch (st) {
@@ -60,6 +60,7 @@ struct Parent {
   int slot = -1;
   int64_t gen = -1;
 };
+struct SbWait;
 
 struct Node {
   double bound;
@@ -72,8 +73,25 @@ struct Node {
   // the fixed value, the parent's bound
   int bvar = -1, bdir = 0;
   double bfrac = 0.0, pbound = -std::numeric_limits<double>::infinity();
+  std::shared_ptr<SbWait> sb;   // STRONG: the branching node its probe belongs to, candidate sb_i
+  int sb_i = -1;
 };
 using NodeP = std::shared_ptr<Node>;
+
+// a branching node waiting for its strong-branching probes (p.branching == 2): candidate variables, their LP values,
+// and per direction the probe's bound (NaN pending, +inf infeasible / cut off) and its finished slot (the child's
+// warm-start state: the probe ran on the child's own box)
+struct SbWait {
+  NodeP node;
+  Parent at;
+  double bound = 0.0;
+  std::vector<int> cand;
+  std::vector<double> zc, est[2];
+  std::vector<char> probed;
+  std::vector<double> res[2];
+  std::vector<Parent> src[2];
+  int pending = 0;
+};
 
 struct Engine {
   nep_bnb_engine ops{};         // the model's calls (ops.ctx: the engine handle for nep_lp_*)
@@ -215,7 +233,12 @@ struct NepBnb {
   double gap_abs(double incv) const {
     if (!std::isfinite(incv)) return 0.0;
     double g = p.gap * std::max(1.0, std::fabs(incv));
-    if (p.objective_integral) g = std::max(g, 1.0 - std::min(0.5, 1e-6 + 1e-9 * std::fabs(incv)));
+    if (p.objective_integral) {
+      // bound >= inc - unit + delta prunes: no integral point lies strictly between (delta: the fp64 error of a
+      // Lagrangian bound of this size, and the reference's eps-scale terms)
+      const double u = p.objective_unit > 0 ? p.objective_unit : 1.0;
+      g = std::max(g, u * (1.0 - std::min(0.5, 1e-6 + 1e-9 * std::fabs(incv) / u)));
+    }
     return g;
   }
   double incv() const { return std::min(inc, cut); }   // the pruning incumbent (the agreed one when sharded)
@@ -255,6 +278,11 @@ struct NepBnb {
   double pck_sum[2][2] = {{0, 0}, {0, 0}};   // [kind: 0 c, 1 n][direction]
   int64_t pck_cnt[2][2] = {{0, 0}, {0, 0}};
   void pc_update(const Node &node, double gain_bound);
+  // strong branching (reliability branching: probes only for candidates whose pseudo-costs are unreliable)
+  std::deque<NodeP> strong_q;
+  int64_t sb_waiting = 0;
+  int start_strong(const NodeP &node, const float *flow, const double *z, double bound, const Parent &me);
+  void decide_strong(SbWait &w);
   int drain_and_close();
 };
 
@@ -309,8 +337,10 @@ int NepBnb::submit(std::vector<std::pair<Engine *, std::pair<int, NodeP>>> &item
     }
     const int64_t budget = (node->kind == RETRY || node->kind == REFROOT || !eng->root_ready)
                                ? p.root_max_iters
-                               : (node->kind == NODE ? p.node_max_iters : p.max_iters);
-    const double bres = (node->kind == NODE && (eng->root_ready || two)) ? p.node_bound_res : 0.0;
+                               : (node->kind == NODE ? p.node_max_iters
+                                                     : (node->kind == STRONG ? p.strong_iters : p.max_iters));
+    const double bres = ((node->kind == NODE || node->kind == STRONG) && (eng->root_ready || two)) ? p.node_bound_res
+                                                                                                  : 0.0;
     const int ce = (node->kind == REFROOT || !eng->root_ready) ? p.root_check_every : p.check_every;
     Group *g = nullptr;
     for (auto &gg : groups)
@@ -372,8 +402,17 @@ int NepBnb::submit(std::vector<std::pair<Engine *, std::pair<int, NodeP>>> &item
       const NodeP &node = g.its[b].second;
       g.eng->gen[slot] += 1;
       st.lps += 1;
+      if (sts[b] == NEP_LP_INFEASIBLE && node->kind == STRONG) {
+        st.strong_lps += 1;
+        pc_update(*node, incv());
+        SbWait &w = *node->sb;
+        w.res[node->bdir][node->sb_i] = INF;
+        g.eng->free.push_back(slot);
+        if (--w.pending == 0) decide_strong(w);
+        continue;
+      }
       if (sts[b] == NEP_LP_INFEASIBLE) {
-        if (p.branching == 1 && node->kind == NODE) pc_update(*node, incv());
+        if (p.branching >= 1 && node->kind == NODE) pc_update(*node, incv());
         st.lp_status[6] += 1;
         st.lp_status_kind[node->kind][6] += 1;
         g.eng->free.push_back(slot);
@@ -409,6 +448,140 @@ void NepBnb::pc_update(const Node &node, double child_bound) {
 // n whose LP value is fractional (and, for c, that carry flow), the largest product score
 // max(psi_down z, eps) * max(psi_up (1 - z), eps); a variable never branched takes its kind's average pseudo-cost
 // (1 before any).  No fractional candidate: the flow rule below.
+// reliability branching: the top strong_cands candidates by pseudo-cost score; those whose pseudo-costs rest on
+// fewer than strong_rel observations in either direction get two probe LPs each (STRONG nodes, strong_iters
+// iterations, warm from this node's state, on the same model), submitted ahead of every other node; the node
+// branches when its probes are back (decide_strong).  Returns 1 when probes were queued, 0 when the pseudo-costs
+// decide at once.
+int NepBnb::start_strong(const NodeP &node, const float *flow, const double *z, double bound, const Parent &me) {
+  const int FN = p.F * p.N;
+  std::vector<char> fixed(std::max(p.c1, p.n1) + 1, 0);
+  for (int32_t i : node->idx) fixed[i] = 1;
+  const double ftol = 1e-4, eps = 1e-6;
+  double avg[2][2];
+  for (int k = 0; k < 2; ++k)
+    for (int d = 0; d < 2; ++d)
+      avg[k][d] = pck_cnt[k][d] > 0 ? pck_sum[k][d] / (double)pck_cnt[k][d]
+                                    : (pck_cnt[k][1 - d] > 0 ? pck_sum[k][1 - d] / (double)pck_cnt[k][1 - d] : 1.0);
+  const bool have = !pc_sum[0].empty();
+  struct C { double sc; int v; int rel; double e0, e1; };
+  std::vector<C> cs;
+  auto consider = [&](int v, int k) {
+    const double zf = z[v];
+    if (!(zf > ftol && zf < 1.0 - ftol)) return;
+    const int n0 = have ? pc_cnt[0][v] : 0, n1 = have ? pc_cnt[1][v] : 0;
+    const double p0 = n0 > 0 ? pc_sum[0][v] / n0 : avg[k][0], p1 = n1 > 0 ? pc_sum[1][v] / n1 : avg[k][1];
+    const double e0 = p0 * zf, e1 = p1 * (1.0 - zf);
+    cs.push_back(C{std::max(e0, eps) * std::max(e1, eps), v, std::min(n0, n1), e0, e1});
+  };
+  if (p.n0 >= 0)
+    for (int v = p.n0; v < p.n1; ++v)
+      if (!fixed[v]) consider(v, 1);
+  for (int q = 0; q < FN; ++q)
+    if (!fixed[p.c0 + q] && (double)flow[q] > p.flow_tol) consider(p.c0 + q, 0);
+  if (cs.empty()) return 0;
+  std::sort(cs.begin(), cs.end(), [](const C &a, const C &b) { return a.sc != b.sc ? a.sc > b.sc : a.v < b.v; });
+  const int K = std::min((int)cs.size(), std::max(1, p.strong_cands));
+  int unrel = 0;
+  for (int i = 0; i < K; ++i) unrel += cs[i].rel < p.strong_rel;
+  if (unrel == 0) return 0;
+  auto w = std::make_shared<SbWait>();
+  w->node = node;
+  w->at = me;
+  w->bound = bound;
+  for (int i = 0; i < K; ++i) {
+    w->cand.push_back(cs[i].v);
+    w->zc.push_back(z[cs[i].v]);
+    w->est[0].push_back(cs[i].e0);
+    w->est[1].push_back(cs[i].e1);
+    w->probed.push_back(cs[i].rel < p.strong_rel);
+  }
+  for (int d = 0; d < 2; ++d) {
+    w->res[d].assign(K, std::numeric_limits<double>::quiet_NaN());
+    w->src[d].assign(K, Parent{});
+  }
+  for (int i = 0; i < K; ++i) {
+    if (!w->probed[i]) continue;
+    for (int d = 1; d >= 0; --d) {
+      auto pr = std::make_shared<Node>();
+      pr->idx = node->idx;
+      pr->idx.push_back(w->cand[i]);
+      pr->val = node->val;
+      pr->val.push_back((double)d);
+      pr->bound = bound;
+      pr->kind = STRONG;
+      pr->parent = me;
+      pr->depth = node->depth + 1;
+      pr->bvar = w->cand[i];
+      pr->bdir = d;
+      pr->bfrac = std::max(1e-6, d ? 1.0 - w->zc[i] : w->zc[i]);
+      pr->pbound = bound;
+      pr->sb = w;
+      pr->sb_i = i;
+      strong_q.push_back(pr);
+      w->pending += 1;
+    }
+  }
+  sb_waiting += 1;
+  st.strong_nodes += 1;
+  return 1;
+}
+
+// all probes of a node are back: branch on the candidate with the best product of bound gains (a probe's bound is
+// a valid bound of its child — the child inherits it; an infeasible / cut-off probe removes that child); both
+// children of a candidate infeasible: the node's subtree is empty
+void NepBnb::decide_strong(SbWait &w) {
+  sb_waiting -= 1;
+  const Node &node = *w.node;
+  if (pruned(w.bound)) return;
+  const double big = 1e30, eps = 1e-12;
+  int best = -1;
+  double bs = -1.0;
+  for (size_t i = 0; i < w.cand.size(); ++i) {
+    double g[2];
+    for (int d = 0; d < 2; ++d) {
+      if (w.probed[i]) {
+        const double r = w.res[d][i];
+        g[d] = (!(r < INF) || pruned(r)) ? big : std::max(eps, r - w.bound);
+      } else {
+        g[d] = std::max(eps, w.est[d][i]);
+      }
+    }
+    if (g[0] >= big && g[1] >= big) return;   // neither child exists: nothing below this node
+    const double sc = g[0] * g[1];
+    if (sc > bs) { bs = sc; best = (int)i; }
+  }
+  if (best < 0) return;
+  const int var = w.cand[best];
+  st.strong_decided += 1;
+  for (double v : {1.0, 0.0}) {
+    const int d = v > 0.5 ? 1 : 0;
+    double cb = w.bound;
+    Parent src = w.at;
+    if (w.probed[best]) {
+      const double r = w.res[d][best];
+      if (!(r < INF)) continue;                 // the probe proved this child infeasible / above the cutoff
+      cb = std::max(cb, r);
+      if (w.src[d][best].eng) src = w.src[d][best];
+    }
+    auto ch = std::make_shared<Node>();
+    ch->idx = node.idx;
+    ch->idx.push_back(var);
+    ch->val = node.val;
+    ch->val.push_back(v);
+    ch->bound = std::max(cb, ibound(ch->idx, ch->val));
+    ch->bvar = var;
+    ch->bdir = d;
+    ch->bfrac = std::max(1e-6, d ? 1.0 - w.zc[best] : w.zc[best]);
+    ch->pbound = w.bound;
+    if (pruned(ch->bound)) continue;
+    ch->kind = (int)ch->idx.size() >= nb() ? LEAF : NODE;
+    ch->parent = src;
+    ch->depth = node.depth + 1;
+    push_heap(ch);
+  }
+}
+
 int NepBnb::branch_var_pc(const Node &node, const float *flow, const double *z) const {
   const int FN = p.F * p.N;
   std::vector<char> fixed(std::max(p.c1, p.n1) + 1, 0);
@@ -617,6 +790,19 @@ int NepBnb::finish_one(Engine &eng, int slot, const NodeP &node, int status, dou
   st.lp_iterations += iters;
   lp_iters.push_back(iters);
   const int col = status_col(status);
+  if (node->kind == STRONG) {   // a strong-branching probe: its bound (or infeasibility) for the waiting node
+    st.strong_lps += 1;
+    st.strong_iterations += iters;
+    const bool gone = status == NEP_LP_INFEASIBLE || status == NEP_LP_CUTOFF;
+    pc_update(*node, gone ? incv() : o);
+    SbWait &w = *node->sb;
+    const int d = node->bdir, i = node->sb_i;
+    w.res[d][i] = gone ? INF : std::max(node->pbound, o);
+    if (!gone) w.src[d][i] = Parent{&eng, slot, eng.gen[slot]};
+    eng.free.push_back(slot);
+    if (--w.pending == 0) decide_strong(w);
+    return NEP_OK;
+  }
   st.lp_status[col] += 1;
   st.lp_status_kind[node->kind][col] += 1;
   if (node->kind == REFROOT) {
@@ -630,7 +816,7 @@ int NepBnb::finish_one(Engine &eng, int slot, const NodeP &node, int status, dou
     return NEP_OK;
   }
   if (status == NEP_LP_OPTIMAL) st.certified += 1;
-  if (p.branching == 1 && node->kind == NODE)   // (an infeasible / cut-off child gained up to the incumbent)
+  if (p.branching >= 1 && node->kind == NODE)   // (an infeasible / cut-off child gained up to the incumbent)
     pc_update(*node, (status == NEP_LP_INFEASIBLE || status == NEP_LP_CUTOFF) ? incv() : o);
   if (!eng.root_ready && node->depth == 0 && node->kind == NODE) {
     st.root_seconds = now_s() - t0;
@@ -723,7 +909,11 @@ int NepBnb::finish_one(Engine &eng, int slot, const NodeP &node, int status, dou
     ev_parent = me;
     ev_bound = bound;
   }
-  const int var = p.branching == 1 ? branch_var_pc(*node, flow, z) : branch_var(*node, flow, z);
+  if (p.branching == 2 && start_strong(node, flow, z, bound, me)) {
+    eng.free.push_back(slot);   // (its probes warm-start from this slot; they are submitted first)
+    return NEP_OK;
+  }
+  const int var = p.branching >= 1 ? branch_var_pc(*node, flow, z) : branch_var(*node, flow, z);
   if (var >= 0) {
     for (double v : {1.0, 0.0}) {
       auto ch = std::make_shared<Node>();
@@ -833,6 +1023,7 @@ int NepBnb::drain_and_close() {
   while (!heap.empty()) { open.push_back(heap.top().bound); heap.pop(); }
   for (auto &n : pending) open.push_back(n->bound);
   for (auto &n : retry) open.push_back(n->bound);
+  for (auto &n : strong_q) open.push_back(n->bound);
   for (double b : unresolved_bounds) open.push_back(b);
   double bound = incv();
   for (double b : open) bound = std::min(bound, b);
@@ -1111,7 +1302,7 @@ int nep_bnb_run(void *tree, int32_t *event) {
     }
     const bool sharded = T.p.world > 1;
     if (sharded && !T.split && T.heap.size() >= (size_t)T.p.world * (size_t)T.p.batch && L.inflight == 0 &&
-        (!T.two || B.inflight == 0))
+        (!T.two || B.inflight == 0) && T.strong_q.empty() && T.sb_waiting == 0)
       T.deal_frontier();   // the frontier every rank holds identically, dealt once
     bool stop = T.stalled || T.st.nodes >= T.p.node_limit ||
                 (T.p.time_limit > 0 && now_s() - T.t0 > T.p.time_limit);
@@ -1119,7 +1310,7 @@ int nep_bnb_run(void *tree, int32_t *event) {
     for (int e = 0; e < T.n_engines(); ++e)
       for (auto &n : T.engines[e]->running)
         if (n && n->kind != REFROOT) ++busy;
-    int64_t open_n = (int64_t)(T.heap.size() + T.pending.size() + T.retry.size()) + busy;
+    int64_t open_n = (int64_t)(T.heap.size() + T.pending.size() + T.retry.size() + T.strong_q.size()) + busy;
     if (sharded) {
       // one collective per loop, run by the caller: incumbent MIN, stop OR, open + in-flight SUM
       if (!T.sync_answered) {
@@ -1143,9 +1334,13 @@ int nep_bnb_run(void *tree, int32_t *event) {
     // at most `batch` LPs in flight per model; further free slots keep finished states (parked parents)
     int capL = T.p.batch - L.inflight, capB = T.p.batch_b - B.inflight;
     if (!T.two) {
-      while (!L.free.empty() && capL > 0 && (!T.retry.empty() || !T.pending.empty() || !T.heap.empty())) {
+      while (!L.free.empty() && capL > 0 &&
+             (!T.strong_q.empty() || !T.retry.empty() || !T.pending.empty() || !T.heap.empty())) {
         NodeP node;
-        if (!T.retry.empty()) {
+        if (!T.strong_q.empty()) {   // strong-branching probes first: their node waits for them
+          node = T.strong_q.front();
+          T.strong_q.pop_front();
+        } else if (!T.retry.empty()) {
           node = T.retry.front();
           T.retry.pop_front();
         } else if (!T.pending.empty()) {
@@ -1170,6 +1365,14 @@ int nep_bnb_run(void *tree, int32_t *event) {
         --capL;
         items.push_back({&L, {s, T.refroot}});
         T.refroot = nullptr;
+      }
+      while (!B.free.empty() && capB > 0 && !T.strong_q.empty()) {   // probes of branching nodes first
+        NodeP node = T.strong_q.front();
+        T.strong_q.pop_front();
+        const int s = B.free.front();
+        B.free.pop_front();
+        items.push_back({&B, {s, node}});
+        --capB;
       }
       while (!B.free.empty() && capB > 0 && !T.heap.empty() && (!B.root_ready || L.root_ready)) {
         NodeP node = T.heap.top().node;
@@ -1214,7 +1417,8 @@ int nep_bnb_run(void *tree, int32_t *event) {
       // nothing iterates: either this rank's part of a sharded frontier is empty (the others still work), or
       // open nodes wait for a slot that never frees (round-5 ADVICE: e.g. warm starts off with one working slot
       // kept for the incumbent) — end the search as a limit instead of looping forever
-      if (items.empty() && T.heap.size() + T.pending.size() + T.retry.size() > 0) T.stalled = true;
+      if (items.empty() && T.heap.size() + T.pending.size() + T.retry.size() + T.strong_q.size() > 0)
+        T.stalled = true;
       continue;
     }
     T.st.advance_calls += 1;

@@ -57,10 +57,10 @@ def _alloc_set(data, z, F, N):
     return {(data.functions[k], data.nodes[j]) for k, j in zip(*np.nonzero(c))}
 
 
-@pytest.mark.parametrize("n,f,seconds", [(64, 32, 20.0), (256, 128, 40.0)])
+@pytest.mark.parametrize("n,f,seconds", [(64, 32, 20.0), (256, 128, 40.0), (1024, 512, 45.0)])
 def test_neptune_mdu_flow_end_to_end(n, f, seconds):
-    """BASELINE config 5's shape (Alibaba trace: W == 0, D = 1 - I, 0.6 % of (f, j) pre-allocated) at config 2's and
-    3's sizes: step 2 is feasible (the published Alibaba flow: delete infeasible, create places every function
+    """BASELINE config 5's shape (Alibaba trace: W == 0, D = 1 - I, 0.6 % of (f, j) pre-allocated) at config 2's,
+    3's and its own size (1024 x 512, the whole neptune.py:18-39 orchestration on one GPU): step 2 is feasible (the published Alibaba flow: delete infeasible, create places every function
     on the fewest nodes keeping the most old placements), so every step of the flow is checked."""
     from core.utils.synthetic import alibaba_payload
     data, alpha, solver, solved, alloc, score = _flow(alibaba_payload(n, f, seed=0), seconds)

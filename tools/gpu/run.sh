@@ -9,7 +9,7 @@
 #   smoke          __graft_entry__.smoke()
 #   bench          python bench.py (defaults: CPU baseline + product B&B sections included)
 #   bench:<args>   python bench.py <args, comma-separated> (e.g. bench:--seed,1,--cpu-budget,0)
-#   profile        rocprofv3 --kernel-trace --stats over an 8-step bench -> kernel_stats_by_slots.csv
+#   profile        rocprofv3 --kernel-trace --stats over the bench's timed replay -> kernel_stats_by_slots.csv
 #   traffic        separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over tools/traffic.py -> traffic.json
 #   sq             SQ wave / wait / VALU counters of the steady x_pass -> sq.json
 #   probe:<args>   tools/probes/step2_probe.py <args, comma-separated>
@@ -35,7 +35,7 @@ for r in "$@"; do
     bench) step bench 600 python -u bench.py ; grep "^{" "$O/bench.log" | tail -1 > "$O/bench.json" ;;
     bench:*) a=${r#bench:}; step bench_args 600 python -u bench.py ${a//,/ } ; grep "^{" "$O/bench_args.log" | tail -1 > "$O/bench_args.json" ;;
     profile)
-      step profile 300 rocprofv3 --kernel-trace --stats -d /tmp/prof -o run -- python3 bench.py --steps 8 --cpu-budget 0 --bnb-seconds 0
+      step profile 400 rocprofv3 --kernel-trace --stats -d /tmp/prof -o run -- python3 bench.py --steps 8 --cpu-budget 0 --bnb-seconds 0 --alibaba-seconds 0 --native-steps 0 --children-steps 0
       python3 tools/prof_summary.py /tmp/prof > "$O/kernel_stats_by_slots.csv"; cp /tmp/prof/*/*stats.csv "$O/" 2>/dev/null
       head -12 "$O/kernel_stats_by_slots.csv" | cut -c1-160 ;;
     traffic)

@@ -38,11 +38,11 @@ def main():
     from core.utils import data_to_solver_input
     from core.utils.synthetic import synthetic_payload
     rows = []
-    for item in a.sizes.split(","):
+    for item in a.sizes.replace("+", ",").split(","):
         size, _, secs = item.partition(":")
         N, F = (int(t) for t in size.split("x"))
         data = data_to_solver_input(synthetic_payload(N, F, seed=a.seed), with_db=False)
-        for rule in (int(r) for r in a.rules.split(",")):
+        for rule in (int(r) for r in a.rules.replace("+", ",").split(",")):
             st1 = NeptuneStep1CPUMinDelayAndUtilization(alpha=0.5, verbose=False, batch=a.batch, lp_tol=1e-6,
                                                         lp_max_iters=4096)
             st1.load_data(data)
