@@ -345,7 +345,9 @@ def alibaba_flows(a):
         score = {k: float(v) for k, v in body["score"].items()}
         out.append({"solver": stype, "processing_time_s": body["processing_time"], "wall_s": wall,
                     "score": score, "steps": steps,
-                    "all_steps_optimal": all(v["status"] == "OPTIMAL" for v in steps.values() if v),
+                    # every step's search ended with a proof: OPTIMAL, or INFEASIBLE (step-2 delete here, after which
+                    # the reference falls back to create, neptune.py:24-30)
+                    "all_steps_proven": all(v["status"] in ("OPTIMAL", "INFEASIBLE") for v in steps.values() if v),
                     "reference_score": ref_score, "reference_processing_time_s": ref_t,
                     "speedup_vs_reference": ref_t / max(1e-9, body["processing_time"]),
                     "score_matches_reference": all(abs(score[k] - v) <= 1e-6 * max(1.0, abs(v))

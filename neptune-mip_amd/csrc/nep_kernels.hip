@@ -36,6 +36,13 @@
 #ifndef NEP_INLINE_REFLECT
 #define NEP_INLINE_REFLECT 0
 #endif
+// NEP_XPASS_PREFETCH (A/B build flag, default off): the plain x_pass loads each wave's NEXT routing row (x and its
+// delay row) into registers while it projects the current one (one row ahead; 16 more VGPRs at CPL 2, 5 waves per
+// SIMD instead of 6).  Round 1 measured a register prefetch slower (0.591 vs 0.575 ms per launch) before the LDS
+// accumulators freed 32 VGPRs; this flag re-measures it
+#ifndef NEP_XPASS_PREFETCH
+#define NEP_XPASS_PREFETCH 0
+#endif
 // waves per SIMD the certificate x_pass is compiled for (build flag; 2: 210 VGPRs, no spills; 3: 168 VGPRs
 // with 160 B/lane of spills, matching the 3 workgroups per CU its LDS allows)
 #ifndef NEP_CHECK_WAVES
@@ -185,7 +192,8 @@ __device__ __forceinline__ void loaded_shift(const DeviceView &v, int slot, int 
 // certificate iteration takes effect and the anchor is rewritten; the steady-state variant carries
 // no restart code (fewer registers live).
 template <int CPL, bool CHECK, bool INIT, bool FIRST, int TW>
-__global__ __launch_bounds__(kWave * TW) __attribute__((amdgpu_waves_per_eu(CHECK ? NEP_CHECK_WAVES : (TW == 16 ? 4 : 6), 8)))
+__global__ __launch_bounds__(kWave * TW) __attribute__((amdgpu_waves_per_eu(
+    CHECK ? NEP_CHECK_WAVES : (TW == 16 ? 4 : (NEP_XPASS_PREFETCH ? 5 : 6)), 8)))
 void x_pass(DeviceView v, const int32_t *__restrict__ slots, int plain, int it, int nslots, int nt_i) {
   const bool nt = nt_i != 0;
   constexpr int E = 4 * CPL;
@@ -303,18 +311,43 @@ void x_pass(DeviceView v, const int32_t *__restrict__ slots, int plain, int it, 
   double s_score = 0.0, s_pobj = 0.0, s_lagr = 0.0, s_lagr_r = 0.0, s_lagr0 = 0.0, s_move = 0.0, s_dist = 0.0;
   const double s_empty = (cnt_f == 0 && threadIdx.x == 0) ? (double)nrows : 0.0;
 
+  constexpr bool kPf = NEP_XPASS_PREFETCH && !CHECK;
+  float pfx[E], pfd[E];   // (unused without NEP_XPASS_PREFETCH: removed by the compiler)
+  auto row_nd = [&](const RowInfo &q) { return q.src >= 0 && (q.wobj != 0.f || q.wsc != 0.f); };
+  if (kPf && wave < nrows) {
+    const RowInfo q = v.rows[r0 + wave];
+    float dummy[E];
+    load_row<CPL>(x + (int64_t)(r0 + wave) * NP, v.D + (int64_t)(q.src < 0 ? 0 : q.src) * NP, xa, row_nd(q), false, nt,
+                  lane, NP, pfx, pfd, dummy);
+  }
   for (int rr = wave; rr < nrows; rr += TW) {
     const int r = r0 + rr;
     const RowInfo ri = v.rows[r];
-    const bool nd = ri.src >= 0 && (ri.wobj != 0.f || ri.wsc != 0.f);
-    // no software prefetch of the next row: the registers it costs are worth more as occupancy
-    // (0.575 vs 0.591 ms per launch before the LDS accumulators; other waves hide the latency)
+    const bool nd = row_nd(ri);
     float xc[E], dc[E], ac[E];
     // anchor row: kept sparse (<= kAnchorK (j, value) pairs, lanes 0..cnt-1 load one each) or dense
     int acn = 0;
     if (need_anchor) acn = NEP_SPARSE_ANCHOR ? __builtin_amdgcn_readfirstlane(acnt[r]) : kAnchorDense;
-    load_row<CPL>(x + (int64_t)r * NP, v.D + (int64_t)(ri.src < 0 ? 0 : ri.src) * NP, xa + (int64_t)r * NP, nd,
-                  need_anchor && acn > kAnchorK, nt, lane, NP, xc, dc, ac);
+    if (kPf) {
+      // this row came in with the previous one; the next row's loads go out now, ahead of the projection
+#pragma unroll
+      for (int e = 0; e < E; ++e) { xc[e] = pfx[e]; dc[e] = pfd[e]; ac[e] = 0.f; }
+      if (need_anchor && acn > kAnchorK) {
+        float d0[E], d1[E];
+        load_row<CPL>(xa + (int64_t)r * NP, v.D, xa + (int64_t)r * NP, false, false, nt, lane, NP, ac, d0, d1);
+      }
+      if (rr + TW < nrows) {
+        const RowInfo q = v.rows[r + TW];
+        float dummy[E];
+        load_row<CPL>(x + (int64_t)(r + TW) * NP, v.D + (int64_t)(q.src < 0 ? 0 : q.src) * NP, xa, row_nd(q), false,
+                      nt, lane, NP, pfx, pfd, dummy);
+      }
+    } else {
+      // (default: no software prefetch of the next row — the registers it costs are worth more as occupancy,
+      // 0.575 vs 0.591 ms per launch in round 1; other waves hide the latency)
+      load_row<CPL>(x + (int64_t)r * NP, v.D + (int64_t)(ri.src < 0 ? 0 : ri.src) * NP, xa + (int64_t)r * NP, nd,
+                    need_anchor && acn > kAnchorK, nt, lane, NP, xc, dc, ac);
+    }
     if (need_anchor && acn <= kAnchorK) {
       AnchorEnt ae{0, 0.f};
       if (lane < acn) ae = aent[(int64_t)r * kAnchorK + lane];

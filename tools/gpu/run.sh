@@ -8,7 +8,8 @@
 #   tests:<files>  the GPU tests of the given comma-separated test files only
 #   smoke          __graft_entry__.smoke()
 #   bench          python bench.py (defaults: CPU baseline + product B&B sections included)
-#   bench:<args>   python bench.py <args, comma-separated> (e.g. bench:--seed,1,--cpu-budget,0)
+#   bench:<args>   python bench.py <args, comma-separated> (e.g. bench:--seed,1,--cpu-budget,0) -> bench_args<k>.json
+#   env:<VAR>=<v>  export a variable for the following steps (e.g. env:NEPTUNE_LP_LIB=lib/variants/...); unenv:<VAR>
 #   profile        rocprofv3 --kernel-trace --stats over the bench's timed replay -> kernel_stats_by_slots.csv
 #   traffic        separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over tools/traffic.py -> traffic.json
 #   sq             SQ wave / wait / VALU counters of the steady x_pass -> sq.json
@@ -19,6 +20,7 @@ set -u
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 O=gpurun_out/$1; shift; mkdir -p "$O"
+nb=0
 step() {   # step <name> <seconds> <command...>: run, log, stop the call on failure
   local name=$1 secs=$2; shift 2
   echo "== $name: $*"
@@ -33,7 +35,10 @@ for r in "$@"; do
     tests:*) a=${r#tests:}; step pytest_sel 900 python -u -m pytest ${a//,/ } -m gpu -v -s --timeout 300 --timeout-method thread ;;
     smoke) step smoke 240 python -u -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 600 python -u bench.py ; grep "^{" "$O/bench.log" | tail -1 > "$O/bench.json" ;;
-    bench:*) a=${r#bench:}; step bench_args 600 python -u bench.py ${a//,/ } ; grep "^{" "$O/bench_args.log" | tail -1 > "$O/bench_args.json" ;;
+    bench:*) a=${r#bench:}; nb=$((nb + 1)); step bench_args$nb 600 python -u bench.py ${a//,/ }
+      grep "^{" "$O/bench_args$nb.log" | tail -1 > "$O/bench_args$nb.json" ;;
+    env:*) export "${r#env:}"; echo "== export ${r#env:}" ;;
+    unenv:*) unset "${r#unenv:}"; echo "== unset ${r#unenv:}" ;;
     profile)
       step profile 400 rocprofv3 --kernel-trace --stats -d /tmp/prof -o run -- python3 bench.py --steps 8 --cpu-budget 0 --bnb-seconds 0 --alibaba-seconds 0 --native-steps 0 --children-steps 0
       python3 tools/prof_summary.py /tmp/prof > "$O/kernel_stats_by_slots.csv"; cp /tmp/prof/*/*stats.csv "$O/" 2>/dev/null

@@ -31,6 +31,10 @@ def main():
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--node-iters", type=int, default=0)
     ap.add_argument("--bound-gap", type=float, default=0.0)
+    ap.add_argument("--node-limit", type=float, default=1e9)
+    ap.add_argument("--strong-iters", type=int, default=256)
+    ap.add_argument("--strong-cands", type=int, default=8)
+    ap.add_argument("--tag", default="")
     ap.add_argument("--out", default="")
     a = ap.parse_args()
     from core.engine.lp import LPModel
@@ -48,7 +52,8 @@ def main():
             st1.load_data(data)
             m = LPModel(data, "MinDelayAndUtilization", step=1, alpha=0.5, max_batch=a.batch + 2)
             bm = st1.bound_model(data, a.batch + 1)
-            ov = dict(time_limit=float(secs or 60), root_max_iters=400000, gap=a.gap, branching=rule)
+            ov = dict(time_limit=float(secs or 60), root_max_iters=400000, gap=a.gap, branching=rule,
+                      node_limit=a.node_limit, strong_iters=a.strong_iters, strong_cands=a.strong_cands)
             if a.node_iters:
                 ov["node_max_iters"] = a.node_iters
             if a.bound_gap:
@@ -61,7 +66,8 @@ def main():
                 bm.close()
             inc = res.objective
             ref = HIGHS_OPT.get(size) if a.seed == 0 else None
-            row = {"instance": size, "seed": a.seed, "rule": rule, "time_limit": float(secs or 60), "status": res.status,
+            row = {"instance": size, "seed": a.seed, "rule": rule, "tag": a.tag, "node_iters": a.node_iters,
+                   "bound_gap": a.bound_gap, "time_limit": float(secs or 60), "status": res.status, "strong": res.strong,
                    "incumbent": inc, "bound": res.bound,
                    "rel_gap": None if inc is None else (inc - res.bound) / max(1.0, abs(inc)),
                    "nodes": res.nodes, "lps": res.lps, "seconds": time.time() - t0, "native": res.native,
