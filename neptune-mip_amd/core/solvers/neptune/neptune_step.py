@@ -78,6 +78,10 @@ class NeptuneStepBase(Solver):
     # they stop): 256x128 / 20 s: 3678 vs 3274 node LPs, bound 0.00607 vs 0.00596, same incumbent;
     # 512x256 / 45 s: bound 0.00264 vs 0.00243, incumbent 0.5474 vs 0.5483
     node_iters_fraction = 0.25
+    # the native tree's branching rule (core/engine/bnb.py): step 1 uses reliability branching — pseudo-costs, strong-
+    # branching probe LPs while a candidate's pseudo-costs are unreliable (DESIGN.md §7 "Branching rules": 64x32 bound
+    # after 20k nodes 0.13533 against 0.13495 with the flow rule, 48x24 / 56x28 likewise); step 2 keeps the flow rule
+    branching = 2
 
     def seed_leaves(self, layout):
         """Placements to try as leaves right after the root (a B&B primal start); none by default."""
@@ -282,7 +286,7 @@ class NeptuneStepBase(Solver):
                   objective_integral=self.objective_integral(),
                   # step 1: warm starts banded around 8 x the model's cold-start primal weight
                   warm_weight_ref=8.0 if self.step_id() == _lp.STEP1 else 0.0,
-                  step2_native=self.native_bound())
+                  step2_native=self.native_bound(), branching=self.branching)
         kw.update(overrides)
         return BranchAndBound(model, data.workload_matrix, data.function_memory_matrix, data.node_memory_matrix, **kw)
 
@@ -444,6 +448,7 @@ class NeptuneStep2Base(NeptuneStepBase):
     node_bound_res = 0.0   # every node LP to its certificate (see NeptuneStepBase.node_bound_res)
     unit_flow_leaves = False
     node_iters_fraction = 1.0
+    branching = 0
 
     def __init__(self, mode=str, soften_step1_sol=1.3, **kwargs):
         super().__init__(**kwargs)
