@@ -44,6 +44,8 @@ hipError_t launch_compact_f64(const double *vals, int rows, int cols, int64_t ld
                               int32_t *cnt, int32_t *off, int32_t *orow, int32_t *ocol, double *oval, bool count_only,
                               hipStream_t s);
 hipError_t launch_copy_segments(const SlotCopy &c, hipStream_t s);
+hipError_t launch_gather_solutions(const DeviceView &v, const int32_t *slots, int n, int ni, double *out,
+                                   hipStream_t s);
 hipError_t launch_power_iteration(const DeviceView &v, int iters, double *zx, double *zs, double *gx, double *gs,
                                   double *y, double *upart, double *spart, double *gfac, double *part, int nblk,
                                   double *out, const int32_t *rp, const int32_t *ci, const double *cv,
@@ -194,7 +196,8 @@ struct Model {
   std::vector<int32_t> launched;
   Ctrl *h_ctrl = nullptr;
   float *h_flows = nullptr;     // pinned staging of nep_lp_get_flows(_split): [2][max_batch][F*N] + slots
-  double *h_sols = nullptr;     // pinned staging of nep_lp_get_solutions: [max_batch][n_int] + statuses
+  double *h_sols = nullptr;     // pinned staging of nep_lp_get_solutions: [max_batch][n_int] + the slot list
+  double *d_sols = nullptr;     // [max_batch][n_int]: the gathered solutions (gather_solutions)
   // pinned staging of nep_lp_submit's uploads (slots, change offsets / indices / bounds, exact flags): the
   // call returns without waiting for them; two stagings alternate, and a submit waits on the event of the
   // one it rewrites (recorded after that staging's copies, two submits earlier: normally long done)
@@ -1977,14 +1980,14 @@ int nep_lp_get_solutions(void *model, int32_t n, const int32_t *slots, double *z
       return fail(NEP_ERR_NOMEM, "hipHostMalloc (solutions)");
     m.h_sols = static_cast<double *>(hp);
   }
-  int32_t *hst = reinterpret_cast<int32_t *>(m.h_sols + (size_t)m.max_batch * ni);
-  for (int b = 0; b < n; ++b)
-    HIPCHK(hipMemcpyAsync(hst + b, &m.v.ctrl[slots[b]].status, sizeof(int32_t), hipMemcpyDeviceToHost, m.aux));
-  HIPCHK(hipStreamSynchronize(m.aux));
-  for (int b = 0; b < n; ++b) {   // (the certified point for a certified LP, else the iterate: solution_z)
-    const double *z = (hst[b] == NEP_LP_OPTIMAL ? m.v.zr : m.v.zi) + (size_t)slots[b] * m.v.sint;
-    HIPCHK(hipMemcpyAsync(m.h_sols + b * ni, z, ni * sizeof(double), hipMemcpyDeviceToHost, m.aux));
-  }
+  int rc;
+  if (!m.d_sols && (rc = dalloc(m, &m.d_sols, (size_t)m.max_batch * ni))) return rc;
+  // (the certified point for a certified LP, else the iterate — solution_z's choice, made on the device)
+  int32_t *hs = reinterpret_cast<int32_t *>(m.h_sols + (size_t)m.max_batch * ni);
+  std::memcpy(hs, slots, n * sizeof(int32_t));
+  HIPCHK(hipMemcpyAsync(m.d_new, hs, n * sizeof(int32_t), hipMemcpyHostToDevice, m.aux));
+  HIPCHK(launch_gather_solutions(m.v, m.d_new, n, (int)ni, m.d_sols, m.aux));
+  HIPCHK(hipMemcpyAsync(m.h_sols, m.d_sols, (size_t)n * ni * sizeof(double), hipMemcpyDeviceToHost, m.aux));
   HIPCHK(hipStreamSynchronize(m.aux));
   std::memcpy(z_out, m.h_sols, sizeof(double) * n * ni);
   return NEP_OK;
