@@ -160,6 +160,11 @@ int nep_lp_solve_batch(void *model, int32_t B, const int32_t *slots, const doubl
  * nep_lp_active: number of iterating slots. */
 int nep_lp_submit(void *model, int32_t n, const int32_t *slots, const double *lb_int, const double *ub_int,
                   const nep_lp_opts *opts, int32_t *status);
+/* API 12: nep_lp_submit with a per-LP iteration budget and bound stop (max_iters[b] / bound_res[b] for node
+ * b; either array may be NULL, and an entry <= 0 falls back to opts->max_iters / no bound stop), so a
+ * branch-and-bound starts its strong-branching probes, children and re-solves in one submit group. */
+int nep_lp_submit_ex(void *model, int32_t n, const int32_t *slots, const double *lb_int, const double *ub_int,
+                     const nep_lp_opts *opts, const int64_t *max_iters, const double *bound_res, int32_t *status);
 int nep_lp_advance(void *model, int32_t min_done, int32_t *n_done, int32_t *done_slots, double *obj,
                    double *primal_obj, int32_t *status, int64_t *iters);
 int nep_lp_active(void *model);
@@ -343,6 +348,9 @@ typedef struct {
   int (*get_flows)(void *ctx, int32_t n, const int32_t *slots, float *flows);
   int (*get_solutions)(void *ctx, int32_t n, const int32_t *slots, double *z_out);
   int (*get_diag)(void *ctx, int32_t slot, double *out16);
+  /* optional (NULL: one submit per budget / bound-stop group): nep_lp_submit_ex's contract */
+  int (*submit_ex)(void *ctx, int32_t n, const int32_t *slots, const double *lb_int, const double *ub_int,
+                   const nep_lp_opts *opts, const int64_t *max_iters, const double *bound_res, int32_t *status);
 } nep_bnb_engine;
 
 /* NULL on a bad argument (nep_last_error says which): batch < 1, a layout outside n_int, no working slot left

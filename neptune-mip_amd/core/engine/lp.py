@@ -105,13 +105,15 @@ BNB_PARAMS = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_double, ct
 BNB_FLOWS = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int32, _i32p, _fltp)
 BNB_SOLS = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int32, _i32p, _dblp)
 BNB_DIAG = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int32, _dblp)
+BNB_SUBMIT_EX = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int32, _i32p, _dblp, _dblp,
+                                 ctypes.POINTER(LpOpts), _i64p, _dblp, _i32p)
 
 
 class BnbEngine(ctypes.Structure):
     _fields_ = [("ctx", ctypes.c_void_p), ("n_int", ctypes.c_int32), ("max_batch", ctypes.c_int32),
                 ("submit", BNB_SUBMIT), ("advance", BNB_ADVANCE), ("active", BNB_ACTIVE), ("copy_state", BNB_COPY),
                 ("set_params", BNB_PARAMS), ("get_flows", BNB_FLOWS), ("get_solutions", BNB_SOLS),
-                ("get_diag", BNB_DIAG)]
+                ("get_diag", BNB_DIAG), ("submit_ex", BNB_SUBMIT_EX)]
 
 
 class PyBnbEngine:
@@ -121,10 +123,11 @@ class PyBnbEngine:
     over HiGHS (tests/oracle_lp.py).  A Python exception inside a call ends the search with NEP_ERR_STATE and is
     kept in `error` (BranchAndBound re-raises it)."""
 
-    def __init__(self, model, F, N):
+    def __init__(self, model, F, N, per_lp=True):
         self.model, self.F, self.N = model, int(F), int(N)
         self.n_int, self.max_batch = int(model.n_int), int(model.max_batch)
         self.error = None
+        self.ex_calls = 0
         ni, mb = self.n_int, self.max_batch
         A = np.ctypeslib.as_array
 
@@ -144,6 +147,23 @@ class PyBnbEngine:
                               cutoff=o.cutoff, max_iters=int(o.max_iters), check_every=int(o.check_every),
                               warm_start=bool(o.warm_start), bound_res=o.bound_res, gap_tol=o.gap_tol)
             A(status, (n,))[:] = np.asarray(st, np.int32)
+
+        def submit_ex(_, n, slots, lb, ub, opts, mi, br, status):
+            # per-LP budgets / bound stops: one model.submit per distinct (budget, bound stop), in first-seen order
+            o = opts.contents
+            sl, lbs, ubs = A(slots, (n,)).copy(), A(lb, (n, ni)).copy(), A(ub, (n, ni)).copy()
+            mis = A(mi, (n,)).copy() if mi else np.full(n, o.max_iters, np.int64)
+            brs = A(br, (n,)).copy() if br else np.full(n, o.bound_res)
+            keys = list(dict.fromkeys(zip(mis.tolist(), brs.tolist())))
+            out = A(status, (n,))
+            for k_mi, k_br in keys:
+                sel = np.flatnonzero((mis == k_mi) & (brs == k_br))
+                st = model.submit(sl[sel], lbs[sel], ubs[sel], tol=o.tol, cutoff=o.cutoff,
+                                  max_iters=int(k_mi) if k_mi > 0 else int(o.max_iters),
+                                  check_every=int(o.check_every), warm_start=bool(o.warm_start),
+                                  bound_res=max(float(k_br), 0.0), gap_tol=o.gap_tol)
+                out[sel] = np.asarray(st, np.int32)
+            self.ex_calls += 1
 
         def advance(_, min_done, n_done, slots, obj, pobj, status, iters):
             r = model.advance(int(min_done))
@@ -183,12 +203,13 @@ class PyBnbEngine:
 
         self.table = BnbEngine(None, ni, mb, BNB_SUBMIT(guard(submit)), BNB_ADVANCE(guard(advance)),
                                BNB_ACTIVE(active), BNB_COPY(guard(copy_state)), BNB_PARAMS(guard(set_params)),
-                               BNB_FLOWS(guard(flows)), BNB_SOLS(guard(sols)), BNB_DIAG(guard(diag)))
+                               BNB_FLOWS(guard(flows)), BNB_SOLS(guard(sols)), BNB_DIAG(guard(diag)),
+                               BNB_SUBMIT_EX(guard(submit_ex)) if per_lp else BNB_SUBMIT_EX())
 
 
 # every entry point declared in include/neptune_lp.h
 EXPORTS = ("nep_model_create", "nep_model_destroy", "nep_model_get_info", "nep_lp_solve_batch",
-           "nep_lp_submit", "nep_lp_advance", "nep_lp_active",
+           "nep_lp_submit", "nep_lp_submit_ex", "nep_lp_advance", "nep_lp_active",
            "nep_lp_get_solution", "nep_lp_get_rows", "nep_lp_copy_state", "nep_get_stats", "nep_reset_stats",
            "nep_lp_get_flows_split",
            "nep_last_error", "nep_api_version", "nep_lp_get_diag", "nep_debug_build", "nep_debug_state",
@@ -233,6 +254,7 @@ def load_library(path=None):
     lib.nep_lp_solve_batch.argtypes = [vp, i32, ctypes.POINTER(i32), _dp, _dp, ctypes.POINTER(LpOpts), _dp, _dp,
                                        ctypes.POINTER(i32), ctypes.POINTER(i64)]
     lib.nep_lp_submit.argtypes = [vp, i32, pi32, _dp, _dp, ctypes.POINTER(LpOpts), pi32]
+    lib.nep_lp_submit_ex.argtypes = [vp, i32, pi32, _dp, _dp, ctypes.POINTER(LpOpts), pi64, _dp, pi32]
     lib.nep_lp_advance.argtypes = [vp, i32, pi32, pi32, _dp, _dp, pi32, pi64]
     lib.nep_lp_active.argtypes = [vp]
     lib.nep_lp_get_solution.argtypes = [vp, i32, _dp, ctypes.POINTER(ctypes.c_float)]
@@ -507,14 +529,23 @@ class LPModel:
                warm_start=False, warm_omega_floor=0.0, gap_tol=0.0, warm_omega_cap=0.0, polish_after=0.0,
               bound_res=0.0):
         """Start node LPs in free slots; returns their presolve status (LP_INFEASIBLE: proven
-        infeasible, not started; LP_ITERATION_LIMIT: iterating)."""
+        infeasible, not started; LP_ITERATION_LIMIT: iterating).  max_iters / bound_res may be per-LP
+        arrays (length len(slots)): then one nep_lp_submit_ex call (API 12) carries them."""
         slots = np.ascontiguousarray(np.asarray(slots, dtype=np.int32).reshape(-1))
         B = len(slots)
         lbp, ubp = self._bounds(B, lb, ub)
         status = np.zeros(B, np.int32)
-        opts = LpOpts(float(tol), float(cutoff), int(max_iters), int(check_every), 1 if warm_start else 0,
-                      float(warm_omega_floor), float(gap_tol), float(warm_omega_cap), float(polish_after),
-                      float(bound_res))
+        per = np.ndim(max_iters) > 0 or np.ndim(bound_res) > 0
+        mi = np.ascontiguousarray(np.broadcast_to(np.asarray(max_iters, np.int64), (B,))) if per else None
+        br = np.ascontiguousarray(np.broadcast_to(np.asarray(bound_res, np.float64), (B,))) if per else None
+        opts = LpOpts(float(tol), float(cutoff), int(mi.max()) if per and B else int(np.max(max_iters)),
+                      int(check_every), 1 if warm_start else 0, float(warm_omega_floor), float(gap_tol),
+                      float(warm_omega_cap), float(polish_after), 0.0 if per else float(bound_res))
+        if per:
+            _check(self._lib, self._lib.nep_lp_submit_ex(self._h, B, _ptr(slots, ctypes.c_int32), _ptr(lbp), _ptr(ubp),
+                                                         ctypes.byref(opts), _ptr(mi, ctypes.c_int64), _ptr(br),
+                                                         _ptr(status, ctypes.c_int32)), "nep_lp_submit_ex")
+            return status
         _check(self._lib, self._lib.nep_lp_submit(self._h, B, _ptr(slots, ctypes.c_int32), _ptr(lbp), _ptr(ubp),
                                                   ctypes.byref(opts), _ptr(status, ctypes.c_int32)),
                "nep_lp_submit")

@@ -142,6 +142,10 @@ uint32_t crc32_update(uint32_t crc, const void *data, size_t n) {
 // the nep_lp_* calls of an engine model as a call table (ctx = the model handle)
 int op_submit(void *c, int32_t n, const int32_t *sl, const double *lb, const double *ub, const nep_lp_opts *o,
               int32_t *st) { return nep_lp_submit(c, n, sl, lb, ub, o, st); }
+int op_submit_ex(void *c, int32_t n, const int32_t *sl, const double *lb, const double *ub, const nep_lp_opts *o,
+                 const int64_t *mi, const double *br, int32_t *st) {
+  return nep_lp_submit_ex(c, n, sl, lb, ub, o, mi, br, st);
+}
 int op_advance(void *c, int32_t md, int32_t *nd, int32_t *sl, double *ob, double *po, int32_t *st, int64_t *it) {
   return nep_lp_advance(c, md, nd, sl, ob, po, st, it);
 }
@@ -168,6 +172,7 @@ int model_ops(void *lp, nep_bnb_engine *out) {
   out->get_flows = op_flows;
   out->get_solutions = op_sols;
   out->get_diag = op_diag;
+  out->submit_ex = op_submit_ex;
   return NEP_OK;
 }
 
@@ -307,7 +312,8 @@ bool ops_complete(const nep_bnb_engine &o) {
 
 }  // namespace
 
-// one nep_lp_submit per (engine, warm, budget, bound_res, check_every) group, warm-start copies first
+// one submit per (engine, warm, check_every) group — and per (budget, bound_res) too when the engine has no
+// submit_ex (per-LP budgets) — warm-start copies first
 int NepBnb::submit(std::vector<std::pair<Engine *, std::pair<int, NodeP>>> &items) {
   struct Group {
     Engine *eng;
@@ -316,6 +322,8 @@ int NepBnb::submit(std::vector<std::pair<Engine *, std::pair<int, NodeP>>> &item
     double bres;
     int ce;
     std::vector<std::pair<int, NodeP>> its;
+    std::vector<int64_t> mi;
+    std::vector<double> br;
   };
   std::vector<Group> groups;
   std::vector<std::pair<int, int>> copies[2];   // per engine (leaf first): (src, dst)
@@ -342,14 +350,19 @@ int NepBnb::submit(std::vector<std::pair<Engine *, std::pair<int, NodeP>>> &item
     const double bres = ((node->kind == NODE || node->kind == STRONG) && (eng->root_ready || two)) ? p.node_bound_res
                                                                                                   : 0.0;
     const int ce = (node->kind == REFROOT || !eng->root_ready) ? p.root_check_every : p.check_every;
+    const bool ex = eng->ops.submit_ex != nullptr;
+    const int64_t gb = ex ? -1 : budget;
+    const double gr = ex ? -1.0 : bres;
     Group *g = nullptr;
     for (auto &gg : groups)
-      if (gg.eng == eng && gg.warm == warm && gg.budget == budget && gg.bres == bres && gg.ce == ce) g = &gg;
+      if (gg.eng == eng && gg.warm == warm && gg.budget == gb && gg.bres == gr && gg.ce == ce) g = &gg;
     if (!g) {
-      groups.push_back(Group{eng, warm, budget, bres, ce, {}});
+      groups.push_back(Group{eng, warm, gb, gr, ce, {}, {}, {}});
       g = &groups.back();
     }
     g->its.push_back({slot, node});
+    g->mi.push_back(budget);
+    g->br.push_back(bres);
   }
   // copies: a slot that is both a parent state (source) and a new node's slot (destination) is read before
   // it is overwritten; a cycle falls back to the root's state
@@ -389,13 +402,17 @@ int NepBnb::submit(std::vector<std::pair<Engine *, std::pair<int, NodeP>>> &item
     nep_lp_opts o{};
     o.tol = p.tol;
     o.cutoff = std::isfinite(cutoff) ? cutoff : INF;
-    o.max_iters = g.budget;
+    o.max_iters = g.mi[0];
     o.check_every = g.ce;
     o.warm_start = g.warm ? 1 : 0;
     o.gap_tol = (two && g.eng == &B) ? p.bound_gap : 0.0;
-    o.bound_res = g.bres;
+    o.bound_res = g.br[0];
     sts.assign(n, 0);
-    int rc = g.eng->ops.submit(g.eng->ops.ctx, n, sl.data(), lbv.data(), ubv.data(), &o, sts.data());
+    // (a bound-stop entry of 0 means none: nep_lp_submit_ex reads entries <= 0 that way)
+    int rc = g.eng->ops.submit_ex
+                 ? g.eng->ops.submit_ex(g.eng->ops.ctx, n, sl.data(), lbv.data(), ubv.data(), &o, g.mi.data(),
+                                        g.br.data(), sts.data())
+                 : g.eng->ops.submit(g.eng->ops.ctx, n, sl.data(), lbv.data(), ubv.data(), &o, sts.data());
     if (rc) return rc;
     for (int b = 0; b < n; ++b) {
       const int slot = sl[b];

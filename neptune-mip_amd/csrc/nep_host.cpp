@@ -34,7 +34,7 @@ hipError_t launch_node_bounds(const DeviceView &v, const int32_t *slots, int nsl
                               const double *base_ub, const uint8_t *base_mask, const int32_t *off, const int32_t *idx,
                               const double *cl, const double *cu, int max_chg, hipStream_t s);
 hipError_t launch_init_slot(const DeviceView &v, const int32_t *slots, const int32_t *exact, int nslots, bool warm,
-                            double eta, double omega0, hipStream_t s);
+                            double eta, double omega0, const double *per, hipStream_t s);
 hipError_t launch_node_flows(const DeviceView &v, const int32_t *slots, int n, float *out, float *wout,
                              hipStream_t s);
 hipError_t launch_compact_f32(const float *vals, int rows, int cols, int64_t ld, double thr, int round3,
@@ -1438,7 +1438,7 @@ static void presolve_batch(Model &m, int n, const double *lbi, const double *ubi
 // the slot (cold or warm) and add it to the iterating set.  status[b] = NEP_LP_INFEASIBLE for a
 // node presolve proves infeasible (it does not iterate), else NEP_LP_ITERATION_LIMIT.
 int submit(Model &m, int n, const int32_t *slots, const double *lbi, const double *ubi, const nep_lp_opts *opts,
-           int32_t *status) {
+           int32_t *status, const int64_t *mi_per = nullptr, const double *br_per = nullptr) {
   if (n <= 0) return NEP_OK;
   const nep_lp_opts o = resolve_opts(opts);
   if (!m.act.empty() && o.check_every != m.run.check_every)
@@ -1466,6 +1466,8 @@ int submit(Model &m, int n, const int32_t *slots, const double *lbi, const doubl
                                ": moved_from / moved_to bounds must be integral (binary variables; NEP_STEP2_FULL=1 "
                                "iterates the full disruption rows)");
   std::vector<int32_t> fresh, off(1, 0), exact;
+  std::vector<double> per_mi, per_br;   // (nep_lp_submit_ex: the fresh slots' own budget / bound stop)
+  const bool per = mi_per != nullptr || br_per != nullptr;
   int max_chg = 0;
   for (int b = 0; b < n; ++b) {
     const int s = slots[b];
@@ -1477,6 +1479,10 @@ int submit(Model &m, int n, const int32_t *slots, const double *lbi, const doubl
     exact.push_back(nb.ex ? 1 : 0);
     off.push_back(off.back() + (int32_t)nb.cnt);
     max_chg = std::max(max_chg, (int)nb.cnt);
+    if (per) {
+      per_mi.push_back((double)(mi_per && mi_per[b] > 0 ? mi_per[b] : o.max_iters));
+      per_br.push_back(br_per ? (br_per[b] > 0 ? br_per[b] : 0.0) : o.bound_res);
+    }
   }
   const size_t nchg = (size_t)off.back();
   if (fresh.empty()) {
@@ -1487,7 +1493,7 @@ int submit(Model &m, int n, const int32_t *slots, const double *lbi, const doubl
   // the node boxes on the device: base box copy + the packed changes scattered over it (a few
   // KB per node instead of the 2 x 8 x n_int bytes of bounds and the F x NP mask), staged through pinned
   // host memory so the call need not wait for the copies (nor for the initialisation kernels behind them)
-  const size_t need_i = 2 * (size_t)nf + off.size() + nchg, need_d = 2 * nchg;
+  const size_t need_i = 2 * (size_t)nf + off.size() + nchg, need_d = 2 * nchg + (per ? 2 * (size_t)nf : 0);
   const int sk = m.sub_k;
   m.sub_k ^= 1;
   if (m.sub_pending[sk]) HIPCHK(hipEventSynchronize(m.ev_sub[sk]));   // that staging's copies have read it
@@ -1511,6 +1517,10 @@ int submit(Model &m, int n, const int32_t *slots, const double *lbi, const doubl
   if (!m.ev_sub[sk]) HIPCHK(hipEventCreateWithFlags(&m.ev_sub[sk], hipEventDisableTiming));
   int32_t *hf = m.h_sub_i[sk], *ho = hf + nf, *hc = ho + off.size(), *he = hc + nchg;
   double *hl = m.h_sub_d[sk], *hu = hl + nchg;
+  if (per) {
+    std::copy(per_mi.begin(), per_mi.end(), hu + nchg);
+    std::copy(per_br.begin(), per_br.end(), hu + nchg + nf);
+  }
   std::copy(fresh.begin(), fresh.end(), hf);
   std::copy(off.begin(), off.end(), ho);
   std::copy(exact.begin(), exact.end(), he);
@@ -1532,7 +1542,7 @@ int submit(Model &m, int n, const int32_t *slots, const double *lbi, const doubl
   HIPCHK(hipEventRecord(m.ev_sub[sk], m.aux));
   HIPCHK(launch_node_bounds(v, dn, nf, m.d_base_lb, m.d_base_ub, m.d_base_mask, doff, didx, dlb, dub, max_chg,
                             m.aux));
-  HIPCHK(launch_init_slot(v, dn, dex, nf, o.warm_start != 0, m.eta, m.omega0, m.aux));
+  HIPCHK(launch_init_slot(v, dn, dex, nf, o.warm_start != 0, m.eta, m.omega0, per ? dub + nchg : nullptr, m.aux));
   HIPCHK(launch_x_pass(v, dn, nf, false, true, true, true, 0, m.aux));
   HIPCHK(launch_node_pass(v, dn, nf, false, true, true, true, 0, m.aux));
   HIPCHK(launch_scalar_pass(v, dn, nf, false, true, true, true, 0, o.check_every, m.aux));
@@ -1946,6 +1956,12 @@ int nep_lp_submit(void *model, int32_t n, const int32_t *slots, const double *lb
                   const nep_lp_opts *opts, int32_t *status) {
   if (!model || (n > 0 && (!slots || !status))) return fail(NEP_ERR_ARG, "null argument");
   return submit(*static_cast<Model *>(model), n, slots, lb_int, ub_int, opts, status);
+}
+
+int nep_lp_submit_ex(void *model, int32_t n, const int32_t *slots, const double *lb_int, const double *ub_int,
+                     const nep_lp_opts *opts, const int64_t *max_iters, const double *bound_res, int32_t *status) {
+  if (!model || (n > 0 && (!slots || !status))) return fail(NEP_ERR_ARG, "null argument");
+  return submit(*static_cast<Model *>(model), n, slots, lb_int, ub_int, opts, status, max_iters, bound_res);
 }
 
 int nep_lp_advance(void *model, int32_t min_done, int32_t *n_done, int32_t *done_slots, double *obj,

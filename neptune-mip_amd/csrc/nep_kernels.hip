@@ -1476,7 +1476,7 @@ __global__ __launch_bounds__(256) void scalar_pass(DeviceView v, const int32_t *
 
 // cold / warm initialisation of a slot (x̄ ← 0 for cold; the init passes project it)
 __global__ void init_slot(DeviceView v, const int32_t *__restrict__ slots, const int32_t *__restrict__ exact, int warm,
-                          double eta, double omega0) {
+                          double eta, double omega0, const double *__restrict__ per) {
   const int slot = slots[blockIdx.y];
   Ctrl *ctrl = v.ctrl + slot;
   const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1533,8 +1533,9 @@ __global__ void init_slot(DeviceView v, const int32_t *__restrict__ slots, const
     ctrl->status = 1;
     ctrl->active = 1;
     ctrl->exact = exact[blockIdx.y];
-    ctrl->max_iters = v.max_iters;
-    ctrl->bound_res = v.bound_res;
+    // (nep_lp_submit_ex: per-LP iteration budget and bound stop, per = [2][nslots]; else the call's)
+    ctrl->max_iters = per ? (int64_t)per[blockIdx.y] : v.max_iters;
+    ctrl->bound_res = per ? per[gridDim.y + blockIdx.y] : v.bound_res;
     ctrl->infeas_hits = 0;
     ctrl->restart_pending = 1;
     ctrl->polish = ctrl->polish_pending = 0;   // a warm start does not inherit its parent's polishing
@@ -1682,9 +1683,9 @@ hipError_t launch_node_bounds(const DeviceView &v, const int32_t *slots, int nsl
 }
 
 hipError_t launch_init_slot(const DeviceView &v, const int32_t *slots, const int32_t *exact, int nslots, bool warm,
-                            double eta, double omega0, hipStream_t s) {
+                            double eta, double omega0, const double *per, hipStream_t s) {
   dim3 grid(256, nslots), block(256);
-  hipLaunchKernelGGL(init_slot, grid, block, 0, s, v, slots, exact, warm ? 1 : 0, eta, omega0);
+  hipLaunchKernelGGL(init_slot, grid, block, 0, s, v, slots, exact, warm ? 1 : 0, eta, omega0, per);
   return hipGetLastError();
 }
 

@@ -144,3 +144,28 @@ def test_sharded_native_tree_rebalances_idle_ranks():
     assert abs(nat[(True, 0)][1] - rec["mip_objective"]) <= 1e-6 * max(1.0, abs(rec["mip_objective"]))
     print("nodes received by rebalancing per rank:", [nat[(True, r)][5] for r in range(2)])
     assert sum(nat[(True, r)][5] for r in range(2)) > 0, "no rank ever took nodes from another"
+
+
+@pytest.mark.parametrize("branching", [0, 2])
+def test_native_tree_per_lp_budgets_merge_submit_groups(monkeypatch, branching):
+    """API 12 submit_ex: with per-LP budgets / bound stops the tree submits once per (engine, warm, check_every)
+    group instead of once per (budget, bound stop) too — strong-branching probes, children and re-solves go in one
+    call.  The search must end where the per-budget grouping ends (same status, objective and vector)."""
+    import core.engine.lp as lpmod
+    made = []
+
+    class Rec(lpmod.PyBnbEngine):
+        def __init__(self, model, F, N, per_lp=True):
+            super().__init__(model, F, N, per_lp=per_lp)
+            made.append(self)
+
+    name = "syn_8x4_s3_r1.0_NeptuneMinUtilization" if "syn_8x4_s3_r1.0_NeptuneMinUtilization" in G else STEP1[0]
+    out = {}
+    for per_lp in (True, False):
+        made.clear()
+        Rec.__init__.__defaults__ = (per_lp,)
+        monkeypatch.setattr(lpmod, "PyBnbEngine", Rec)
+        res = _search(name, True, branching=branching)
+        out[per_lp] = (res.status, res.objective, None if res.z is None else np.asarray(res.z).tolist())
+        assert made and (made[0].ex_calls > 0) == per_lp
+    assert out[True] == out[False]

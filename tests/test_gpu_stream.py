@@ -53,3 +53,42 @@ def test_stream_refill_matches_highs(name, k):
         assert st == LP_OPTIMAL, (b, st, obj, ref)
         assert abs(obj - ref) <= TOL * max(1.0, abs(ref)), (b, obj, ref)
     m.close()
+
+
+def test_submit_ex_per_lp_budgets_match_separate_submits():
+    """API 12 nep_lp_submit_ex: the per-LP budgets of one call stop each LP where a submit of its own with that
+    budget stops it (same status, iterations and values), and the unlimited ones certify the recorded LP value."""
+    from core.engine.lp import LPModel, LP_ITERATION_LIMIT, LP_OPTIMAL
+    name, k = "payload", 0
+    data, variant, step, kw = build_args(name, k)
+    ref = G[name]["models"][k]["lp_objective"]
+    budgets = np.array([64, 100000, 128, 100000], np.int64)
+
+    def run(per):
+        m = LPModel(data, variant, step=step, max_batch=4, **kw)
+        if per:
+            st = m.submit(np.arange(4), None, None, tol=1e-7, max_iters=budgets, check_every=64,
+                          bound_res=np.zeros(4))
+        else:
+            st = np.concatenate([m.submit([s], None, None, tol=1e-7, max_iters=int(budgets[s]), check_every=64)
+                                 for s in range(4)])
+        assert (st == LP_ITERATION_LIMIT).all()
+        got = {}
+        while m.active():
+            r = m.advance(1)
+            for i, s in enumerate(r["slots"]):
+                got[int(s)] = (int(r["status"][i]), int(r["iters"][i]), float(r["obj"][i]),
+                               float(r["primal_obj"][i]))
+        m.close()
+        return got
+
+    per, sep = run(True), run(False)
+    assert sorted(per) == [0, 1, 2, 3]
+    for s in range(4):
+        assert per[s][:2] == sep[s][:2], (s, per[s], sep[s])
+        assert per[s][1] <= budgets[s]
+        if per[s][0] == LP_ITERATION_LIMIT:
+            assert per[s][1] == budgets[s]
+    for s in (1, 3):
+        assert per[s][0] == LP_OPTIMAL
+        assert abs(per[s][2] - ref) <= TOL * max(1.0, abs(ref))
