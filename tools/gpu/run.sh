@@ -14,6 +14,7 @@
 #   traffic        separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over tools/traffic.py -> traffic.json
 #   sq             SQ wave / wait / VALU counters of the steady x_pass -> sq.json
 #   probe:<args>   tools/probes/step2_probe.py <args, comma-separated>
+#   kprof:<name>,<args>  rocprofv3 --kernel-trace --stats over a dev probe -> kprof_<name>.csv
 #   py:<name>,<args>  a dev probe: python tools/probe.py <name> <args> (tools/probes/<name>.py), or a tools/*.py
 #                  script (py:record_bnb_trace.py,...)
 set -u
@@ -56,6 +57,10 @@ for r in "$@"; do
       # while rocprofv3 wrote a dispatch database of ~178k kernels)
       step pmc_sq 240 rocprofv3 --kernel-include-regex x_pass --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU -d /tmp/pmc_sq -o run -- python3 tools/traffic.py run cold
       python3 tools/traffic.py sq /tmp/pmc_sq > "$O/sq.json"; cat "$O/sq.json" ;;
+    kprof:*) a=${r#kprof:}; n=${a%%,*}
+      step "kprof_$n" 600 rocprofv3 --kernel-trace --stats -d /tmp/kprof_$n -o run -- python3 tools/probe.py ${a//,/ }
+      cp /tmp/kprof_$n/*/*stats.csv "$O/" 2>/dev/null; python3 tools/prof_summary.py /tmp/kprof_$n > "$O/kprof_$n.csv"
+      head -12 "$O/kprof_$n.csv" | cut -c1-160 ;;
     probe:*) a=${r#probe:}; step probe 600 python -u tools/probe.py step2_probe ${a//,/ } ;;
     py:*) a=${r#py:}; n=${a%%,*}; n=${n%.py}
       if [ -f "tools/probes/$n.py" ]; then step "py_$n" 600 python -u tools/probe.py ${a//,/ }

@@ -35,7 +35,7 @@ def main():
             os.environ[k] = v
         m = LPModel(data, "MinDelayAndUtilization", step=1, alpha=alpha, max_batch=2)
         t = time.perf_counter()
-        r = m.solve([0], tol=1e-6, max_iters=400000, check_every=check)
+        r = m.solve([0], tol=1e-6, max_iters=int(os.environ.get("ROOT_MAX", 400000)), check_every=check)
         dt = time.perf_counter() - t
         print(f"{name:10s} {envs:40s} status {int(r['status'][0])} obj {float(r['obj'][0]):.10g} "
               f"iters {int(r['iters'][0])} {dt:.2f}s", flush=True)
