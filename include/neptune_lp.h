@@ -161,7 +161,7 @@ int nep_lp_solve_batch(void *model, int32_t B, const int32_t *slots, const doubl
 int nep_lp_submit(void *model, int32_t n, const int32_t *slots, const double *lb_int, const double *ub_int,
                   const nep_lp_opts *opts, int32_t *status);
 /* API 12: nep_lp_submit with a per-LP iteration budget and bound stop (max_iters[b] / bound_res[b] for node
- * b; either array may be NULL, and an entry <= 0 falls back to opts->max_iters / no bound stop), so a
+ * b; a NULL array takes the opts' value, an entry <= 0 opts->max_iters / no bound stop), so a
  * branch-and-bound starts its strong-branching probes, children and re-solves in one submit group. */
 int nep_lp_submit_ex(void *model, int32_t n, const int32_t *slots, const double *lb_int, const double *ub_int,
                      const nep_lp_opts *opts, const int64_t *max_iters, const double *bound_res, int32_t *status);
