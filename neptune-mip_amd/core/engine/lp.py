@@ -213,7 +213,7 @@ EXPORTS = ("nep_model_create", "nep_model_destroy", "nep_model_get_info", "nep_l
            "nep_lp_get_solution", "nep_lp_get_rows", "nep_lp_copy_state", "nep_get_stats", "nep_reset_stats",
            "nep_lp_get_flows_split",
            "nep_last_error", "nep_api_version", "nep_lp_get_diag", "nep_debug_build", "nep_debug_state",
-           "nep_debug_presolve", "nep_lp_set_params", "nep_lp_get_flows", "nep_lp_routing_entries",
+           "nep_debug_presolve", "nep_debug_sparse_rows", "nep_lp_set_params", "nep_lp_get_flows", "nep_lp_routing_entries",
            "nep_lp_allocation_entries", "nep_lp_score_check", "nep_round_leaf", "nep_lp_copy_routing",
            "nep_lp_get_solutions", "nep_round_leaves", "nep_lp_set_reference_weight",
            "nep_bnb_create", "nep_bnb_destroy", "nep_bnb_add_leaf", "nep_bnb_set_incumbent", "nep_bnb_event_data",
@@ -269,6 +269,7 @@ def load_library(path=None):
     lib.nep_reset_stats.argtypes = [vp]
     lib.nep_reset_stats.restype = None
     lib.nep_lp_get_diag.argtypes = [vp, i32, _dp]
+    lib.nep_debug_sparse_rows.argtypes = [vp, i32, vp, vp]
     lib.nep_debug_build.argtypes = [ctypes.POINTER(ModelDesc), _dp, _dp, _dp, _dp, ctypes.POINTER(i32)]
     lib.nep_debug_state.argtypes = [vp, i32, _dp, _dp, ctypes.POINTER(ctypes.c_float), _dp, _dp]
     lib.nep_debug_presolve.argtypes = [ctypes.POINTER(ModelDesc), i32, _dp, _dp, pi32, pi32, _dp, _dp]
@@ -682,6 +683,16 @@ class LPModel:
 
     DIAG = ("pobj", "lagr", "best_lagr", "pres", "gap", "omega", "tau", "sigma", "eta", "k", "k_since_restart",
             "status", "active", "restart_fpr", "last_fpr", "sigma_max")
+
+    def sparse_rows(self, slot):
+        """Per routing row of a slot: the nonzeros of its Halpern anchor and (facility relaxation) of its x <= c
+        duals as held on the device (kAnchorDense = 17: the row is dense)."""
+        R = self.info.n_rows
+        a = np.zeros(R, np.int32)
+        lam = np.zeros(R, np.int32) if self.relaxation == RELAX_FACILITY else None
+        _check(self._lib, self._lib.nep_debug_sparse_rows(self._h, int(slot), _ptr(a), _ptr(lam)),
+               "nep_debug_sparse_rows")
+        return a, lam
 
     def diag(self, slot):
         out = np.zeros(16)

@@ -76,7 +76,7 @@ __device__ __forceinline__ int store_row_sparse(const float (&val)[4 * CPL], flo
 }
 
 template <int CPL, bool CHECK, bool INIT, bool FIRST, int TW>
-__global__ __launch_bounds__(kWave * TW) __attribute__((amdgpu_waves_per_eu(CHECK ? 2 : 4, 8)))
+__global__ __launch_bounds__(kWave * TW) __attribute__((amdgpu_waves_per_eu(CHECK ? 2 : (CPL >= 8 ? 2 : (CPL >= 4 ? 3 : 4)), 8)))
 void fac_x_pass(DeviceView v, const int32_t *__restrict__ slots, int plain, int it, int nslots, int nt_i) {
   const bool nt = nt_i != 0;
   constexpr int E = 4 * CPL;
@@ -698,6 +698,7 @@ static hipError_t launch_fac_tw(const DeviceView &v, const int32_t *slots, int n
 static int fac_tile_waves(const DeviceView &v, int nslots, bool check) {
   int tw = 4;
   while (tw < 16 && (int64_t)nslots * v.F * tw < 4096) tw *= 2;
+  if (v.CPL >= 4 && tw > 8) tw = 8;   // (N > 512: 1024-thread workgroups cap a lane at 128 VGPRs, which spill)
   while (tw > 4 && fac_lds_bytes(tw, v.NP, check) > 144 * 1024) tw /= 2;
   return tw;
 }

@@ -2222,6 +2222,21 @@ int nep_debug_state(void *model, int32_t slot, double *y, double *kz, float *kty
   return NEP_OK;
 }
 
+int nep_debug_sparse_rows(void *model, int32_t slot, int32_t *anchor_cnt, int32_t *lambda_cnt) {
+  if (!model) return fail(NEP_ERR_ARG, "null model");
+  Model &m = *static_cast<Model *>(model);
+  if (slot < 0 || slot >= m.max_batch) return fail(NEP_ERR_ARG, "slot out of range");
+  const DeviceView &v = m.v;
+  const hipMemcpyKind d2h = hipMemcpyDeviceToHost;
+  if (anchor_cnt) HIPCHK(hipMemcpyAsync(anchor_cnt, v.acnt + (int64_t)slot * m.R, m.R * sizeof(int32_t), d2h, m.aux));
+  if (lambda_cnt) {
+    if (!m.fac) return fail(NEP_ERR_ARG, "not a facility-relaxation model");
+    HIPCHK(hipMemcpyAsync(lambda_cnt, v.lcnt + (int64_t)slot * m.R, m.R * sizeof(int32_t), d2h, m.aux));
+  }
+  HIPCHK(hipStreamSynchronize(m.aux));
+  return NEP_OK;
+}
+
 int nep_debug_build(const nep_model_desc *desc, double *eta, double *rho, double *gam, double *rownorm, int32_t *dims) {
   if (!desc) return fail(NEP_ERR_ARG, "null argument");
   if (desc->device_inputs) return fail(NEP_ERR_ARG, "nep_debug_build takes host arrays (device_inputs = 0)");

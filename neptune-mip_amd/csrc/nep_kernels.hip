@@ -187,13 +187,16 @@ __device__ __forceinline__ void loaded_shift(const DeviceView &v, int slot, int 
 // workgroups per CU resident);
 // measured at 512x256 / ~14 LPs per launch: 0.382 ms per launch vs 0.402 at the compiler's own 86
 // VGPRs (5 waves) and 0.428 when forced to 8 waves (64 VGPRs + 68 B/lane of spills).  The
-// certificate iterations (fp64 Lagrangian terms, 143 VGPRs) run at 3 waves per SIMD.
+// certificate iterations (fp64 Lagrangian terms, 143 VGPRs) run at 3 waves per SIMD.  N > 512 (CPL 4, 8: 16 / 32
+// destinations per lane) gets the register budget of 4 / 2 waves per SIMD: held to 6 waves those variants spilled
+// 60 (CPL 4) to 280 (CPL 8) VGPRs per lane to scratch, and the 1024x512 lone root ran its TW 8 launches at 370 us
+// (DESIGN.md §6 "N > 512").
 // FIRST: the block's first iteration, the only one (with INIT) where a restart decided at the
 // certificate iteration takes effect and the anchor is rewritten; the steady-state variant carries
 // no restart code (fewer registers live).
 template <int CPL, bool CHECK, bool INIT, bool FIRST, int TW>
 __global__ __launch_bounds__(kWave * TW) __attribute__((amdgpu_waves_per_eu(
-    CHECK ? NEP_CHECK_WAVES : (TW == 16 ? 4 : (NEP_XPASS_PREFETCH ? 5 : 6)), 8)))
+    CHECK ? NEP_CHECK_WAVES : (TW == 16 ? 4 : (CPL >= 8 ? 2 : (CPL >= 4 ? 4 : (NEP_XPASS_PREFETCH ? 5 : 6)))), 8)))
 void x_pass(DeviceView v, const int32_t *__restrict__ slots, int plain, int it, int nslots, int nt_i) {
   const bool nt = nt_i != 0;
   constexpr int E = 4 * CPL;
@@ -1619,6 +1622,7 @@ static hipError_t launch_x_tw(const DeviceView &v, const int32_t *slots, int nsl
 static int tile_waves(const DeviceView &v, int nslots, bool check) {
   int tw = 4;
   while (tw < 16 && (int64_t)nslots * v.F * tw < 4096) tw *= 2;
+  if (v.CPL >= 8 && tw > 8) tw = 8;   // (N > 1024: 1024-thread workgroups cap a lane at 128 VGPRs, which spill)
   while (check && tw > 4 && (size_t)((NEP_INLINE_REFLECT ? 5 : 4) * tw + 2) * v.NP * sizeof(float) + 4 * v.NP * sizeof(double) > 144 * 1024)
     tw /= 2;
   return tw;

@@ -22,6 +22,7 @@ cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 O=gpurun_out/$1; shift; mkdir -p "$O"
 nb=0
+npy=0
 step() {   # step <name> <seconds> <command...>: run, log, stop the call on failure
   local name=$1 secs=$2; shift 2
   echo "== $name: $*"
@@ -62,9 +63,9 @@ for r in "$@"; do
       cp /tmp/kprof_$n/*/*stats.csv "$O/" 2>/dev/null; python3 tools/prof_summary.py /tmp/kprof_$n > "$O/kprof_$n.csv"
       head -12 "$O/kprof_$n.csv" | cut -c1-160 ;;
     probe:*) a=${r#probe:}; step probe 600 python -u tools/probe.py step2_probe ${a//,/ } ;;
-    py:*) a=${r#py:}; n=${a%%,*}; n=${n%.py}
-      if [ -f "tools/probes/$n.py" ]; then step "py_$n" 600 python -u tools/probe.py ${a//,/ }
-      else step "py_$n" 600 python -u tools/${a//,/ }; fi ;;
+    py:*) a=${r#py:}; n=${a%%,*}; n=${n%.py}; npy=$((npy + 1))
+      if [ -f "tools/probes/$n.py" ]; then step "py${npy}_$n" 600 python -u tools/probe.py ${a//,/ }
+      else step "py${npy}_$n" 600 python -u tools/${a//,/ }; fi ;;
     *) echo "unknown recipe $r"; exit 2 ;;
   esac
 done
