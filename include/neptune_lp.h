@@ -237,8 +237,8 @@ int nep_lp_get_diag(void *model, int32_t slot, double *out16);
  * packed f32 duals of the x pass [F*NP+NP+4], node bounds [n_int] */
 int nep_debug_state(void *model, int32_t slot, double *y, double *kz, float *kty, double *lb, double *ub);
 /* API 12: per routing row of a slot (length R), the nonzeros its Halpern anchor is held with (17 = dense) and, on a
- * facility-relaxation model, those of its x <= c duals (17 = dense; all 17 with NEP_FAC_SPARSE_LAMBDA=0) */
-int nep_debug_sparse_rows(void *model, int32_t slot, int32_t *anchor_cnt, int32_t *lambda_cnt);
+ * facility-relaxation model, the nonzeros of its x <= c duals (counted on the host) */
+int nep_debug_sparse_rows(void *model, int32_t slot, int32_t *anchor_cnt, float *lambda_nnz);
 /* host-only model build (no device work): step size, scalings, row norms, dims = {R, F, n_int,
  * n_dual}.  Lets the CPU test-suite check the model build without a GPU. */
 int nep_debug_build(const nep_model_desc *desc, double *eta, double *rho, double *gam, double *rownorm,

@@ -685,11 +685,11 @@ class LPModel:
             "status", "active", "restart_fpr", "last_fpr", "sigma_max")
 
     def sparse_rows(self, slot):
-        """Per routing row of a slot: the nonzeros of its Halpern anchor and (facility relaxation) of its x <= c
-        duals as held on the device (kAnchorDense = 17: the row is dense)."""
+        """Per routing row of a slot: the nonzeros its Halpern anchor is held with (kAnchorDense = 17: the row is
+        dense) and (facility relaxation) the nonzeros of its x <= c duals."""
         R = self.info.n_rows
         a = np.zeros(R, np.int32)
-        lam = np.zeros(R, np.int32) if self.relaxation == RELAX_FACILITY else None
+        lam = np.zeros(R, np.float32) if self.relaxation == RELAX_FACILITY else None
         _check(self._lib, self._lib.nep_debug_sparse_rows(self._h, int(slot), _ptr(a), _ptr(lam)),
                "nep_debug_sparse_rows")
         return a, lam

@@ -25,56 +25,6 @@
 
 namespace nep {
 
-// A row held as (j, value) pairs (cnt <= kAnchorK) scattered into the lanes that own its destinations
-// (destination j lives in lane (j >> 2) & 63, register 4 * (j >> 8) + (j & 3); load_row's layout).  dst is
-// zero on entry.
-template <int E>
-__device__ __forceinline__ void scatter_pairs(const AnchorEnt *__restrict__ ent, int cnt, int lane, float (&dst)[E]) {
-  AnchorEnt ae{0, 0.f};
-  if (lane < cnt) ae = ent[lane];
-  for (int k = 0; k < cnt; ++k) {
-    const int jk = __builtin_amdgcn_readlane(ae.j, k);
-    const float vk = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ae.v), k));
-    const int ek = ((jk >> 8) << 2) | (jk & 3);   // wave-uniform
-    const bool mine = lane == ((jk >> 2) & (kWave - 1));
-#pragma unroll
-    for (int e = 0; e < E; ++e)
-      if (e == ek) dst[e] = mine ? vk : dst[e];
-  }
-}
-
-// store a row: as (j, value) pairs when it has <= kAnchorK nonzeros (returns their count), else dense
-// (returns kAnchorDense).  The pairs hold the exact fp32 values, so a read gives back the same row.
-template <int CPL>
-__device__ __forceinline__ int store_row_sparse(const float (&val)[4 * CPL], float *__restrict__ dense,
-                                                AnchorEnt *__restrict__ ent, int lane, int NP, bool nt) {
-  constexpr int E = 4 * CPL;
-  int tot = 0;
-#pragma unroll
-  for (int e = 0; e < E; ++e) tot += __popcll(__ballot(4 * (lane + kWave * (e / 4)) < NP && val[e] != 0.f));
-  if (tot <= kAnchorK) {
-    int base = 0;
-#pragma unroll
-    for (int e = 0; e < E; ++e) {
-      const bool nz = 4 * (lane + kWave * (e / 4)) < NP && val[e] != 0.f;
-      const uint64_t b = __ballot(nz);
-      if (nz) {
-        const int pos =
-            base + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
-        ent[pos] = AnchorEnt{4 * (lane + kWave * (e / 4)) + (e & 3), val[e]};
-      }
-      base += __popcll(b);
-    }
-    return tot;
-  }
-#pragma unroll
-  for (int q = 0; q < CPL; ++q) {
-    const int j0 = 4 * (lane + kWave * q);
-    if (j0 < NP) st_x4(dense + j0, f32x4{val[4 * q], val[4 * q + 1], val[4 * q + 2], val[4 * q + 3]}, nt);
-  }
-  return kAnchorDense;
-}
-
 template <int CPL, bool CHECK, bool INIT, bool FIRST, int TW>
 __global__ __launch_bounds__(kWave * TW) __attribute__((amdgpu_waves_per_eu(CHECK ? 2 : (CPL >= 8 ? 2 : (CPL >= 4 ? 3 : 4)), 8)))
 void fac_x_pass(DeviceView v, const int32_t *__restrict__ slots, int plain, int it, int nslots, int nt_i) {
@@ -107,10 +57,6 @@ void fac_x_pass(DeviceView v, const int32_t *__restrict__ slots, int plain, int 
   float *__restrict__ xa = v.xa + slot * v.sx;
   float *__restrict__ lm = v.lam + slot * v.sx;      // x <= c duals, [R][NP] like x
   float *__restrict__ lma = v.lama + slot * v.sx;    // their anchor
-  const bool lsp = NEP_FAC_SPARSE_LAMBDA && v.lam_sparse != 0;   // (rows with <= kAnchorK nonzeros as pairs)
-  int32_t *__restrict__ lcnt = v.lcnt + (int64_t)slot * v.R, *__restrict__ lacnt = v.lacnt + (int64_t)slot * v.R;
-  AnchorEnt *__restrict__ lent = v.lent + ((int64_t)slot * v.R) * kAnchorK;
-  AnchorEnt *__restrict__ laent = v.laent + ((int64_t)slot * v.R) * kAnchorK;
   int32_t *__restrict__ acnt = v.acnt + (int64_t)slot * v.R;
   AnchorEnt *__restrict__ aent = v.aent + ((int64_t)slot * v.R) * kAnchorK;
   float *__restrict__ th_row = v.theta + (int64_t)slot * v.R;
@@ -214,23 +160,19 @@ void fac_x_pass(DeviceView v, const int32_t *__restrict__ slots, int plain, int 
           if (e == ek) ac[e] = mine ? vk : ac[e];
       }
     }
-    // the row's x <= c duals and (Halpern / restart distance) their anchor, each dense or as pairs
-    const int lcn = lsp ? __builtin_amdgcn_readfirstlane(lcnt[r]) : kAnchorDense;
-    const int lan = (lsp && need_anchor) ? __builtin_amdgcn_readfirstlane(lacnt[r]) : kAnchorDense;
+    // the row's x <= c duals and (Halpern / restart distance) their anchor
     float lv[E], la[E];
 #pragma unroll
     for (int q = 0; q < CPL; ++q) {
       const int j0 = 4 * (lane + kWave * q);
       f32x4 t = {0.f, 0.f, 0.f, 0.f}, u = t;
       if (j0 < NP) {
-        if (lcn > kAnchorK) t = ld_x4(lm + (int64_t)r * NP + j0, nt);
-        if (need_anchor && lan > kAnchorK) u = ld_x4(lma + (int64_t)r * NP + j0, nt);
+        t = ld_x4(lm + (int64_t)r * NP + j0, nt);
+        if (need_anchor) u = ld_x4(lma + (int64_t)r * NP + j0, nt);
       }
       lv[4 * q] = t.x; lv[4 * q + 1] = t.y; lv[4 * q + 2] = t.z; lv[4 * q + 3] = t.w;
       la[4 * q] = u.x; la[4 * q + 1] = u.y; la[4 * q + 2] = u.z; la[4 * q + 3] = u.w;
     }
-    if (lcn <= kAnchorK) scatter_pairs<E>(lent + (int64_t)r * kAnchorK, lcn, lane, lv);
-    if (need_anchor && lan <= kAnchorK) scatter_pairs<E>(laent + (int64_t)r * kAnchorK, lan, lane, la);
     const float w = ri.w, wobj = ri.wobj;
     float vv[E];
     float s = 0.f;
@@ -323,9 +265,6 @@ void fac_x_pass(DeviceView v, const int32_t *__restrict__ slots, int plain, int 
     }
     // store x, and lambda's dual step: y' = prox(y - sigma rho^2 K(2ŵ - w)) on its row x - c <= 0, with the
     // reflected activity (2x̂ - x)[r, j] - (2ĉ - c)[f, j]; the Halpern combination as for x
-    float lnv[E];   // the row's new lambda (stored after the loop: dense or as pairs)
-#pragma unroll
-    for (int e = 0; e < E; ++e) lnv[e] = lv[e];
 #pragma unroll
     for (int q = 0; q < CPL; ++q) {
       const int j0 = 4 * (lane + kWave * q);
@@ -349,26 +288,15 @@ void fac_x_pass(DeviceView v, const int32_t *__restrict__ slots, int plain, int 
             }
           }
           ln[t] = lnew;
-          lnv[e] = lnew;
         }
         st_x4(x + (int64_t)r * NP + j0, f32x4{o[0], o[1], o[2], o[3]}, nt);
-        if (!INIT && !lsp) st_x4(lm + (int64_t)r * NP + j0, f32x4{ln[0], ln[1], ln[2], ln[3]}, nt);
-        if (restart && !lsp)
+        if (!INIT) st_x4(lm + (int64_t)r * NP + j0, f32x4{ln[0], ln[1], ln[2], ln[3]}, nt);
+        if (restart)
           st_x4(lma + (int64_t)r * NP + j0, f32x4{lv[4 * q], lv[4 * q + 1], lv[4 * q + 2], lv[4 * q + 3]}, nt);
         float4 *pl = reinterpret_cast<float4 *>(lL + wave * NP + j0);
         float4 cl = *pl;
         cl.x += ln[0]; cl.y += ln[1]; cl.z += ln[2]; cl.w += ln[3];
         *pl = cl;
-      }
-    }
-    if (lsp) {   // lambda and (at a restart) its anchor = the row's lambda before this step
-      if (!INIT) {
-        const int c = store_row_sparse<CPL>(lnv, lm + (int64_t)r * NP, lent + (int64_t)r * kAnchorK, lane, NP, nt);
-        if (lane == 0) lcnt[r] = c;
-      }
-      if (restart) {
-        const int c = store_row_sparse<CPL>(lv, lma + (int64_t)r * NP, laent + (int64_t)r * kAnchorK, lane, NP, nt);
-        if (lane == 0) lacnt[r] = c;
       }
     }
     if (restart) {

@@ -855,20 +855,6 @@ int setup_dense(Model &m, const nep_model_desc &d) {
     if ((rc = upload(m, &v.rho_l, rl))) return rc;
     HIPCHK(hipMemsetAsync(v.lam, 0, sizeof(float) * B * v.sx, m.stream));
     HIPCHK(hipMemsetAsync(v.lsum, 0, sizeof(float) * B * v.slsum, m.stream));
-    {   // sparse lambda rows (NEP_FAC_SPARSE_LAMBDA=0: always dense, for A/B)
-      const char *e = std::getenv("NEP_FAC_SPARSE_LAMBDA");
-      v.lam_sparse = (NEP_FAC_SPARSE_LAMBDA && !(e && e[0] == '0')) ? 1 : 0;
-    }
-    if ((rc = dalloc(m, &v.lcnt, (size_t)B * m.R))) return rc;
-    if ((rc = dalloc(m, &v.lacnt, (size_t)B * m.R))) return rc;
-    if ((rc = dalloc(m, &v.lent, (size_t)B * m.R * kAnchorK))) return rc;
-    if ((rc = dalloc(m, &v.laent, (size_t)B * m.R * kAnchorK))) return rc;
-    // every row starts sparse and empty (lam = 0); with lam_sparse off the counts say dense
-    {
-      std::vector<int32_t> c0((size_t)B * m.R, v.lam_sparse ? 0 : kAnchorDense);
-      HIPCHK(hipMemcpy(v.lcnt, c0.data(), c0.size() * sizeof(int32_t), hipMemcpyHostToDevice));
-      HIPCHK(hipMemcpy(v.lacnt, c0.data(), c0.size() * sizeof(int32_t), hipMemcpyHostToDevice));
-    }
   }
   if ((rc = dalloc(m, &v.rpart, (size_t)B * v.srpart))) return rc;
   if ((rc = dalloc(m, &v.ctrl, (size_t)B))) return rc;
@@ -2102,8 +2088,6 @@ int nep_lp_copy_state(void *model, int32_t src, int32_t dst) {
   if (m.fac) {   // the x <= c duals and their per-(f, j) sums travel with the state
     seg(v.lam, v.sx);
     seg(v.lsum, v.slsum);
-    seg(v.lcnt, (int64_t)m.R);
-    seg(v.lent, (int64_t)m.R * kAnchorK);
   }
   HIPCHK(launch_copy_segments(c, m.aux));
   // no host wait: every later use of src / dst is ordered behind these copies — host reads and submits run
@@ -2222,18 +2206,25 @@ int nep_debug_state(void *model, int32_t slot, double *y, double *kz, float *kty
   return NEP_OK;
 }
 
-int nep_debug_sparse_rows(void *model, int32_t slot, int32_t *anchor_cnt, int32_t *lambda_cnt) {
+int nep_debug_sparse_rows(void *model, int32_t slot, int32_t *anchor_cnt, float *lambda_nnz) {
   if (!model) return fail(NEP_ERR_ARG, "null model");
   Model &m = *static_cast<Model *>(model);
   if (slot < 0 || slot >= m.max_batch) return fail(NEP_ERR_ARG, "slot out of range");
+  if (lambda_nnz && !m.fac) return fail(NEP_ERR_ARG, "not a facility-relaxation model");
   const DeviceView &v = m.v;
   const hipMemcpyKind d2h = hipMemcpyDeviceToHost;
   if (anchor_cnt) HIPCHK(hipMemcpyAsync(anchor_cnt, v.acnt + (int64_t)slot * m.R, m.R * sizeof(int32_t), d2h, m.aux));
-  if (lambda_cnt) {
-    if (!m.fac) return fail(NEP_ERR_ARG, "not a facility-relaxation model");
-    HIPCHK(hipMemcpyAsync(lambda_cnt, v.lcnt + (int64_t)slot * m.R, m.R * sizeof(int32_t), d2h, m.aux));
+  std::vector<float> lam;
+  if (lambda_nnz) {
+    lam.resize((size_t)v.sx);
+    HIPCHK(hipMemcpyAsync(lam.data(), v.lam + slot * v.sx, lam.size() * sizeof(float), d2h, m.aux));
   }
   HIPCHK(hipStreamSynchronize(m.aux));
+  for (int r = 0; lambda_nnz && r < m.R; ++r) {   // (nonzeros of each row of the x <= c duals, host count)
+    int c = 0;
+    for (int j = 0; j < m.N; ++j) c += lam[(size_t)r * m.NP + j] != 0.f;
+    lambda_nnz[r] = (float)c;
+  }
   return NEP_OK;
 }
 

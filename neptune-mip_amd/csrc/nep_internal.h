@@ -37,12 +37,6 @@
 #ifndef NEP_SPARSE_ANCHOR
 #define NEP_SPARSE_ANCHOR 1
 #endif
-//   NEP_FAC_SPARSE_LAMBDA 1: the facility relaxation's x <= c dual rows may be held as (j, value) pairs
-//                      (DeviceView::lam_sparse; runtime switch NEP_FAC_SPARSE_LAMBDA=0 at model creation).
-//                      0 compiles the dense-only kernel of round 5 (A/B variant).
-#ifndef NEP_FAC_SPARSE_LAMBDA
-#define NEP_FAC_SPARSE_LAMBDA 1
-#endif
 
 #if defined(__HIPCC__) || defined(__HIP__)
 #define NEP_HD __host__ __device__
@@ -193,12 +187,6 @@ struct DeviceView {
   // facility relaxation (fac): the duals of x[r, j] - c[f, j] <= 0, one per routing entry ([R][NP] f32 like x),
   // their Halpern anchor, and per (f, j) their sum over the rows of f (c's reduced cost, next iteration)
   float *lam, *lama, *lsum;
-  // (lam_sparse: a lambda row with <= kAnchorK nonzeros is held as (j, value) pairs, as the x anchor is —
-  // lcnt / lent for the iterate, lacnt / laent for its anchor; kAnchorDense: the row is dense in lam / lama.
-  // Exact: the same fp32 values, 8 B per nonzero instead of NP floats; DESIGN.md §7 "Sparse facility duals")
-  int lam_sparse;
-  int32_t *lcnt, *lacnt;                 // [R] per slot
-  AnchorEnt *lent, *laent;               // [R][kAnchorK] per slot
   const float *rho_l;                    // [F][NP] row scale of those rows (the same for every row of f at j)
   int64_t slsum;
   int64_t sx, smask, sint, sdual, skty, stpart, sbpart, snpart, srpart;   // per-slot strides (elements)

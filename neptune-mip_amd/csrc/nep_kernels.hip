@@ -1489,14 +1489,9 @@ __global__ void init_slot(DeviceView v, const int32_t *__restrict__ slots, const
   if (!warm) {
     float *x = v.x + slot * v.sx;
     for (int64_t i = tid; i < (int64_t)v.R * v.NP; i += stride) x[i] = 0.f;
-    if (v.fac) {   // the x <= c duals and their sums (sparse rows: every row empty)
+    if (v.fac) {   // the x <= c duals and their sums
       float *lam = v.lam + slot * v.sx, *ls = v.lsum + slot * v.slsum;
-      if (v.lam_sparse) {
-        int32_t *lc = v.lcnt + (int64_t)slot * v.R;
-        for (int64_t i = tid; i < v.R; i += stride) lc[i] = 0;
-      } else {
-        for (int64_t i = tid; i < (int64_t)v.R * v.NP; i += stride) lam[i] = 0.f;
-      }
+      for (int64_t i = tid; i < (int64_t)v.R * v.NP; i += stride) lam[i] = 0.f;
       for (int64_t i = tid; i < v.slsum; i += stride) ls[i] = 0.f;
     }
     double *y = v.y + slot * v.sdual;

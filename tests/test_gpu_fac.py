@@ -106,36 +106,3 @@ def test_facility_relaxation_matches_highs(N, F, variant):
     finally:
         m.close()
 
-
-def test_sparse_lambda_rows_are_exact(monkeypatch):
-    """The x <= c duals' rows held as (j, value) pairs when they have <= 16 nonzeros (NEP_FAC_SPARSE_LAMBDA, the
-    default) are the same fp32 values as the dense rows: a root and warm-started children take the same iterations
-    to the same bound as with every row dense (NEP_FAC_SPARSE_LAMBDA=0)."""
-    from core.engine.lp import LPModel, RELAX_FACILITY
-    from core.utils import data_to_solver_input
-    from core.utils.synthetic import synthetic_payload
-    N, F, variant = 64, 32, "MinDelayAndUtilization"
-    p = synthetic_payload(N, F, seed=0)
-    alpha = p["solver"]["args"]["alpha"]
-    data = data_to_solver_input(p, with_db=False)
-    fix = _fixings(F, N, np.random.default_rng(7), 4)
-    B = len(fix)
-    out = {}
-    for mode in ("1", "0"):
-        monkeypatch.setenv("NEP_FAC_SPARSE_LAMBDA", mode)
-        m = LPModel(data, variant, step=1, alpha=alpha, max_batch=B + 1, relaxation=RELAX_FACILITY)
-        try:
-            rr = m.solve([B], None, None, tol=1e-6, max_iters=6000)
-            lb = np.full((B, m.n_int), -np.inf)
-            ub = np.full((B, m.n_int), np.inf)
-            for b, (idx, val) in enumerate(fix):
-                lb[b, idx] = ub[b, idx] = val
-                m.copy_state(B, b)
-            res = m.solve(np.arange(B), lb, ub, tol=1e-6, max_iters=3000, warm_start=True)
-            out[mode] = [(int(r["status"][k]), int(r["iters"][k]), float(r["obj"][k]), float(r["primal_obj"][k]))
-                         for r, n in ((rr, 1), (res, B)) for k in range(n)]
-        finally:
-            m.close()
-    print("sparse", out["1"])
-    print("dense ", out["0"])
-    assert out["1"] == out["0"]

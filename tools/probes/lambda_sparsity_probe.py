@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
-"""Dev probe (GPU box): how sparse the facility relaxation's x <= c dual rows and the routing anchors are on the
-device (nep_debug_sparse_rows: nonzeros per row as held, 17 = dense) — its root LP after a few thousand iterations
-and warm children after a branching node's budget — and the seconds per LP-iteration, so the sparse-row storage
-(NEP_FAC_SPARSE_LAMBDA) is sized on measured rows.
+"""Dev probe (GPU box): how sparse the facility relaxation's x <= c dual rows (nonzeros per row) and the routing
+anchors (nonzeros as held, 17 = dense) are (nep_debug_sparse_rows) — its root LP after a few thousand iterations and
+warm children after a branching node's budget — and the seconds per LP-iteration (DESIGN.md §7 "Sparse facility
+duals": a (j, value)-pair storage of the dual rows was built on these counts, measured and removed).
 
   python3 tools/probe.py lambda_sparsity_probe 512x256 [root_iters] [child_iters]
 """
