@@ -181,6 +181,9 @@ int nep_lp_get_solutions(void *model, int32_t n, const int32_t *slots, double *z
 int nep_lp_get_rows(void *model, int32_t slot, float *xbar, int32_t *row_f, int32_t *row_src);
 /* copy a slot's primal/dual state to another (not iterating) slot: warm start of a child node */
 int nep_lp_copy_state(void *model, int32_t src_slot, int32_t dst_slot);
+/* API 12: n such copies with the result of n nep_lp_copy_state calls in order, in as few launches as their overlaps
+ * allow (a B&B submit's warm-start copies: usually one) */
+int nep_lp_copy_states(void *model, int32_t n, const int32_t *src_slots, const int32_t *dst_slots);
 
 /* tol / cutoff of every LP in flight, effective from the next iteration block (a B&B lowers the
  * cutoff to each new incumbent without resubmitting). */
@@ -354,6 +357,8 @@ typedef struct {
   /* optional (NULL: one submit per budget / bound-stop group): nep_lp_submit_ex's contract */
   int (*submit_ex)(void *ctx, int32_t n, const int32_t *slots, const double *lb_int, const double *ub_int,
                    const nep_lp_opts *opts, const int64_t *max_iters, const double *bound_res, int32_t *status);
+  /* optional (NULL: copy_state per pair): nep_lp_copy_states' contract */
+  int (*copy_states)(void *ctx, int32_t n, const int32_t *src_slots, const int32_t *dst_slots);
 } nep_bnb_engine;
 
 /* NULL on a bad argument (nep_last_error says which): batch < 1, a layout outside n_int, no working slot left

@@ -105,6 +105,7 @@ BNB_PARAMS = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_double, ct
 BNB_FLOWS = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int32, _i32p, _fltp)
 BNB_SOLS = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int32, _i32p, _dblp)
 BNB_DIAG = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int32, _dblp)
+BNB_COPIES = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int32, _i32p, _i32p)
 BNB_SUBMIT_EX = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int32, _i32p, _dblp, _dblp,
                                  ctypes.POINTER(LpOpts), _i64p, _dblp, _i32p)
 
@@ -113,7 +114,7 @@ class BnbEngine(ctypes.Structure):
     _fields_ = [("ctx", ctypes.c_void_p), ("n_int", ctypes.c_int32), ("max_batch", ctypes.c_int32),
                 ("submit", BNB_SUBMIT), ("advance", BNB_ADVANCE), ("active", BNB_ACTIVE), ("copy_state", BNB_COPY),
                 ("set_params", BNB_PARAMS), ("get_flows", BNB_FLOWS), ("get_solutions", BNB_SOLS),
-                ("get_diag", BNB_DIAG), ("submit_ex", BNB_SUBMIT_EX)]
+                ("get_diag", BNB_DIAG), ("submit_ex", BNB_SUBMIT_EX), ("copy_states", BNB_COPIES)]
 
 
 class PyBnbEngine:
@@ -128,6 +129,7 @@ class PyBnbEngine:
         self.n_int, self.max_batch = int(model.n_int), int(model.max_batch)
         self.error = None
         self.ex_calls = 0
+        self.copies_calls = 0
         ni, mb = self.n_int, self.max_batch
         A = np.ctypeslib.as_array
 
@@ -179,6 +181,12 @@ class PyBnbEngine:
         def copy_state(_, src, dst):
             model.copy_state(int(src), int(dst))
 
+        def copy_states(_, n, src, dst):
+            # (the Python model copies pair by pair, in order: the contract of nep_lp_copy_states)
+            for a, b in zip(A(src, (n,)).tolist(), A(dst, (n,)).tolist()):
+                model.copy_state(int(a), int(b))
+            self.copies_calls += 1
+
         def set_params(_, tol, cutoff):
             model.set_params(tol, cutoff)
 
@@ -204,12 +212,13 @@ class PyBnbEngine:
         self.table = BnbEngine(None, ni, mb, BNB_SUBMIT(guard(submit)), BNB_ADVANCE(guard(advance)),
                                BNB_ACTIVE(active), BNB_COPY(guard(copy_state)), BNB_PARAMS(guard(set_params)),
                                BNB_FLOWS(guard(flows)), BNB_SOLS(guard(sols)), BNB_DIAG(guard(diag)),
-                               BNB_SUBMIT_EX(guard(submit_ex)) if per_lp else BNB_SUBMIT_EX())
+                               BNB_SUBMIT_EX(guard(submit_ex)) if per_lp else BNB_SUBMIT_EX(),
+                               BNB_COPIES(guard(copy_states)) if per_lp else BNB_COPIES())
 
 
 # every entry point declared in include/neptune_lp.h
 EXPORTS = ("nep_model_create", "nep_model_destroy", "nep_model_get_info", "nep_lp_solve_batch",
-           "nep_lp_submit", "nep_lp_submit_ex", "nep_lp_advance", "nep_lp_active",
+           "nep_lp_submit", "nep_lp_submit_ex", "nep_lp_advance", "nep_lp_active", "nep_lp_copy_states",
            "nep_lp_get_solution", "nep_lp_get_rows", "nep_lp_copy_state", "nep_get_stats", "nep_reset_stats",
            "nep_lp_get_flows_split",
            "nep_last_error", "nep_api_version", "nep_lp_get_diag", "nep_debug_build", "nep_debug_state",
@@ -261,6 +270,7 @@ def load_library(path=None):
     lib.nep_lp_get_rows.argtypes = [vp, i32, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(i32),
                                     ctypes.POINTER(i32)]
     lib.nep_lp_copy_state.argtypes = [vp, i32, i32]
+    lib.nep_lp_copy_states.argtypes = [vp, i32, vp, vp]
     lib.nep_lp_copy_routing.argtypes = [vp, i32, vp, i32]
     lib.nep_lp_get_solutions.argtypes = [vp, i32, pi32, _dp]
     lib.nep_round_leaves.argtypes = [i32, i32, _dp, _dp, ctypes.POINTER(ctypes.c_float), _dp, _dp, _dp, i32, pi32, _dp,
@@ -715,6 +725,16 @@ class LPModel:
 
     def copy_state(self, src, dst):
         _check(self._lib, self._lib.nep_lp_copy_state(self._h, int(src), int(dst)), "nep_lp_copy_state")
+
+    def copy_states(self, src, dst):
+        """copy_state(src[k], dst[k]) for every k, in order, in as few launches as the pairs allow
+        (nep_lp_copy_states)."""
+        src = np.ascontiguousarray(np.asarray(src, np.int32).reshape(-1))
+        dst = np.ascontiguousarray(np.asarray(dst, np.int32).reshape(-1))
+        if src.size != dst.size:
+            raise ValueError("copy_states: src and dst differ in length")
+        _check(self._lib, self._lib.nep_lp_copy_states(self._h, int(src.size), _ptr(src, ctypes.c_int32),
+                                                       _ptr(dst, ctypes.c_int32)), "nep_lp_copy_states")
 
     def copy_routing_from(self, other, src, dst):
         """x and thresholds of slot `src` of model `other` (same instance and rows, e.g. the facility

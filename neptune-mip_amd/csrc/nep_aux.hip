@@ -322,6 +322,40 @@ hipError_t launch_gather_solutions(const DeviceView &v, const int32_t *slots, in
   return hipGetLastError();
 }
 
+__global__ __launch_bounds__(256) void copy_slots(SlotCopyN c) {
+  const int k = blockIdx.y, q = blockIdx.z;
+  if (k >= c.nseg || q >= c.npairs) return;
+  const int64_t bytes = c.stride[k];
+  const char *src = c.base[k] + (int64_t)c.src[q] * bytes;
+  char *dst = c.base[k] + (int64_t)c.dst[q] * bytes;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if ((((uintptr_t)src | (uintptr_t)dst) & 15) == 0) {
+    const int64_t n16 = bytes >> 4;
+    const uint4 *s4 = reinterpret_cast<const uint4 *>(src);
+    uint4 *d4 = reinterpret_cast<uint4 *>(dst);
+    for (int64_t i = t0; i < n16; i += stride) d4[i] = s4[i];
+    const int64_t tail = (bytes - (n16 << 4)) >> 2;   // (< 4 words)
+    if (t0 < tail) reinterpret_cast<uint32_t *>(dst + (n16 << 4))[t0] = reinterpret_cast<const uint32_t *>(src + (n16 << 4))[t0];
+  } else {
+    const int64_t n4 = bytes >> 2;
+    const uint32_t *s1 = reinterpret_cast<const uint32_t *>(src);
+    uint32_t *d1 = reinterpret_cast<uint32_t *>(dst);
+    for (int64_t i = t0; i < n4; i += stride) d1[i] = s1[i];
+  }
+}
+
+hipError_t launch_copy_slots(const SlotCopyN &c, hipStream_t s) {
+  if (c.nseg <= 0 || c.npairs <= 0) return hipSuccess;
+  int64_t most = 0;
+  for (int k = 0; k < c.nseg; ++k) most = std::max(most, c.stride[k]);
+  // (the pairs share the chip: fewer blocks per segment the more pairs a launch carries)
+  const int64_t cap = std::max<int64_t>(16, 1024 / c.npairs);
+  const int64_t blocks = std::min<int64_t>(cap, std::max<int64_t>(1, (most / 16 + 255) / 256));
+  hipLaunchKernelGGL(copy_slots, dim3((unsigned)blocks, c.nseg, c.npairs), dim3(256), 0, s, c);
+  return hipGetLastError();
+}
+
 hipError_t launch_copy_segments(const SlotCopy &c, hipStream_t s) {
   if (c.n <= 0) return hipSuccess;
   int64_t most = 0;

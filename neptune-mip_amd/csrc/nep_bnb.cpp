@@ -151,6 +151,7 @@ int op_advance(void *c, int32_t md, int32_t *nd, int32_t *sl, double *ob, double
 }
 int op_active(void *c) { return nep_lp_active(c); }
 int op_copy(void *c, int32_t a, int32_t b) { return nep_lp_copy_state(c, a, b); }
+int op_copies(void *c, int32_t n, const int32_t *a, const int32_t *b) { return nep_lp_copy_states(c, n, a, b); }
 int op_params(void *c, double tol, double cut) { return nep_lp_set_params(c, tol, cut); }
 int op_flows(void *c, int32_t n, const int32_t *sl, float *f) { return nep_lp_get_flows(c, n, sl, f); }
 int op_sols(void *c, int32_t n, const int32_t *sl, double *z) { return nep_lp_get_solutions(c, n, sl, z); }
@@ -173,6 +174,7 @@ int model_ops(void *lp, nep_bnb_engine *out) {
   out->get_solutions = op_sols;
   out->get_diag = op_diag;
   out->submit_ex = op_submit_ex;
+  out->copy_states = op_copies;
   return NEP_OK;
 }
 
@@ -229,7 +231,7 @@ struct NepBnb {
   int64_t agreed_open = 0;
   bool stalled = false;      // nothing could be submitted and nothing was in flight (ends the search)
   // scratch
-  std::vector<int32_t> sl, done_slots, sts;
+  std::vector<int32_t> sl, done_slots, sts, cp_src, cp_dst;
   std::vector<double> obj, pobj, lbv, ubv;
   std::vector<int64_t> its;
 
@@ -369,6 +371,8 @@ int NepBnb::submit(std::vector<std::pair<Engine *, std::pair<int, NodeP>>> &item
   for (int e = 0; e < 2; ++e) {
     Engine *eng = e == 0 ? &L : &B;
     auto &cps = copies[e];
+    cp_src.clear();
+    cp_dst.clear();
     while (!cps.empty()) {
       size_t k = cps.size();
       for (size_t i = 0; i < cps.size() && k == cps.size(); ++i) {
@@ -382,8 +386,18 @@ int NepBnb::submit(std::vector<std::pair<Engine *, std::pair<int, NodeP>>> &item
       }
       const auto c = cps[k];
       cps.erase(cps.begin() + k);
-      int rc = eng->ops.copy_state(eng->ops.ctx, c.first, c.second);
+      cp_src.push_back(c.first);
+      cp_dst.push_back(c.second);
+    }
+    // in that order: one call (nep_lp_copy_states: as few launches as the overlaps allow), else one per pair
+    if (!cp_src.empty() && eng->ops.copy_states) {
+      int rc = eng->ops.copy_states(eng->ops.ctx, (int)cp_src.size(), cp_src.data(), cp_dst.data());
       if (rc) return rc;
+    } else {
+      for (size_t q = 0; q < cp_src.size(); ++q) {
+        int rc = eng->ops.copy_state(eng->ops.ctx, cp_src[q], cp_dst[q]);
+        if (rc) return rc;
+      }
     }
   }
   for (auto &g : groups) {

@@ -44,6 +44,7 @@ hipError_t launch_compact_f64(const double *vals, int rows, int cols, int64_t ld
                               int32_t *cnt, int32_t *off, int32_t *orow, int32_t *ocol, double *oval, bool count_only,
                               hipStream_t s);
 hipError_t launch_copy_segments(const SlotCopy &c, hipStream_t s);
+hipError_t launch_copy_slots(const SlotCopyN &c, hipStream_t s);
 hipError_t launch_gather_solutions(const DeviceView &v, const int32_t *slots, int n, int ni, double *out,
                                    hipStream_t s);
 hipError_t launch_power_iteration(const DeviceView &v, int iters, double *zx, double *zs, double *gx, double *gs,
@@ -2093,6 +2094,63 @@ int nep_lp_copy_state(void *model, int32_t src, int32_t dst) {
   // no host wait: every later use of src / dst is ordered behind these copies — host reads and submits run
   // on `aux`, and a slot iterates on `stream` only after its submit's initialisation (ev_aux)
   return NEP_OK;
+}
+
+int nep_lp_copy_states(void *model, int32_t n, const int32_t *src, const int32_t *dst) {
+  if (!model) return fail(NEP_ERR_ARG, "null model");
+  if (n < 0 || (n > 0 && (!src || !dst))) return fail(NEP_ERR_ARG, "null argument");
+  Model &m = *static_cast<Model *>(model);
+  for (int k = 0; k < n; ++k) {
+    if (src[k] < 0 || dst[k] < 0 || src[k] >= m.max_batch || dst[k] >= m.max_batch)
+      return fail(NEP_ERR_ARG, "slot out of range");
+    if (m.busy[dst[k]]) return fail(NEP_ERR_STATE, "destination slot is still iterating");
+    if (m.busy[src[k]]) return fail(NEP_ERR_STATE, "source slot is still iterating");
+  }
+  const DeviceView &v = m.v;
+  SlotCopyN c{};
+  auto seg = [&](auto *base, int64_t stride) {
+    c.base[c.nseg] = reinterpret_cast<char *>(base);
+    c.stride[c.nseg] = stride * (int64_t)sizeof(*base);
+    ++c.nseg;
+  };
+  // the arrays nep_lp_copy_state copies
+  seg(v.x, v.sx);
+  seg(v.theta, (int64_t)m.R);
+  seg(v.zi, v.sint);
+  seg(v.y, v.sdual);
+  seg(v.kty, v.skty);
+  seg(v.zr, v.sint);
+  seg(v.rpart, v.srpart);
+  seg(v.ctrl, (int64_t)1);
+  if (m.fac) {
+    seg(v.lam, v.sx);
+    seg(v.lsum, v.slsum);
+  }
+  // the same result as n nep_lp_copy_state calls in order: a launch takes pairs while none of them reads or writes
+  // a slot an earlier pair of the launch writes, or writes a slot an earlier pair reads
+  std::vector<int32_t> rd, wr;
+  auto flush = [&]() -> int {
+    if (c.npairs) HIPCHK(launch_copy_slots(c, m.aux));
+    c.npairs = 0;
+    rd.clear();
+    wr.clear();
+    return NEP_OK;
+  };
+  auto has = [](const std::vector<int32_t> &a, int32_t x) { return std::find(a.begin(), a.end(), x) != a.end(); };
+  for (int k = 0; k < n; ++k) {
+    if (src[k] == dst[k]) continue;
+    if (c.npairs == SlotCopyN::kPairs || has(wr, src[k]) || has(wr, dst[k]) || has(rd, dst[k])) {
+      const int rc = flush();
+      if (rc) return rc;
+    }
+    c.src[c.npairs] = src[k];
+    c.dst[c.npairs] = dst[k];
+    ++c.npairs;
+    rd.push_back(src[k]);
+    wr.push_back(dst[k]);
+  }
+  // (no host wait, as nep_lp_copy_state)
+  return flush();
 }
 
 int nep_lp_copy_routing(void *dst_model, int32_t dst_slot, void *src_model, int32_t src_slot) {

@@ -216,5 +216,14 @@ struct SlotCopy {
   int64_t bytes[kMax];
   int n;
 };
+// several slot-state copies in one launch (nep_lp_copy_states): per segment the array base and the slot stride in
+// bytes, per pair the source and destination slot; no pair reads or writes a slot another pair of the launch writes
+struct SlotCopyN {
+  static constexpr int kSeg = 12, kPairs = 32;
+  char *base[kSeg];
+  int64_t stride[kSeg];
+  int32_t src[kPairs], dst[kPairs];
+  int nseg, npairs;
+};
 
 }  // namespace nep

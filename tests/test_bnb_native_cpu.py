@@ -148,9 +148,10 @@ def test_sharded_native_tree_rebalances_idle_ranks():
 
 @pytest.mark.parametrize("branching", [0, 2])
 def test_native_tree_per_lp_budgets_merge_submit_groups(monkeypatch, branching):
-    """API 12 submit_ex: with per-LP budgets / bound stops the tree submits once per (engine, warm, check_every)
-    group instead of once per (budget, bound stop) too — strong-branching probes, children and re-solves go in one
-    call.  The search must end where the per-budget grouping ends (same status, objective and vector)."""
+    """API 12 submit_ex / copy_states: with per-LP budgets / bound stops the tree submits once per (engine, warm,
+    check_every) group instead of once per (budget, bound stop) too — strong-branching probes, children and re-solves
+    go in one call — and makes a submit's warm-start copies in one call.  The search must end where the per-budget,
+    per-copy form ends (same status, objective and vector)."""
     import core.engine.lp as lpmod
     made = []
 
@@ -168,4 +169,5 @@ def test_native_tree_per_lp_budgets_merge_submit_groups(monkeypatch, branching):
         res = _search(name, True, branching=branching)
         out[per_lp] = (res.status, res.objective, None if res.z is None else np.asarray(res.z).tolist())
         assert made and (made[0].ex_calls > 0) == per_lp
+        assert (made[0].copies_calls > 0) == per_lp   # (warm-start copies through copy_states)
     assert out[True] == out[False]

@@ -92,3 +92,36 @@ def test_submit_ex_per_lp_budgets_match_separate_submits():
     for s in (1, 3):
         assert per[s][0] == LP_OPTIMAL
         assert abs(per[s][2] - ref) <= TOL * max(1.0, abs(ref))
+
+
+
+def test_copy_states_equals_copies_in_order():
+    """API 12 nep_lp_copy_states: a chain of warm-start copies in one call (a destination read by a later pair, a
+    source overwritten by a later pair) leaves every slot as the same copies made one nep_lp_copy_state at a time."""
+    from core.engine.lp import LPModel
+    name, k = "payload", 0
+    data, variant, step, kw = build_args(name, k)
+    src, dst = [0, 3, 1, 2, 4], [3, 4, 0, 5, 2]
+    states = []
+    for batched in (True, False):
+        m = LPModel(data, variant, step=step, max_batch=6, **kw)
+        lb = np.full((3, m.n_int), -np.inf)
+        ub = np.full((3, m.n_int), np.inf)
+        for b in range(3):
+            lb[b, b] = ub[b, b] = 0.0
+        m.solve(np.arange(3), lb, ub, tol=1e-7, max_iters=96, check_every=32)
+        if batched:
+            m.copy_states(src, dst)
+        else:
+            for a, b in zip(src, dst):
+                m.copy_state(a, b)
+        got = []
+        for sl in range(6):
+            z, _ = m.solution(sl, dense_x=False)
+            d = m.diag(sl)
+            got.append((sl, z.tobytes(), m.rows(sl)[0].tobytes(), d["omega"], d["k"]))
+        states.append(got)
+        m.close()
+    # the chain's expected sources: 0 <- 1, 2 <- 0 (via 3, 4), 3 <- 0, 4 <- 0, 5 <- 2
+    assert states[0] == states[1]
+    assert states[0][2][1:] == states[0][3][1:] == states[0][4][1:]
