@@ -21,6 +21,8 @@
 #include <chrono>
 #include <cmath>
 #include <cstdint>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <limits>
@@ -184,6 +186,18 @@ struct NepBnb {
   nep_bnb_params p{};
   Engine L, B;
   bool two = false;
+  // NEP_BNB_PROFILE=1: host seconds per section, printed to stderr when the tree is destroyed (dev measurement)
+  bool prof = false;
+  double pr_round = 0, pr_reads = 0, pr_copies = 0, pr_submit = 0, pr_finish = 0;
+  int64_t pr_submit_calls = 0, pr_copy_calls = 0, pr_reads_calls = 0, pr_rounds = 0;
+  ~NepBnb() {
+    if (prof)
+      std::fprintf(stderr,
+                   "[nep_bnb profile] lps %lld | submit calls %lld %.3fs, copies calls %lld %.3fs | reads calls %lld "
+                   "%.3fs | rounding nodes %lld %.3fs | finish_one %.3fs\n",
+                   (long long)st.lps, (long long)pr_submit_calls, pr_submit, (long long)pr_copy_calls, pr_copies,
+                   (long long)pr_reads_calls, pr_reads, (long long)pr_rounds, pr_round, pr_finish);
+  }
   std::vector<double> fn_mem, node_mem;
   std::priority_queue<HeapItem, std::vector<HeapItem>, std::greater<HeapItem>> heap;
   std::deque<NodeP> pending, retry;
@@ -390,6 +404,8 @@ int NepBnb::submit(std::vector<std::pair<Engine *, std::pair<int, NodeP>>> &item
       cp_dst.push_back(c.second);
     }
     // in that order: one call (nep_lp_copy_states: as few launches as the overlaps allow), else one per pair
+    const double tc = prof ? now_s() : 0.0;
+    if (prof && !cp_src.empty()) ++pr_copy_calls;
     if (!cp_src.empty() && eng->ops.copy_states) {
       int rc = eng->ops.copy_states(eng->ops.ctx, (int)cp_src.size(), cp_src.data(), cp_dst.data());
       if (rc) return rc;
@@ -399,6 +415,7 @@ int NepBnb::submit(std::vector<std::pair<Engine *, std::pair<int, NodeP>>> &item
         if (rc) return rc;
       }
     }
+    if (prof) pr_copies += now_s() - tc;
   }
   for (auto &g : groups) {
     const int n = (int)g.its.size(), ni = g.eng->n_int;
@@ -423,10 +440,12 @@ int NepBnb::submit(std::vector<std::pair<Engine *, std::pair<int, NodeP>>> &item
     o.bound_res = g.br[0];
     sts.assign(n, 0);
     // (a bound-stop entry of 0 means none: nep_lp_submit_ex reads entries <= 0 that way)
+    const double ts = prof ? now_s() : 0.0;
     int rc = g.eng->ops.submit_ex
                  ? g.eng->ops.submit_ex(g.eng->ops.ctx, n, sl.data(), lbv.data(), ubv.data(), &o, g.mi.data(),
                                         g.br.data(), sts.data())
                  : g.eng->ops.submit(g.eng->ops.ctx, n, sl.data(), lbv.data(), ubv.data(), &o, sts.data());
+    if (prof) { pr_submit += now_s() - ts; ++pr_submit_calls; }
     if (rc) return rc;
     for (int b = 0; b < n; ++b) {
       const int slot = sl[b];
@@ -930,7 +949,11 @@ int NepBnb::finish_one(Engine &eng, int slot, const NodeP &node, int status, dou
   }
   st.nodes += 1;
   const Parent me{&eng, slot, eng.gen[slot]};
-  round_all(*node, flow, z, bound, me);
+  {
+    const double t0 = prof ? now_s() : 0.0;
+    round_all(*node, flow, z, bound, me);
+    if (prof) { pr_round += now_s() - t0; ++pr_rounds; }
+  }
   if (p.primal_at_root && node->depth == 0 && !root_event_done) {
     // the caller's primal heuristic runs on this node's LP (z, flows) before the search goes on
     root_event_pending = true;
@@ -983,10 +1006,12 @@ int NepBnb::finish_block(Engine &eng, int nd) {
   std::vector<float> fl(want.size() * FN);
   std::vector<double> zs(want.size() * ni);
   if (!want.empty()) {
+    const double t0 = prof ? now_s() : 0.0;
     int rc = eng.ops.get_flows(eng.ops.ctx, (int)want.size(), want.data(), fl.data());
     if (rc) return rc;
     rc = eng.ops.get_solutions(eng.ops.ctx, (int)want.size(), want.data(), zs.data());
     if (rc) return rc;
+    if (prof) { pr_reads += now_s() - t0; ++pr_reads_calls; }
   }
   // (copies: finish_one may submit nothing, but the outputs are reused by later advances)
   const std::vector<int32_t> ds(done_slots.begin(), done_slots.begin() + nd);
@@ -1015,7 +1040,9 @@ int NepBnb::finish_block(Engine &eng, int nd) {
       f = fl1.data();
       z = z1.data();
     }
+    const double t0 = prof ? now_s() : 0.0;
     int rc = finish_one(eng, slot, node, ss[i], ob[i], po[i], it[i], f, z);
+    if (prof) pr_finish += now_s() - t0;
     if (rc) return rc;
   }
   return NEP_OK;
@@ -1150,6 +1177,10 @@ void *nep_bnb_create_engines(const nep_bnb_engine *leaf, const nep_bnb_engine *b
     return nullptr;
   }
   auto *t = new NepBnb();
+  {
+    const char *e = std::getenv("NEP_BNB_PROFILE");
+    t->prof = e && e[0] == '1';
+  }
   t->p = *params;
   t->two = bound != nullptr;
   t->fn_mem.assign(fn_mem, fn_mem + params->F);

@@ -104,6 +104,11 @@ struct PresolveScratch {
 };
 
 struct Model {
+  // NEP_HOST_PROFILE=1: host seconds of nep_lp_submit (presolve / staging + launches) and nep_lp_advance,
+  // printed to stderr when the model is destroyed (dev measurement)
+  bool prof = false;
+  double pr_pre = 0, pr_stage = 0, pr_adv = 0;
+  int64_t pr_calls = 0, pr_lps = 0, pr_adv_calls = 0;
   // problem
   int N = 0, F = 0, NP = 0, variant = 0, step = 1, has_n = 0, step2 = 0;
   int fac = 0;                      // NEP_RELAX_FACILITY (include/neptune_lp.h)
@@ -1460,7 +1465,20 @@ int submit(Model &m, int n, const int32_t *slots, const double *lbi, const doubl
   // tol / cutoff of every LP in flight: device memory, read by the (graph-replayed) blocks
   HIPCHK(set_prm(m, o.tol, o.cutoff, o.gap_tol));
   std::vector<NodeBox> box;
+  const auto tp0 = std::chrono::steady_clock::now();
   presolve_batch(m, n, lbi, ubi, box);
+  if (m.prof) {
+    m.pr_pre += std::chrono::duration<double>(std::chrono::steady_clock::now() - tp0).count();
+    ++m.pr_calls;
+    m.pr_lps += n;
+  }
+  struct StageTimer {   // (the rest of the call: staging and launches)
+    Model &m;
+    std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+    ~StageTimer() {
+      if (m.prof) m.pr_stage += std::chrono::duration<double>(std::chrono::steady_clock::now() - t).count();
+    }
+  } stage_timer{m};
   for (int b = 0; b < n; ++b)
     if (box[b].bad)
       return fail(NEP_ERR_ARG, "step-2 node box " + std::to_string(b) +
@@ -1924,11 +1942,19 @@ int nep_model_create(const nep_model_desc *desc_in, int32_t max_batch, void *hip
   if (rc) return rc;
   if (!host_power && (rc = power_device(*m))) return rc;
   if (const char *e = std::getenv("NEP_ETA_SCALE")) m->eta *= std::atof(e);   // (probe: tools/probes/root_chaos_probe.py)
+  if (const char *e = std::getenv("NEP_HOST_PROFILE")) m->prof = e[0] == '1';
   *out_model = m.release();
   return NEP_OK;
 }
 
-void nep_model_destroy(void *model) { delete static_cast<Model *>(model); }
+void nep_model_destroy(void *model) {
+  Model *m = static_cast<Model *>(model);
+  if (m && m->prof)
+    std::fprintf(stderr, "[nep_lp profile] %dx%d%s | submit calls %lld lps %lld presolve %.3fs staging+launch %.3fs | "
+                 "advance calls %lld %.3fs\n", m->N, m->F, m->fac ? " fac" : "", (long long)m->pr_calls,
+                 (long long)m->pr_lps, m->pr_pre, m->pr_stage, (long long)m->pr_adv_calls, m->pr_adv);
+  delete m;
+}
 
 int nep_model_get_info(void *model, nep_model_info *info) {
   if (!model || !info) return fail(NEP_ERR_ARG, "null argument");
@@ -1972,7 +1998,9 @@ int nep_lp_advance(void *model, int32_t min_done, int32_t *n_done, int32_t *done
   auto t0 = std::chrono::steady_clock::now();
   Model &m = *static_cast<Model *>(model);
   const int rc = advance(m, min_done, n_done, done_slots, obj, primal_obj, status, iters);
-  m.stats.solve_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  m.stats.solve_ms += 1e3 * dt;
+  if (m.prof) { m.pr_adv += dt; ++m.pr_adv_calls; }
   return rc;
 }
 
