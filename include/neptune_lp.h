@@ -176,6 +176,8 @@ int nep_lp_get_solution(void *model, int32_t slot, double *z_int, float *x_dense
 /* API 8: z_int of n finished slots at once (z_out [n][n_int], each as nep_lp_get_solution's): one device
  * round trip for all the branching nodes an advance returned. */
 int nep_lp_get_solutions(void *model, int32_t n, const int32_t *slots, double *z_out);
+/* API 12: nep_lp_get_flows and nep_lp_get_solutions of the same n slots in one device round trip (one wait) */
+int nep_lp_get_flows_solutions(void *model, int32_t n, const int32_t *slots, float *flows, double *z_out);
 /* aggregated routing rows (host float, R*N) and the row map (row_f, row_src; src = -1: pooled
  * zero-workload sources of function f, each routed identically). */
 int nep_lp_get_rows(void *model, int32_t slot, float *xbar, int32_t *row_f, int32_t *row_src);
@@ -359,6 +361,8 @@ typedef struct {
                    const nep_lp_opts *opts, const int64_t *max_iters, const double *bound_res, int32_t *status);
   /* optional (NULL: copy_state per pair): nep_lp_copy_states' contract */
   int (*copy_states)(void *ctx, int32_t n, const int32_t *src_slots, const int32_t *dst_slots);
+  /* optional (NULL: get_flows, then get_solutions): nep_lp_get_flows_solutions' contract */
+  int (*get_flows_solutions)(void *ctx, int32_t n, const int32_t *slots, float *flows, double *z_out);
 } nep_bnb_engine;
 
 /* NULL on a bad argument (nep_last_error says which): batch < 1, a layout outside n_int, no working slot left

@@ -106,6 +106,7 @@ BNB_FLOWS = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int32, _i32
 BNB_SOLS = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int32, _i32p, _dblp)
 BNB_DIAG = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int32, _dblp)
 BNB_COPIES = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int32, _i32p, _i32p)
+BNB_FLOWS_SOLS = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int32, _i32p, _fltp, _dblp)
 BNB_SUBMIT_EX = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int32, _i32p, _dblp, _dblp,
                                  ctypes.POINTER(LpOpts), _i64p, _dblp, _i32p)
 
@@ -114,7 +115,8 @@ class BnbEngine(ctypes.Structure):
     _fields_ = [("ctx", ctypes.c_void_p), ("n_int", ctypes.c_int32), ("max_batch", ctypes.c_int32),
                 ("submit", BNB_SUBMIT), ("advance", BNB_ADVANCE), ("active", BNB_ACTIVE), ("copy_state", BNB_COPY),
                 ("set_params", BNB_PARAMS), ("get_flows", BNB_FLOWS), ("get_solutions", BNB_SOLS),
-                ("get_diag", BNB_DIAG), ("submit_ex", BNB_SUBMIT_EX), ("copy_states", BNB_COPIES)]
+                ("get_diag", BNB_DIAG), ("submit_ex", BNB_SUBMIT_EX), ("copy_states", BNB_COPIES),
+                ("get_flows_solutions", BNB_FLOWS_SOLS)]
 
 
 class PyBnbEngine:
@@ -130,6 +132,7 @@ class PyBnbEngine:
         self.error = None
         self.ex_calls = 0
         self.copies_calls = 0
+        self.flows_sols_calls = 0
         ni, mb = self.n_int, self.max_batch
         A = np.ctypeslib.as_array
 
@@ -196,6 +199,11 @@ class PyBnbEngine:
         def sols(_, n, slots, out):
             A(out, (n * ni,))[:] = np.asarray(model.solutions(A(slots, (n,)).copy()), np.float64).ravel()
 
+        def flows_sols(_, n, slots, fout, zout):
+            flows(_, n, slots, fout)
+            sols(_, n, slots, zout)
+            self.flows_sols_calls += 1
+
         def diag(_, slot, out):
             d = model.diag(int(slot))
             o = A(out, (16,))
@@ -213,12 +221,13 @@ class PyBnbEngine:
                                BNB_ACTIVE(active), BNB_COPY(guard(copy_state)), BNB_PARAMS(guard(set_params)),
                                BNB_FLOWS(guard(flows)), BNB_SOLS(guard(sols)), BNB_DIAG(guard(diag)),
                                BNB_SUBMIT_EX(guard(submit_ex)) if per_lp else BNB_SUBMIT_EX(),
-                               BNB_COPIES(guard(copy_states)) if per_lp else BNB_COPIES())
+                               BNB_COPIES(guard(copy_states)) if per_lp else BNB_COPIES(),
+                               BNB_FLOWS_SOLS(guard(flows_sols)) if per_lp else BNB_FLOWS_SOLS())
 
 
 # every entry point declared in include/neptune_lp.h
 EXPORTS = ("nep_model_create", "nep_model_destroy", "nep_model_get_info", "nep_lp_solve_batch",
-           "nep_lp_submit", "nep_lp_submit_ex", "nep_lp_advance", "nep_lp_active", "nep_lp_copy_states",
+           "nep_lp_submit", "nep_lp_submit_ex", "nep_lp_advance", "nep_lp_active", "nep_lp_copy_states", "nep_lp_get_flows_solutions",
            "nep_lp_get_solution", "nep_lp_get_rows", "nep_lp_copy_state", "nep_get_stats", "nep_reset_stats",
            "nep_lp_get_flows_split",
            "nep_last_error", "nep_api_version", "nep_lp_get_diag", "nep_debug_build", "nep_debug_state",
@@ -271,6 +280,7 @@ def load_library(path=None):
                                     ctypes.POINTER(i32)]
     lib.nep_lp_copy_state.argtypes = [vp, i32, i32]
     lib.nep_lp_copy_states.argtypes = [vp, i32, vp, vp]
+    lib.nep_lp_get_flows_solutions.argtypes = [vp, i32, vp, vp, vp]
     lib.nep_lp_copy_routing.argtypes = [vp, i32, vp, i32]
     lib.nep_lp_get_solutions.argtypes = [vp, i32, pi32, _dp]
     lib.nep_round_leaves.argtypes = [i32, i32, _dp, _dp, ctypes.POINTER(ctypes.c_float), _dp, _dp, _dp, i32, pi32, _dp,
@@ -637,6 +647,16 @@ class LPModel:
         """tol / cutoff of every LP in flight (nep_lp_set_params): a B&B lowers the cutoff to each new
         incumbent without resubmitting."""
         _check(self._lib, self._lib.nep_lp_set_params(self._h, float(tol), float(cutoff)), "nep_lp_set_params")
+
+    def flows_solutions(self, slots):
+        """(flows(slots), solutions(slots)) in one device round trip (nep_lp_get_flows_solutions)."""
+        slots = np.ascontiguousarray(np.asarray(slots, dtype=np.int32).reshape(-1))
+        fl = np.zeros((len(slots), self.F, self.N), np.float32)
+        z = np.zeros((len(slots), self.n_int))
+        _check(self._lib, self._lib.nep_lp_get_flows_solutions(self._h, len(slots), _ptr(slots, ctypes.c_int32),
+                                                               _ptr(fl, ctypes.c_float), _ptr(z)),
+               "nep_lp_get_flows_solutions")
+        return fl, z
 
     def flows(self, slots, split=False):
         """flow[b, f, j] = sum_i x[i, f, j] of finished slots, reduced on the device (nep_lp_get_flows);

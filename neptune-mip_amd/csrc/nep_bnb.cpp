@@ -154,6 +154,9 @@ int op_advance(void *c, int32_t md, int32_t *nd, int32_t *sl, double *ob, double
 int op_active(void *c) { return nep_lp_active(c); }
 int op_copy(void *c, int32_t a, int32_t b) { return nep_lp_copy_state(c, a, b); }
 int op_copies(void *c, int32_t n, const int32_t *a, const int32_t *b) { return nep_lp_copy_states(c, n, a, b); }
+int op_flows_sols(void *c, int32_t n, const int32_t *sl, float *f, double *z) {
+  return nep_lp_get_flows_solutions(c, n, sl, f, z);
+}
 int op_params(void *c, double tol, double cut) { return nep_lp_set_params(c, tol, cut); }
 int op_flows(void *c, int32_t n, const int32_t *sl, float *f) { return nep_lp_get_flows(c, n, sl, f); }
 int op_sols(void *c, int32_t n, const int32_t *sl, double *z) { return nep_lp_get_solutions(c, n, sl, z); }
@@ -177,6 +180,7 @@ int model_ops(void *lp, nep_bnb_engine *out) {
   out->get_diag = op_diag;
   out->submit_ex = op_submit_ex;
   out->copy_states = op_copies;
+  out->get_flows_solutions = op_flows_sols;
   return NEP_OK;
 }
 
@@ -204,6 +208,7 @@ struct NepBnb {
   std::vector<NodeP> seeds;   // seed leaves, queued when the root finishes
   NodeP refroot;
   std::unordered_set<std::string> seen;
+  std::vector<int32_t> leaf_idx;   // the variables a rounding leaf fixes (built at the first one)
   std::vector<double> unresolved_bounds;
   std::vector<int64_t> lp_iters;
   int64_t seq = 0;
@@ -821,13 +826,15 @@ void NepBnb::round_all(const Node &node, const float *flow, const double *z, dou
     leaf->kind = LEAF;
     leaf->parent = me;
     leaf->depth = node.depth + 1;
-    leaf->idx.reserve(nb());
-    for (int k = p.c0; k < p.c1; ++k) leaf->idx.push_back(k);
-    leaf->val.assign(cout.begin() + (size_t)q * FN, cout.begin() + (size_t)(q + 1) * FN);
-    if (p.n0 >= 0) {
-      for (int k = p.n0; k < p.n1; ++k) leaf->idx.push_back(k);
-      leaf->val.insert(leaf->val.end(), nout.begin() + (size_t)q * N, nout.begin() + (size_t)(q + 1) * N);
+    if (leaf_idx.empty()) {   // (every rounding leaf fixes the same variables: every c, then every n)
+      for (int k = p.c0; k < p.c1; ++k) leaf_idx.push_back(k);
+      if (p.n0 >= 0)
+        for (int k = p.n0; k < p.n1; ++k) leaf_idx.push_back(k);
     }
+    leaf->idx = leaf_idx;
+    leaf->val.reserve(leaf_idx.size());
+    leaf->val.assign(cout.begin() + (size_t)q * FN, cout.begin() + (size_t)(q + 1) * FN);
+    if (p.n0 >= 0) leaf->val.insert(leaf->val.end(), nout.begin() + (size_t)q * N, nout.begin() + (size_t)(q + 1) * N);
     if (!seen.insert(key_of(leaf->val)).second) continue;
     leaf->bound = std::max(bound, ibound(leaf->idx, leaf->val));
     if (!pruned(leaf->bound)) pending.push_back(leaf);
@@ -1007,9 +1014,13 @@ int NepBnb::finish_block(Engine &eng, int nd) {
   std::vector<double> zs(want.size() * ni);
   if (!want.empty()) {
     const double t0 = prof ? now_s() : 0.0;
-    int rc = eng.ops.get_flows(eng.ops.ctx, (int)want.size(), want.data(), fl.data());
-    if (rc) return rc;
-    rc = eng.ops.get_solutions(eng.ops.ctx, (int)want.size(), want.data(), zs.data());
+    int rc;
+    if (eng.ops.get_flows_solutions) {
+      rc = eng.ops.get_flows_solutions(eng.ops.ctx, (int)want.size(), want.data(), fl.data(), zs.data());
+    } else {
+      rc = eng.ops.get_flows(eng.ops.ctx, (int)want.size(), want.data(), fl.data());
+      if (!rc) rc = eng.ops.get_solutions(eng.ops.ctx, (int)want.size(), want.data(), zs.data());
+    }
     if (rc) return rc;
     if (prof) { pr_reads += now_s() - t0; ++pr_reads_calls; }
   }
@@ -1034,8 +1045,9 @@ int NepBnb::finish_block(Engine &eng, int nd) {
       // (the incumbent improved within this block: read it now)
       fl1.resize(FN);
       z1.resize(ni);
-      int rc = eng.ops.get_flows(eng.ops.ctx, 1, &slot, fl1.data());
-      if (!rc) rc = eng.ops.get_solutions(eng.ops.ctx, 1, &slot, z1.data());
+      int rc = eng.ops.get_flows_solutions ? eng.ops.get_flows_solutions(eng.ops.ctx, 1, &slot, fl1.data(), z1.data())
+                                           : eng.ops.get_flows(eng.ops.ctx, 1, &slot, fl1.data());
+      if (!rc && !eng.ops.get_flows_solutions) rc = eng.ops.get_solutions(eng.ops.ctx, 1, &slot, z1.data());
       if (rc) return rc;
       f = fl1.data();
       z = z1.data();

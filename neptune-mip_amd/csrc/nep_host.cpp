@@ -2038,6 +2038,46 @@ int nep_lp_get_solutions(void *model, int32_t n, const int32_t *slots, double *z
   return NEP_OK;
 }
 
+int nep_lp_get_flows_solutions(void *model, int32_t n, const int32_t *slots, float *flows_out, double *z_out) {
+  if (!model || (n > 0 && (!slots || !flows_out || !z_out))) return fail(NEP_ERR_ARG, "null argument");
+  Model &m = *static_cast<Model *>(model);
+  if (n <= 0) return NEP_OK;
+  if (n > m.max_batch) return fail(NEP_ERR_ARG, "n > max_batch");
+  for (int b = 0; b < n; ++b) {
+    if (slots[b] < 0 || slots[b] >= m.max_batch) return fail(NEP_ERR_ARG, "slot out of range");
+    if (m.busy[slots[b]]) return fail(NEP_ERR_STATE, "slot is still iterating");
+  }
+  const size_t ni = (size_t)m.il.n_int, plane = (size_t)m.max_batch * m.F * m.N;
+  int rc;
+  if (!m.d_flows && (rc = dalloc(m, &m.d_flows, 2 * plane))) return rc;
+  if (!m.d_sols && (rc = dalloc(m, &m.d_sols, (size_t)m.max_batch * ni))) return rc;
+  if (!m.h_flows) {
+    void *h = nullptr;
+    if (hipHostMalloc(&h, sizeof(float) * 2 * plane + sizeof(int32_t) * m.max_batch) != hipSuccess)
+      return fail(NEP_ERR_NOMEM, "hipHostMalloc (flows)");
+    m.h_flows = static_cast<float *>(h);
+  }
+  if (!m.h_sols) {
+    void *hp = nullptr;
+    if (hipHostMalloc(&hp, sizeof(double) * m.max_batch * (ni + 1)) != hipSuccess)
+      return fail(NEP_ERR_NOMEM, "hipHostMalloc (solutions)");
+    m.h_sols = static_cast<double *>(hp);
+  }
+  // nep_lp_get_flows + nep_lp_get_solutions with one slot list, both gathers and one wait
+  int32_t *hs = reinterpret_cast<int32_t *>(m.h_flows + 2 * plane);
+  std::memcpy(hs, slots, n * sizeof(int32_t));
+  const size_t cnt = (size_t)n * m.F * m.N;
+  HIPCHK(hipMemcpyAsync(m.d_new, hs, n * sizeof(int32_t), hipMemcpyHostToDevice, m.aux));
+  HIPCHK(launch_node_flows(m.v, m.d_new, n, m.d_flows, nullptr, m.aux));
+  HIPCHK(launch_gather_solutions(m.v, m.d_new, n, (int)ni, m.d_sols, m.aux));
+  HIPCHK(hipMemcpyAsync(m.h_flows, m.d_flows, cnt * sizeof(float), hipMemcpyDeviceToHost, m.aux));
+  HIPCHK(hipMemcpyAsync(m.h_sols, m.d_sols, (size_t)n * ni * sizeof(double), hipMemcpyDeviceToHost, m.aux));
+  HIPCHK(hipStreamSynchronize(m.aux));
+  std::memcpy(flows_out, m.h_flows, cnt * sizeof(float));
+  std::memcpy(z_out, m.h_sols, sizeof(double) * n * ni);
+  return NEP_OK;
+}
+
 int nep_lp_get_solution(void *model, int32_t slot, double *z_int, float *x_dense) {
   if (!model) return fail(NEP_ERR_ARG, "null model");
   Model &m = *static_cast<Model *>(model);

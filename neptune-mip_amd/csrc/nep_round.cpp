@@ -51,32 +51,47 @@ void open_in_order(int N, const std::vector<int> &ks, const std::vector<double> 
   }
 }
 
-}  // namespace
+// the part of a rounding every mode shares: c from the node's fixings, the node memories they use, the closed
+// placements, and the LP's near-integral placements opened (largest c first).  0: the fixings alone overfill a node
+struct RoundPrefix {
+  std::vector<double> c, used, room, tot;
+  std::vector<char> closed;
+};
 
-extern "C" int nep_round_leaf(int32_t F, int32_t N, const double *c_fix, const double *n_fix, const float *flow,
-                              const double *zc, const double *fn_mem, const double *node_mem, int32_t by_flow,
-                              double flow_threshold, double *c_out, double *n_out) {
-  if (F <= 0 || N <= 0 || !c_fix || !flow || !fn_mem || !node_mem || !c_out) return NEP_ERR_ARG;
+int round_prefix(int32_t F, int32_t N, const double *c_fix, const double *n_fix, const double *zc, const double *fn_mem,
+                 const double *node_mem, RoundPrefix &r) {
+  const size_t FN = (size_t)F * N;
+  r.c.assign(FN, 0.0);
+  r.used.assign(N, 0.0);
+  r.room.resize(N);
+  r.tot.resize(N);
+  for (size_t k = 0; k < FN; ++k) r.c[k] = c_fix[k] > 0.5 ? 1.0 : 0.0;
+  for (int j = 0; j < N; ++j) r.room[j] = node_mem[j] + 1e-9;
+  for (int f = 0; f < F; ++f)
+    for (int j = 0; j < N; ++j) r.used[j] += fn_mem[f] * r.c[(size_t)f * N + j];
+  for (int j = 0; j < N; ++j)
+    if (r.used[j] > r.room[j]) return 0;
+  r.closed.resize(FN);
+  for (size_t k = 0; k < FN; ++k) r.closed[k] = c_fix[k] >= 0 || (n_fix && n_fix[k % N] == 0.0);
+  // the LP's near-integral placements first, largest c first
+  std::vector<int> ks;
+  std::vector<double> key;
+  for (size_t k = 0; k < FN; ++k)
+    if (!r.closed[k] && (zc ? zc[k] : 0.0) >= 0.5) { ks.push_back((int)k); key.push_back(zc[k]); }
+  open_in_order(N, ks, key, fn_mem, r.room, r.used, r.c, r.tot);
+  return 1;
+}
+
+// one mode from the shared prefix (r is this mode's copy): by flow above the threshold, then a destination for every
+// function left without one, then n
+int round_finish(int32_t F, int32_t N, const double *c_fix, const double *n_fix, const float *flow, const double *zc,
+                 const double *fn_mem, int32_t by_flow, double flow_threshold, RoundPrefix &r, double *c_out,
+                 double *n_out) {
   const double NINF = -std::numeric_limits<double>::infinity();
   const size_t FN = (size_t)F * N;
-  std::vector<double> c(FN, 0.0), used(N, 0.0), room(N), tot(N);
-  for (size_t k = 0; k < FN; ++k) c[k] = c_fix[k] > 0.5 ? 1.0 : 0.0;
-  for (int j = 0; j < N; ++j) room[j] = node_mem[j] + 1e-9;
-  for (int f = 0; f < F; ++f)
-    for (int j = 0; j < N; ++j) used[j] += fn_mem[f] * c[(size_t)f * N + j];
-  for (int j = 0; j < N; ++j)
-    if (used[j] > room[j]) return 0;
-  std::vector<char> closed(FN);
-  for (size_t k = 0; k < FN; ++k) closed[k] = c_fix[k] >= 0 || (n_fix && n_fix[k % N] == 0.0);
+  std::vector<double> &c = r.c, &used = r.used, &room = r.room, &tot = r.tot;
+  const std::vector<char> &closed = r.closed;
   auto zcv = [&](size_t k) { return zc ? zc[k] : 0.0; };
-  // the LP's near-integral placements first, largest c first
-  {
-    std::vector<int> ks;
-    std::vector<double> key;
-    for (size_t k = 0; k < FN; ++k)
-      if (!closed[k] && zcv(k) >= 0.5) { ks.push_back((int)k); key.push_back(zcv(k)); }
-    open_in_order(N, ks, key, fn_mem, room, used, c, tot);
-  }
   if (by_flow) {
     std::vector<int> ks;
     std::vector<double> key;
@@ -150,16 +165,33 @@ extern "C" int nep_round_leaf(int32_t F, int32_t N, const double *c_fix, const d
   return 1;
 }
 
+}  // namespace
+
+extern "C" int nep_round_leaf(int32_t F, int32_t N, const double *c_fix, const double *n_fix, const float *flow,
+                              const double *zc, const double *fn_mem, const double *node_mem, int32_t by_flow,
+                              double flow_threshold, double *c_out, double *n_out) {
+  if (F <= 0 || N <= 0 || !c_fix || !flow || !fn_mem || !node_mem || !c_out) return NEP_ERR_ARG;
+  RoundPrefix r;
+  if (!round_prefix(F, N, c_fix, n_fix, zc, fn_mem, node_mem, r)) return 0;
+  return round_finish(F, N, c_fix, n_fix, flow, zc, fn_mem, by_flow, flow_threshold, r, c_out, n_out);
+}
+
 extern "C" int nep_round_leaves(int32_t F, int32_t N, const double *c_fix, const double *n_fix, const float *flow,
                                 const double *zc, const double *fn_mem, const double *node_mem, int32_t modes,
                                 const int32_t *by_flow, const double *flow_threshold, double *c_out, double *n_out,
                                 int32_t *found) {
   if (modes < 0 || (modes > 0 && (!by_flow || !flow_threshold || !c_out || !found))) return NEP_ERR_ARG;
+  if (modes == 0) return NEP_OK;
+  if (F <= 0 || N <= 0 || !c_fix || !flow || !fn_mem || !node_mem) return NEP_ERR_ARG;
+  // the modes share the prefix (fixings, near-integral placements): computed once, copied per mode
+  RoundPrefix pre, r;
+  const int ok = round_prefix(F, N, c_fix, n_fix, zc, fn_mem, node_mem, pre);
   for (int k = 0; k < modes; ++k) {
-    const int rc = nep_round_leaf(F, N, c_fix, n_fix, flow, zc, fn_mem, node_mem, by_flow[k], flow_threshold[k],
-                                  c_out + (size_t)k * F * N, n_out ? n_out + (size_t)k * N : nullptr);
-    if (rc < 0) return rc;
-    found[k] = rc;
+    found[k] = 0;
+    if (!ok) continue;
+    r = pre;
+    found[k] = round_finish(F, N, c_fix, n_fix, flow, zc, fn_mem, by_flow[k], flow_threshold[k], r,
+                            c_out + (size_t)k * F * N, n_out ? n_out + (size_t)k * N : nullptr);
   }
   return NEP_OK;
 }

@@ -120,6 +120,9 @@ def test_copy_states_equals_copies_in_order():
             z, _ = m.solution(sl, dense_x=False)
             d = m.diag(sl)
             got.append((sl, z.tobytes(), m.rows(sl)[0].tobytes(), d["omega"], d["k"]))
+        if batched:   # (nep_lp_get_flows_solutions: the two reads of the tree's branching nodes in one round trip)
+            fl, z = m.flows_solutions([5, 0, 2])
+            assert np.array_equal(fl, m.flows([5, 0, 2])) and np.array_equal(z, m.solutions([5, 0, 2]))
         states.append(got)
         m.close()
     # the chain's expected sources: 0 <- 1, 2 <- 0 (via 3, 4), 3 <- 0, 4 <- 0, 5 <- 2
