@@ -77,9 +77,10 @@ def test_native_search_host_share(n, f, seconds):
         assert r.objective is not None and math.isfinite(r.bound) and r.bound <= r.objective + 1e-9
     # host seconds per node LP: at 64x32, where the per-LP Python work was the host's time, the native loop's is
     # below the Python loop's (at 256x128 both are the native submit / rounding / device reads: equal within noise).
-    # The host SHARE depends on how fast the LPs converge (DESIGN.md §7 "Native tree search"): below 0.35 here
+    # The host SHARE depends on how fast the LPs converge (DESIGN.md §7 "Native tree search"): 0.242-0.253 measured
+    # at 64x32 over four boxes of round 6 (the round-4 target 0.25; round 5: 0.29) — the bar keeps box-to-box slack
     print(f"host seconds per LP: python {out[False][5] * 1e6:.0f} us, native {out[True][5] * 1e6:.0f} us")
-    assert out[True][0] < 0.35
+    assert out[True][0] < 0.30
     if n <= 64:
         assert out[True][5] < out[False][5]
 
