@@ -48,6 +48,10 @@
 #ifndef NEP_CHECK_WAVES
 #define NEP_CHECK_WAVES 2
 #endif
+// waves per SIMD the plain x_pass (N <= 512) is compiled for (build flag for A/B)
+#ifndef NEP_XPASS_WAVES
+#define NEP_XPASS_WAVES 6
+#endif
 
 namespace nep {
 
@@ -196,7 +200,7 @@ __device__ __forceinline__ void loaded_shift(const DeviceView &v, int slot, int 
 // no restart code (fewer registers live).
 template <int CPL, bool CHECK, bool INIT, bool FIRST, int TW>
 __global__ __launch_bounds__(kWave * TW) __attribute__((amdgpu_waves_per_eu(
-    CHECK ? NEP_CHECK_WAVES : (TW == 16 ? 4 : (CPL >= 8 ? 2 : (CPL >= 4 ? 4 : (NEP_XPASS_PREFETCH ? 5 : 6)))), 8)))
+    CHECK ? NEP_CHECK_WAVES : (TW == 16 ? 4 : (CPL >= 8 ? 2 : (CPL >= 4 ? 4 : (NEP_XPASS_PREFETCH ? 5 : NEP_XPASS_WAVES)))), 8)))
 void x_pass(DeviceView v, const int32_t *__restrict__ slots, int plain, int it, int nslots, int nt_i) {
   const bool nt = nt_i != 0;
   constexpr int E = 4 * CPL;

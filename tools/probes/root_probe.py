@@ -32,7 +32,7 @@ def main():
             os.environ.pop(k, None)
         for kv in filter(None, envs.split(";")):
             k, _, v = kv.partition("=")
-            os.environ[k] = v
+            os.environ[k] = v.replace("/", ",")   # ("/" for "," in values: tools/gpu/run.sh splits arguments on ",")
         m = LPModel(data, "MinDelayAndUtilization", step=1, alpha=alpha, max_batch=2)
         t = time.perf_counter()
         r = m.solve([0], tol=1e-6, max_iters=int(os.environ.get("ROOT_MAX", 400000)), check_every=check)
