@@ -37,8 +37,10 @@ def main():
         t = time.perf_counter()
         r = m.solve([0], tol=1e-6, max_iters=int(os.environ.get("ROOT_MAX", 400000)), check_every=check)
         dt = time.perf_counter() - t
+        d = m.diag(0)
         print(f"{name:10s} {envs:40s} status {int(r['status'][0])} obj {float(r['obj'][0]):.10g} "
-              f"iters {int(r['iters'][0])} {dt:.2f}s", flush=True)
+              f"iters {int(r['iters'][0])} {dt:.2f}s | pobj {d['pobj']:.10g} best bound {d['best_lagr']:.10g} "
+              f"primal residual {d['pres']:.3g} gap {d['gap']:.3g} omega {d['omega']:.3g}", flush=True)
         m.close()
 
 
