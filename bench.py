@@ -102,6 +102,9 @@ def parse(argv=None):
                     help="after the root certifies at --tol, continue it (warm, same slot) until its objective gap "
                          "is below this: the children warm-start from a well-converged root (0 = off)")
     ap.add_argument("--cold", action="store_true", help="cold-start every node LP")
+    ap.add_argument("--leaf-start", default="parent", choices=("parent", "root", "cold"),
+                    help="(A/B) where a replayed rounding leaf starts: its branching node's state (default), the "
+                         "root's, or cold")
     ap.add_argument("--stream", default="auto", choices=("auto", "replay", "children"),
                     help="the timed node-LP stream: the product B&B's recorded nodes (replay, tests/golden/"
                          "bnb_trace_<N>x<F>_s<seed>.json.gz) or root children with --fix random fixings; auto: "
@@ -552,9 +555,12 @@ class ReplayStream:
                 if p is not None:
                     pkey = (name, (rep, p))
             warm_parent = pkey in self.where
-            if warm_parent:
+            leaf_start = getattr(a, "leaf_start", "parent") if e["kind"] == "leaf" else "parent"
+            if warm_parent and leaf_start == "parent":
                 src = self.where[pkey]
                 self.warm_parent += 1
+            else:
+                warm_parent = False
             m.copy_state(src, slot)
             lb, ub = self._box(m, e)
             self.counter += 1
@@ -566,7 +572,7 @@ class ReplayStream:
             wf, wc = a.warm_omega_floor, 0.0
             if "open" in e and getattr(a, "leaf_omega", ""):
                 wf, wc = (float(t) for t in a.leaf_omega.split(":"))
-            st = m.submit([slot], lb[None], ub[None], tol=a.tol, check_every=a.check_every, warm_start=True,
+            st = m.submit([slot], lb[None], ub[None], tol=a.tol, check_every=a.check_every, warm_start=leaf_start != "cold",
                           warm_omega_floor=wf, warm_omega_cap=wc, polish_after=getattr(a, "polish_after", 0.0), **kw)
             if int(st[0]) == LP_INFEASIBLE:
                 self.done.append((LP_INFEASIBLE, float("inf"), float("nan"), 0))
