@@ -68,7 +68,10 @@ NEP_HD inline void dred_interval(double sigma4, double la, double ua, double ld,
 // The Halpern anchor is always a point on the routing simplexes (it is set right after a plain
 // PDHG step, or from the initial projection), so its rows are sparse: a row keeps up to kAnchorK
 // (destination, value) pairs, 8 B each, instead of NP floats.
-constexpr int kAnchorK = 16;
+#ifndef NEP_ANCHOR_K
+#define NEP_ANCHOR_K 16
+#endif
+constexpr int kAnchorK = NEP_ANCHOR_K;   // (build flag for A/B)
 constexpr int kAnchorDense = kAnchorK + 1;
 struct AnchorEnt {
   int32_t j;
