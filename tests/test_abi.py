@@ -42,6 +42,19 @@ def test_bad_arguments_fail_loudly():
         lp.debug_build(data, 7)
 
 
+def test_api12_entries_reject_null_model():
+    """The round-6 entry points (nep_lp_submit_ex, nep_lp_copy_states, nep_lp_get_flows_solutions,
+    nep_debug_sparse_rows) return NEP_ERR_ARG with a message for a null model, before any device work."""
+    from core.engine import lp
+    lib = lp.load_library()
+    for name, args in (("nep_lp_submit_ex", (None, 1, None, None, None, None, None, None, None)),
+                       ("nep_lp_copy_states", (None, 1, None, None)),
+                       ("nep_lp_get_flows_solutions", (None, 1, None, None, None)),
+                       ("nep_debug_sparse_rows", (None, 0, None, None))):
+        assert getattr(lib, name)(*args) == -1, name
+        assert lib.nep_last_error(), name
+
+
 CASES = lp_cases(max_vars=2000)
 
 
