@@ -1,5 +1,6 @@
-"""The whole NEPTUNE flow on the GPU at BASELINE config 2's and 3's sizes: the reference's
-orchestration (core/solvers/neptune/neptune.py:18-39 — step 1, max_score = its objective, step-2 delete, and
+"""The whole NEPTUNE flow on the GPU at BASELINE config 2's, 3's and 4's sizes (VERDICT r4 item 6, r5 missing #3):
+the reference's orchestration (core/solvers/neptune/neptune.py:18-39 — step 1, max_score = its objective, step-2
+delete, and
 create when delete does not end OPTIMAL) through the product's NeptuneMinDelayAndUtilization, every step's
 branch-and-bound time-limited.  Checked on the host in fp64 against the reference's own rows:
   * step 1's placement meets every step-1 row (constraints_step1.py) and its score is the MDU objective of it
@@ -57,7 +58,7 @@ def _alloc_set(data, z, F, N):
     return {(data.functions[k], data.nodes[j]) for k, j in zip(*np.nonzero(c))}
 
 
-@pytest.mark.parametrize("n,f,seconds", [(64, 32, 20.0), (256, 128, 40.0), (1024, 512, 45.0)])
+@pytest.mark.parametrize("n,f,seconds", [(64, 32, 20.0), (256, 128, 40.0), (512, 256, 45.0), (1024, 512, 45.0)])
 def test_neptune_mdu_flow_end_to_end(n, f, seconds):
     """BASELINE config 5's shape (Alibaba trace: W == 0, D = 1 - I, 0.6 % of (f, j) pre-allocated) at config 2's,
     3's and its own size (1024 x 512, the whole neptune.py:18-39 orchestration on one GPU): step 2 is feasible (the published Alibaba flow: delete infeasible, create places every function
@@ -88,7 +89,7 @@ def test_neptune_mdu_flow_end_to_end(n, f, seconds):
             assert abs(obj2 - score["step2"]) <= 1e-6 * max(1.0, abs(score["step2"])), (obj2, score)
 
 
-@pytest.mark.parametrize("n,f,seconds", [(64, 32, 15.0), (256, 128, 30.0)])
+@pytest.mark.parametrize("n,f,seconds", [(64, 32, 15.0), (256, 128, 30.0), (512, 256, 45.0)])
 def test_neptune_mdu_flow_synthetic_generator(n, f, seconds):
     """The SURVEY §8(d) generator: its step-2 score row (constraints_step2.py:76-88, delays normalised by
     max(1000, max_k D[k, i]), not by step 1's MWD: SURVEY Appendix B #5) admits no placement within 1.3 x the
