@@ -13,6 +13,7 @@
 #   profile        rocprofv3 --kernel-trace --stats over the bench's timed replay -> kernel_stats_by_slots.csv
 #   traffic        separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over tools/traffic.py -> traffic.json
 #   sq             SQ wave / wait / VALU counters of the steady x_pass -> sq.json
+#   sq2            SQ LDS wait / bank-conflict / VMEM-read cycle counters of the steady x_pass -> sq2.json
 #   probe:<args>   tools/probes/step2_probe.py <args, comma-separated>
 #   kprof:<name>,<args>  rocprofv3 --kernel-trace --stats over a dev probe -> kprof_<name>.csv
 #   py:<name>,<args>  a dev probe: python tools/probe.py <name> <args> (tools/probes/<name>.py), or a tools/*.py
@@ -62,6 +63,11 @@ for r in "$@"; do
       step "kprof_$n" 600 rocprofv3 --kernel-trace --stats -d /tmp/kprof_$n -o run -- python3 tools/probe.py ${a//,/ }
       cp /tmp/kprof_$n/*/*stats.csv "$O/" 2>/dev/null; python3 tools/prof_summary.py /tmp/kprof_$n > "$O/kprof_$n.csv"
       head -12 "$O/kprof_$n.csv" | cut -c1-160 ;;
+    sq2)
+      export ROC_AQL_QUEUE_SIZE=65536
+      # LDS waits beside the memory waits of the steady x_pass (round 6: is the row loop waiting on LDS?)
+      step pmc_sq2 240 rocprofv3 --kernel-include-regex x_pass --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INST_CYCLES_VMEM_RD -d /tmp/pmc_sq2 -o run -- python3 tools/traffic.py run cold
+      python3 tools/traffic.py sq /tmp/pmc_sq2 > "$O/sq2.json"; cat "$O/sq2.json" ;;
     probe:*) a=${r#probe:}; step probe 600 python -u tools/probe.py step2_probe ${a//,/ } ;;
     py:*) a=${r#py:}; n=${a%%,*}; n=${n%.py}; npy=$((npy + 1))
       if [ -f "tools/probes/$n.py" ]; then step "py${npy}_$n" 600 python -u tools/probe.py ${a//,/ }
