@@ -36,12 +36,15 @@
 #ifndef NEP_INLINE_REFLECT
 #define NEP_INLINE_REFLECT 0
 #endif
-// NEP_XPASS_PREFETCH (A/B build flag, default off): the plain x_pass loads each wave's NEXT routing row (x and its
-// delay row) into registers while it projects the current one (one row ahead; 16 more VGPRs at CPL 2, 5 waves per
-// SIMD instead of 6).  Round 1 measured a register prefetch slower (0.591 vs 0.575 ms per launch) before the LDS
-// accumulators freed 32 VGPRs; this flag re-measures it
+// NEP_XPASS_PREFETCH: the plain x_pass (rows of 257..512 destinations) loads each wave's NEXT routing row into
+// registers while it works on the current one (5 waves per SIMD instead of 6).  1: the next row's x and delay row go
+// out before the projection — measured slower (0.575 vs 0.545 ms per 29-slot launch, round 6; round 1 likewise).
+// 2 (default since round 6): every load of the next row goes out after the projection and before the current row's
+// stores, so no row waits for the previous row's stores to be acknowledged (the vector-memory counter counts stores,
+// in order): 0.484 vs 0.512 ms per 32-slot launch on the whole-trace replay, the same iterations.
+// 0: no prefetch (6 waves).
 #ifndef NEP_XPASS_PREFETCH
-#define NEP_XPASS_PREFETCH 0
+#define NEP_XPASS_PREFETCH 2
 #endif
 // waves per SIMD the certificate x_pass is compiled for (build flag; 2: 210 VGPRs, no spills; 3: 168 VGPRs
 // with 160 B/lane of spills, matching the 3 workgroups per CU its LDS allows)
@@ -51,6 +54,9 @@
 // waves per SIMD the plain x_pass (N <= 512) is compiled for (build flag for A/B)
 #ifndef NEP_XPASS_WAVES
 #define NEP_XPASS_WAVES 6
+#endif
+#ifndef NEP_XPASS_PF_WAVES   // (the same with a prefetch: its registers cost a wave)
+#define NEP_XPASS_PF_WAVES 5
 #endif
 
 namespace nep {
@@ -200,7 +206,7 @@ __device__ __forceinline__ void loaded_shift(const DeviceView &v, int slot, int 
 // no restart code (fewer registers live).
 template <int CPL, bool CHECK, bool INIT, bool FIRST, int TW>
 __global__ __launch_bounds__(kWave * TW) __attribute__((amdgpu_waves_per_eu(
-    CHECK ? NEP_CHECK_WAVES : (TW == 16 ? 4 : (CPL >= 8 ? 2 : (CPL >= 4 ? 4 : (NEP_XPASS_PREFETCH ? 5 : NEP_XPASS_WAVES)))), 8)))
+    CHECK ? NEP_CHECK_WAVES : (TW == 16 ? 4 : (CPL >= 8 ? 2 : (CPL >= 4 ? 4 : ((NEP_XPASS_PREFETCH && CPL == 2) ? NEP_XPASS_PF_WAVES : NEP_XPASS_WAVES)))), 8)))
 void x_pass(DeviceView v, const int32_t *__restrict__ slots, int plain, int it, int nslots, int nt_i) {
   const bool nt = nt_i != 0;
   constexpr int E = 4 * CPL;
@@ -318,10 +324,35 @@ void x_pass(DeviceView v, const int32_t *__restrict__ slots, int plain, int it, 
   double s_score = 0.0, s_pobj = 0.0, s_lagr = 0.0, s_lagr_r = 0.0, s_lagr0 = 0.0, s_move = 0.0, s_dist = 0.0;
   const double s_empty = (cnt_f == 0 && threadIdx.x == 0) ? (double)nrows : 0.0;
 
-  constexpr bool kPf = NEP_XPASS_PREFETCH && !CHECK;
-  float pfx[E], pfd[E];   // (unused without NEP_XPASS_PREFETCH: removed by the compiler)
+  // (rows of 257..512 destinations only: measured there; wider rows would spill, narrower ones are unmeasured)
+  constexpr bool kPf = NEP_XPASS_PREFETCH && !CHECK && CPL == 2;
+  // NEP_XPASS_PREFETCH == 2 ("late"): every load of the next row — its RowInfo, anchor count and pairs, threshold
+  // hint, x, delay and dense anchor rows — goes out after this row's projection and BEFORE this row's stores, so the
+  // wait for them at the next row's top need not wait for the stores (the vector-memory counter is in order and
+  // counts stores): DESIGN.md §11 "x_pass store latency".  The arithmetic is the default's, value for value.
+  constexpr bool kLate = NEP_XPASS_PREFETCH == 2 && kPf;
+  float pfx[E], pfd[E], pfa[E];   // (unused without NEP_XPASS_PREFETCH: removed by the compiler)
+  RowInfo pri{};
+  int pacn = 0;
+  float pth = 0.f;
+  AnchorEnt pae{0, 0.f};
   auto row_nd = [&](const RowInfo &q) { return q.src >= 0 && (q.wobj != 0.f || q.wsc != 0.f); };
-  if (kPf && wave < nrows) {
+  auto prefetch = [&](int rn) {
+    const RowInfo q = v.rows[rn];
+    int qa = 0;
+    if (need_anchor) qa = NEP_SPARSE_ANCHOR ? __builtin_amdgcn_readfirstlane(acnt[rn]) : kAnchorDense;
+    load_row<CPL>(x + (int64_t)rn * NP, v.D + (int64_t)(q.src < 0 ? 0 : q.src) * NP, xa + (int64_t)rn * NP, row_nd(q),
+                  need_anchor && qa > kAnchorK, nt, lane, NP, pfx, pfd, pfa);
+    AnchorEnt qe{0, 0.f};
+    if (need_anchor && qa <= kAnchorK && lane < qa) qe = aent[(int64_t)rn * kAnchorK + lane];
+    pth = th_row[rn];
+    pri = q;
+    pacn = qa;
+    pae = qe;
+  };
+  if (kLate && wave < nrows) {
+    prefetch(r0 + wave);
+  } else if (kPf && wave < nrows) {
     const RowInfo q = v.rows[r0 + wave];
     float dummy[E];
     load_row<CPL>(x + (int64_t)(r0 + wave) * NP, v.D + (int64_t)(q.src < 0 ? 0 : q.src) * NP, xa, row_nd(q), false, nt,
@@ -329,13 +360,17 @@ void x_pass(DeviceView v, const int32_t *__restrict__ slots, int plain, int it, 
   }
   for (int rr = wave; rr < nrows; rr += TW) {
     const int r = r0 + rr;
-    const RowInfo ri = v.rows[r];
+    const RowInfo ri = kLate ? pri : v.rows[r];
     const bool nd = row_nd(ri);
     float xc[E], dc[E], ac[E];
     // anchor row: kept sparse (<= kAnchorK (j, value) pairs, lanes 0..cnt-1 load one each) or dense
     int acn = 0;
-    if (need_anchor) acn = NEP_SPARSE_ANCHOR ? __builtin_amdgcn_readfirstlane(acnt[r]) : kAnchorDense;
-    if (kPf) {
+    if (kLate) acn = pacn;
+    else if (need_anchor) acn = NEP_SPARSE_ANCHOR ? __builtin_amdgcn_readfirstlane(acnt[r]) : kAnchorDense;
+    if (kLate) {
+#pragma unroll
+      for (int e = 0; e < E; ++e) { xc[e] = pfx[e]; dc[e] = pfd[e]; ac[e] = pfa[e]; }
+    } else if (kPf) {
       // this row came in with the previous one; the next row's loads go out now, ahead of the projection
 #pragma unroll
       for (int e = 0; e < E; ++e) { xc[e] = pfx[e]; dc[e] = pfd[e]; ac[e] = 0.f; }
@@ -357,7 +392,8 @@ void x_pass(DeviceView v, const int32_t *__restrict__ slots, int plain, int it, 
     }
     if (need_anchor && acn <= kAnchorK) {
       AnchorEnt ae{0, 0.f};
-      if (lane < acn) ae = aent[(int64_t)r * kAnchorK + lane];
+      if (kLate) ae = pae;
+      else if (lane < acn) ae = aent[(int64_t)r * kAnchorK + lane];
       // scatter the pairs into the lanes that own their destinations (ac is zero from load_row)
       // (destination j lives in lane (j >> 2) & 63, register 4 * (j >> 8) + (j & 3): see load_row)
       for (int k = 0; k < acn; ++k) {
@@ -432,7 +468,7 @@ void x_pass(DeviceView v, const int32_t *__restrict__ slots, int plain, int it, 
       // root from either side, f being convex), and the support usually stops changing one pass
       // later.  Cold rows start from -inf (S = sum of all allowed values, c = cnt_f).  Either way
       // the loop ends on the same exact (S* - 1) / |S*|, so the start only changes the pass count.
-      const float th0 = th_row[r];
+      const float th0 = kLate ? pth : th_row[r];
       float lo_s = 0.f;
       int lo_c = 0;
       if (!INIT && th0 > -INFINITY && th0 < INFINITY) {   // false for NaN (no hint yet)
@@ -475,6 +511,7 @@ void x_pass(DeviceView v, const int32_t *__restrict__ slots, int plain, int it, 
         }
       }
     }
+    if (kLate && rr + TW < nrows) prefetch(r + TW);   // (before this row's first store)
     if (lane == 0) th_row[r] = theta;
     float xn[E];
     if (CHECK && cnt_f > 0) {
