@@ -36,7 +36,7 @@
 #ifndef NEP_INLINE_REFLECT
 #define NEP_INLINE_REFLECT 0
 #endif
-// NEP_XPASS_PREFETCH: the plain x_pass (rows of 257..512 destinations) loads each wave's NEXT routing row into
+// NEP_XPASS_PREFETCH: the plain x_pass (rows of up to 512 destinations) loads each wave's NEXT routing row into
 // registers while it works on the current one (5 waves per SIMD instead of 6).  1: the next row's x and delay row go
 // out before the projection — measured slower (0.575 vs 0.545 ms per 29-slot launch, round 6; round 1 likewise).
 // 2 (default since round 6): every load of the next row goes out after the projection and before the current row's
@@ -57,6 +57,9 @@
 #endif
 #ifndef NEP_XPASS_PF_WAVES   // (the same with a prefetch: its registers cost a wave)
 #define NEP_XPASS_PF_WAVES 5
+#endif
+#ifndef NEP_XPASS_PF_CPL1    // (the prefetch for rows of <= 256 destinations too: 256x128 product search, 20 s:
+#define NEP_XPASS_PF_CPL1 1  //  9166 vs 8814 node LPs, the same incumbent and bound)
 #endif
 
 namespace nep {
@@ -206,7 +209,7 @@ __device__ __forceinline__ void loaded_shift(const DeviceView &v, int slot, int 
 // no restart code (fewer registers live).
 template <int CPL, bool CHECK, bool INIT, bool FIRST, int TW>
 __global__ __launch_bounds__(kWave * TW) __attribute__((amdgpu_waves_per_eu(
-    CHECK ? NEP_CHECK_WAVES : (TW == 16 ? 4 : (CPL >= 8 ? 2 : (CPL >= 4 ? 4 : ((NEP_XPASS_PREFETCH && CPL == 2) ? NEP_XPASS_PF_WAVES : NEP_XPASS_WAVES)))), 8)))
+    CHECK ? NEP_CHECK_WAVES : (TW == 16 ? 4 : (CPL >= 8 ? 2 : (CPL >= 4 ? 4 : ((NEP_XPASS_PREFETCH && (CPL == 2 || (NEP_XPASS_PF_CPL1 && CPL == 1))) ? NEP_XPASS_PF_WAVES : NEP_XPASS_WAVES)))), 8)))
 void x_pass(DeviceView v, const int32_t *__restrict__ slots, int plain, int it, int nslots, int nt_i) {
   const bool nt = nt_i != 0;
   constexpr int E = 4 * CPL;
@@ -324,8 +327,8 @@ void x_pass(DeviceView v, const int32_t *__restrict__ slots, int plain, int it, 
   double s_score = 0.0, s_pobj = 0.0, s_lagr = 0.0, s_lagr_r = 0.0, s_lagr0 = 0.0, s_move = 0.0, s_dist = 0.0;
   const double s_empty = (cnt_f == 0 && threadIdx.x == 0) ? (double)nrows : 0.0;
 
-  // (rows of 257..512 destinations only: measured there; wider rows would spill, narrower ones are unmeasured)
-  constexpr bool kPf = NEP_XPASS_PREFETCH && !CHECK && CPL == 2;
+  // (rows of up to 512 destinations: wider ones would spill)
+  constexpr bool kPf = NEP_XPASS_PREFETCH && !CHECK && (CPL == 2 || (NEP_XPASS_PF_CPL1 && CPL == 1));
   // NEP_XPASS_PREFETCH == 2 ("late"): every load of the next row — its RowInfo, anchor count and pairs, threshold
   // hint, x, delay and dense anchor rows — goes out after this row's projection and BEFORE this row's stores, so the
   // wait for them at the next row's top need not wait for the stores (the vector-memory counter is in order and
