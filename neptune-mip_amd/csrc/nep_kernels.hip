@@ -58,6 +58,9 @@
 #ifndef NEP_XPASS_PF_WAVES   // (the same with a prefetch: its registers cost a wave)
 #define NEP_XPASS_PF_WAVES 5
 #endif
+#ifndef NEP_XPASS_PF_ANCHOR  // (0, default: the late prefetch leaves a dense anchor row to the row's top — 90 instead
+#define NEP_XPASS_PF_ANCHOR 0  //  of 96 VGPRs, 0.4955 vs 0.5044 ms per 32-slot launch; 1: prefetched with the rest)
+#endif
 #ifndef NEP_XPASS_PF_CPL1    // (the prefetch for rows of <= 256 destinations too: 256x128 product search, 20 s:
 #define NEP_XPASS_PF_CPL1 1  //  9166 vs 8814 node LPs, the same incumbent and bound)
 #endif
@@ -345,7 +348,7 @@ void x_pass(DeviceView v, const int32_t *__restrict__ slots, int plain, int it, 
     int qa = 0;
     if (need_anchor) qa = NEP_SPARSE_ANCHOR ? __builtin_amdgcn_readfirstlane(acnt[rn]) : kAnchorDense;
     load_row<CPL>(x + (int64_t)rn * NP, v.D + (int64_t)(q.src < 0 ? 0 : q.src) * NP, xa + (int64_t)rn * NP, row_nd(q),
-                  need_anchor && qa > kAnchorK, nt, lane, NP, pfx, pfd, pfa);
+                  NEP_XPASS_PF_ANCHOR && need_anchor && qa > kAnchorK, nt, lane, NP, pfx, pfd, pfa);
     AnchorEnt qe{0, 0.f};
     if (need_anchor && qa <= kAnchorK && lane < qa) qe = aent[(int64_t)rn * kAnchorK + lane];
     pth = th_row[rn];
@@ -372,7 +375,11 @@ void x_pass(DeviceView v, const int32_t *__restrict__ slots, int plain, int it, 
     else if (need_anchor) acn = NEP_SPARSE_ANCHOR ? __builtin_amdgcn_readfirstlane(acnt[r]) : kAnchorDense;
     if (kLate) {
 #pragma unroll
-      for (int e = 0; e < E; ++e) { xc[e] = pfx[e]; dc[e] = pfd[e]; ac[e] = pfa[e]; }
+      for (int e = 0; e < E; ++e) { xc[e] = pfx[e]; dc[e] = pfd[e]; ac[e] = NEP_XPASS_PF_ANCHOR ? pfa[e] : 0.f; }
+      if (!NEP_XPASS_PF_ANCHOR && need_anchor && acn > kAnchorK) {   // (A/B: the dense anchor loaded here instead)
+        float d0[E], d1[E];
+        load_row<CPL>(xa + (int64_t)r * NP, v.D, xa + (int64_t)r * NP, false, false, nt, lane, NP, ac, d0, d1);
+      }
     } else if (kPf) {
       // this row came in with the previous one; the next row's loads go out now, ahead of the projection
 #pragma unroll
