@@ -212,7 +212,7 @@ __device__ __forceinline__ void loaded_shift(const DeviceView &v, int slot, int 
 // no restart code (fewer registers live).
 template <int CPL, bool CHECK, bool INIT, bool FIRST, int TW>
 __global__ __launch_bounds__(kWave * TW) __attribute__((amdgpu_waves_per_eu(
-    CHECK ? NEP_CHECK_WAVES : (TW == 16 ? 4 : (CPL >= 8 ? 2 : (CPL >= 4 ? 4 : ((NEP_XPASS_PREFETCH && (CPL == 2 || (NEP_XPASS_PF_CPL1 && CPL == 1))) ? NEP_XPASS_PF_WAVES : NEP_XPASS_WAVES)))), 8)))
+    CHECK ? NEP_CHECK_WAVES : (TW == 16 ? 4 : (CPL >= 8 ? 2 : (CPL >= 4 ? 4 : ((NEP_XPASS_PREFETCH && !FIRST && (CPL == 2 || (NEP_XPASS_PF_CPL1 && CPL == 1))) ? NEP_XPASS_PF_WAVES : NEP_XPASS_WAVES)))), 8)))
 void x_pass(DeviceView v, const int32_t *__restrict__ slots, int plain, int it, int nslots, int nt_i) {
   const bool nt = nt_i != 0;
   constexpr int E = 4 * CPL;
@@ -331,7 +331,8 @@ void x_pass(DeviceView v, const int32_t *__restrict__ slots, int plain, int it, 
   const double s_empty = (cnt_f == 0 && threadIdx.x == 0) ? (double)nrows : 0.0;
 
   // (rows of up to 512 destinations: wider ones would spill)
-  constexpr bool kPf = NEP_XPASS_PREFETCH && !CHECK && (CPL == 2 || (NEP_XPASS_PF_CPL1 && CPL == 1));
+  // (not the block's first iteration either: its restart code with the prefetch spills 41 VGPRs, 0.85 vs 0.57 ms)
+  constexpr bool kPf = NEP_XPASS_PREFETCH && !CHECK && !FIRST && (CPL == 2 || (NEP_XPASS_PF_CPL1 && CPL == 1));
   // NEP_XPASS_PREFETCH == 2 ("late"): every load of the next row — its RowInfo, anchor count and pairs, threshold
   // hint, x, delay and dense anchor rows — goes out after this row's projection and BEFORE this row's stores, so the
   // wait for them at the next row's top need not wait for the stores (the vector-memory counter is in order and
